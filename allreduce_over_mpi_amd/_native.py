@@ -1,0 +1,229 @@
+"""ctypes binding of ``libflexar.so`` (the native runtime; see csrc/include/flexar/flexar.h).
+
+The library is loaded from the package's in-tree ``_lib/`` directory (built by
+``_build.build()``), never from site-packages, so the GPU box loads exactly the
+code object compiled here. ``import torch`` happens first so the HIP runtime
+already mapped by torch (same soname ``libamdhip64.so.7``) is the one the
+library binds to — one HIP runtime per process.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+from . import _build
+
+_lock = threading.Lock()
+_lib = None
+
+DTYPES = {
+    "float32": 0, "float16": 1, "bfloat16": 2, "float64": 3, "fp8_e4m3": 4, "fp8_e5m2": 5,
+    "int8": 6, "uint8": 7, "int16": 8, "uint16": 9, "int32": 10, "uint32": 11, "int64": 12,
+    "uint64": 13, "bool": 14,
+}
+OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "avg": 4, "band": 5, "bor": 6, "bxor": 7}
+ERRORS = {0: "ok", 1: "invalid", 2: "unsupported", 3: "hip", 4: "timeout", 5: "state", 6: "nomem", 7: "rccl"}
+
+
+class FlexarError(RuntimeError):
+    def __init__(self, rc: int, msg: str):
+        super().__init__(f"flexar error {rc} ({ERRORS.get(rc, '?')}): {msg}")
+        self.rc = rc
+
+
+def _sig(lib):
+    c = ctypes
+    vp, sz, i, f, d, cp = c.c_void_p, c.c_size_t, c.c_int, c.c_float, c.c_double, c.c_char_p
+    u64 = c.c_uint64
+    table = {
+        "flexar_version": (cp, []),
+        "flexar_last_error": (cp, []),
+        "flexar_dtype_size": (sz, [i]),
+        "flexar_comm_create": (i, [i, i, i, sz, c.POINTER(vp)]),
+        "flexar_handle_size": (sz, []),
+        "flexar_comm_export": (i, [vp, vp]),
+        "flexar_comm_connect": (i, [vp, vp]),
+        "flexar_comm_destroy": (i, [vp]),
+        "flexar_comm_rank": (i, [vp]),
+        "flexar_comm_size": (i, [vp]),
+        "flexar_comm_set_algo": (i, [vp, cp]),
+        "flexar_comm_set_grid": (i, [vp, i, i]),
+        "flexar_allreduce": (i, [vp, vp, vp, sz, i, i, vp]),
+        "flexar_allreduce_ex": (i, [vp, vp, vp, sz, i, i, vp, cp, f]),
+        "flexar_comm_check": (i, [vp]),
+        "flexar_comm_describe": (i, [vp, sz, i, cp, sz]),
+        "flexar_group_create": (i, [i, i, sz, c.POINTER(vp)]),
+        "flexar_group_allreduce": (i, [c.POINTER(vp), i, c.POINTER(vp), c.POINTER(vp), sz, i, i, vp, cp, f]),
+        "flexar_reduce": (i, [vp, c.POINTER(vp), i, sz, i, i, f, vp]),
+        "flexar_reduce_host": (i, [vp, c.POINTER(vp), i, sz, i, i, f]),
+        "flexar_parse_ft_topo": (i, [cp, i, cp, sz]),
+        "flexar_count_factorizations": (u64, [i]),
+        "flexar_enumerate_plans": (i, [i, cp, sz]),
+        "flexar_model_cost_us": (d, [cp, i, d]),
+        "flexar_select_plan": (i, [i, d, cp, sz]),
+        "flexar_legacy_cost": (d, [cp, i, d]),
+        "flexar_plan_dump": (i, [cp, i, i, sz, i, cp, sz]),
+        "flexar_simulate": (i, [cp, i, sz, i, i, c.POINTER(vp), c.POINTER(vp), i, i, i, f]),
+    }
+    for name, (res, args) in table.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def lib():
+    """Load (building first if needed) the native library."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            try:
+                import torch  # noqa: F401  (bind to torch's HIP runtime first)
+            except Exception:
+                pass
+            path = _build.LIB_PATH
+            if _build.needs_build() and os.environ.get("FLEXAR_NO_BUILD") != "1":
+                path = _build.build()
+            if not os.path.exists(path):
+                raise FlexarError(5, f"native library missing: {path} (run __graft_entry__.build())")
+            l = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+            _sig(l)
+            _lib = l
+    return _lib
+
+
+def last_error() -> str:
+    return lib().flexar_last_error().decode(errors="replace")
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        raise FlexarError(rc, (what + ": " if what else "") + last_error())
+
+
+def lib_path() -> str:
+    return _build.LIB_PATH
+
+
+def dtype_code(dtype) -> int:
+    """Map a torch dtype / numpy dtype / name to the flexar dtype enum."""
+    name = str(dtype).replace("torch.", "")
+    alias = {"float": "float32", "half": "float16", "double": "float64", "float8_e4m3fn": "fp8_e4m3",
+             "float8_e5m2": "fp8_e5m2", "int": "int32", "long": "int64", "uint8": "uint8"}
+    name = alias.get(name, name)
+    if name not in DTYPES:
+        raise FlexarError(2, f"unsupported dtype {dtype}")
+    return DTYPES[name]
+
+
+def op_code(op) -> int:
+    if isinstance(op, int):
+        return op
+    name = str(op).lower().replace("reduceop.", "").replace("redopttype.", "")
+    alias = {"product": "prod", "average": "avg", "mean": "avg"}
+    name = alias.get(name, name)
+    if name not in OPS:
+        raise FlexarError(2, f"unsupported reduce op {op}")
+    return OPS[name]
+
+
+def _strbuf(n=1 << 16):
+    return ctypes.create_string_buffer(n)
+
+
+def parse_ft_topo(ft_topo: str | None, nranks: int) -> str:
+    b = _strbuf(256)
+    check(lib().flexar_parse_ft_topo((ft_topo or "").encode(), nranks, b, 256), "parse_ft_topo")
+    return b.value.decode()
+
+
+def count_factorizations(n: int) -> int:
+    return int(lib().flexar_count_factorizations(n))
+
+
+def enumerate_plans(nranks: int) -> list[str]:
+    b = _strbuf(1 << 20)
+    check(lib().flexar_enumerate_plans(nranks, b, 1 << 20), "enumerate_plans")
+    return [x for x in b.value.decode().split("\n") if x]
+
+
+def model_cost_us(spec: str, nranks: int, nbytes: float) -> float:
+    v = lib().flexar_model_cost_us(spec.encode(), nranks, float(nbytes))
+    if v < 0:
+        raise FlexarError(1, last_error())
+    return v
+
+
+def select_plan(nranks: int, nbytes: float) -> str:
+    b = _strbuf(256)
+    check(lib().flexar_select_plan(nranks, float(nbytes), b, 256), "select_plan")
+    return b.value.decode()
+
+
+def legacy_cost(widths, nranks: int, chunk: float) -> float:
+    s = ",".join(str(w) for w in widths)
+    return float(lib().flexar_legacy_cost(s.encode(), nranks, float(chunk)))
+
+
+def plan_dump(spec: str, rank: int, nranks: int, count: int, dtype="float32") -> str:
+    b = _strbuf(1 << 22)
+    check(lib().flexar_plan_dump(spec.encode(), rank, nranks, count, dtype_code(dtype), b, 1 << 22), "plan_dump")
+    return b.value.decode()
+
+
+def _ptr_array(ptrs):
+    arr = (ctypes.c_void_p * len(ptrs))()
+    for k, p in enumerate(ptrs):
+        arr[k] = p
+    return arr
+
+
+def simulate(spec: str, inputs, op="sum", grid=2, ncalls=2, in_place=False, scale=1.0):
+    """Run the device op programs on host numpy arrays (one thread per rank x block).
+
+    ``inputs`` is a list of equally shaped contiguous numpy arrays (one per rank).
+    Returns the list of per-rank outputs.
+    """
+    import numpy as np
+
+    n = len(inputs)
+    first = inputs[0]
+    dt = {"float32": "float32", "float64": "float64", "int32": "int32", "int64": "int64", "int8": "int8",
+          "uint8": "uint8", "int16": "int16", "uint16": "uint16", "uint32": "uint32",
+          "uint64": "uint64", "bool": "bool"}.get(str(first.dtype))
+    code = DTYPES[getattr(inputs, "flexar_dtype", None) or dt] if dt else None
+    return _simulate_raw(spec, inputs, code, op, grid, ncalls, in_place, scale, np)
+
+
+def _simulate_raw(spec, inputs, code, op, grid, ncalls, in_place, scale, np):
+    n = len(inputs)
+    ins = [np.ascontiguousarray(x) for x in inputs]
+    outs = [np.empty_like(x) for x in ins]
+    if in_place:
+        for o, x in zip(outs, ins):
+            o[...] = x
+    rc = lib().flexar_simulate(spec.encode(), n, ins[0].size, code, op_code(op),
+                               _ptr_array([x.ctypes.data for x in ins]),
+                               _ptr_array([o.ctypes.data for o in outs]), grid, ncalls, int(in_place), float(scale))
+    check(rc, "simulate")
+    return outs
+
+
+def simulate_typed(spec: str, inputs, dtype: str, op="sum", grid=2, ncalls=2, in_place=False, scale=1.0):
+    """Like simulate() but with an explicit flexar dtype name for raw-bit arrays (bf16/fp16/fp8 as uint16/uint8)."""
+    import numpy as np
+
+    return _simulate_raw(spec, inputs, DTYPES[dtype], op, grid, ncalls, in_place, scale, np)
+
+
+def reduce_host(srcs, op="sum", scale=1.0, dtype: str | None = None):
+    import numpy as np
+
+    srcs = [np.ascontiguousarray(s) for s in srcs]
+    out = np.empty_like(srcs[0])
+    code = DTYPES[dtype] if dtype else dtype_code(srcs[0].dtype)
+    check(lib().flexar_reduce_host(out.ctypes.data, _ptr_array([s.ctypes.data for s in srcs]), len(srcs),
+                                   srcs[0].size, code, op_code(op), float(scale)), "reduce_host")
+    return out

@@ -1,0 +1,162 @@
+/*
+ * flexar — MI355X-native allreduce library (C API).
+ *
+ * Capability parity with the reference's public entry `MPI_Allreduce_FT`
+ * (reference: allreduce_over_mpi/mpi_mod.hpp:1167-1221) and its FT_TOPO
+ * topology selection (mpi_mod.hpp:880-929), re-designed for GPU-resident
+ * buffers moved peer-to-peer over xGMI by CU-issued loads/stores into
+ * IPC-mapped workspaces, with the local reduction fused into the transfer.
+ *
+ * Lifecycle (no MPI dependency — the bootstrap is pluggable):
+ *   flexar_comm_create()  -> allocate workspace/flags on `device`
+ *   flexar_comm_export()  -> opaque handle bytes (IPC handles) of this rank
+ *   <application all-gathers the handle bytes: MPI_Allgather, torch store, ...>
+ *   flexar_comm_connect() -> map every peer's workspace
+ *   flexar_allreduce()    -> stream-ordered, graph-capturable collective
+ *   flexar_comm_destroy()
+ */
+#ifndef FLEXAR_FLEXAR_H
+#define FLEXAR_FLEXAR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FLEXAR_VERSION_MAJOR 0
+#define FLEXAR_VERSION_MINOR 1
+#define FLEXAR_VERSION_PATCH 0
+
+typedef enum {
+  FLEXAR_FLOAT32 = 0,
+  FLEXAR_FLOAT16 = 1,
+  FLEXAR_BFLOAT16 = 2,
+  FLEXAR_FLOAT64 = 3,
+  FLEXAR_FP8_E4M3 = 4, /* OCP e4m3fn (gfx950 native), saturating */
+  FLEXAR_FP8_E5M2 = 5, /* OCP e5m2, saturating */
+  FLEXAR_INT8 = 6,
+  FLEXAR_UINT8 = 7,
+  FLEXAR_INT16 = 8,
+  FLEXAR_UINT16 = 9,
+  FLEXAR_INT32 = 10,
+  FLEXAR_UINT32 = 11,
+  FLEXAR_INT64 = 12,
+  FLEXAR_UINT64 = 13,
+  FLEXAR_BOOL = 14,
+  FLEXAR_NUM_DTYPES = 15
+} flexar_dtype_t;
+
+typedef enum {
+  FLEXAR_SUM = 0,
+  FLEXAR_PROD = 1,
+  FLEXAR_MAX = 2,
+  FLEXAR_MIN = 3,
+  FLEXAR_AVG = 4, /* SUM followed by a fused 1/N post-scale */
+  FLEXAR_BAND = 5,
+  FLEXAR_BOR = 6,
+  FLEXAR_BXOR = 7,
+  FLEXAR_NUM_OPS = 8
+} flexar_op_t;
+
+/* Error codes (0 = success). */
+enum {
+  FLEXAR_OK = 0,
+  FLEXAR_ERR_INVALID = 1,
+  FLEXAR_ERR_UNSUPPORTED = 2,
+  FLEXAR_ERR_HIP = 3,
+  FLEXAR_ERR_TIMEOUT = 4,
+  FLEXAR_ERR_STATE = 5,
+  FLEXAR_ERR_NOMEM = 6,
+  FLEXAR_ERR_RCCL = 7
+};
+
+typedef struct flexar_comm* flexar_comm_t;
+
+/* ---- version / errors ---------------------------------------------------- */
+const char* flexar_version(void);
+const char* flexar_last_error(void); /* thread-local message of the last failure */
+size_t flexar_dtype_size(int dtype);
+
+/* ---- communicator ------------------------------------------------------- */
+/* workspace_bytes: staging capacity (both parities); 0 = default (FLEXAR_WORKSPACE_BYTES or 512 MiB). */
+int flexar_comm_create(int rank, int nranks, int device, size_t workspace_bytes, flexar_comm_t* out);
+size_t flexar_handle_size(void);
+int flexar_comm_export(flexar_comm_t comm, void* handle_out);
+/* all_handles: nranks * flexar_handle_size() bytes, rank-major. */
+int flexar_comm_connect(flexar_comm_t comm, const void* all_handles);
+int flexar_comm_destroy(flexar_comm_t comm);
+int flexar_comm_rank(flexar_comm_t comm);
+int flexar_comm_size(flexar_comm_t comm);
+
+/* Algorithm spec strings:
+ *   "auto"                 cost-model selection (default)
+ *   "ring" | "ring:C"      ring (C channels over link-disjoint Hamiltonian cycles)
+ *   "flat"                 one-stage tree = direct reduce-scatter + all-gather (FT_TOPO unset)
+ *   "rhd"                  tree 2,2,...,2 (recursive halving / doubling)
+ *   "tree:a,b,c"           mixed-radix FlexTree with the given stage widths
+ *   "oneshot"              every rank reduces the full buffer (small messages)
+ *   "ft"                   honour FT_TOPO exactly like the reference (any 1 = ring)
+ * Optional suffixes: "+pull" (all-gather pulls from owners) / "+push" (owners push).
+ */
+int flexar_comm_set_algo(flexar_comm_t comm, const char* spec);
+int flexar_comm_set_grid(flexar_comm_t comm, int grid_blocks, int block_threads); /* 0 = auto */
+
+/* sendbuf == NULL or sendbuf == recvbuf => in place. count is size_t (no 2^31 cap). */
+int flexar_allreduce(flexar_comm_t comm, const void* sendbuf, void* recvbuf, size_t count, int dtype,
+                     int op, void* hip_stream);
+/* Same, with an explicit algorithm spec (NULL = communicator default) and a fused
+ * post-scale applied to the reduced value (1.0f = none; AVG multiplies 1/N on top). */
+int flexar_allreduce_ex(flexar_comm_t comm, const void* sendbuf, void* recvbuf, size_t count, int dtype,
+                        int op, void* hip_stream, const char* algo, float scale);
+/* Non-blocking health check: returns FLEXAR_ERR_TIMEOUT (and fills flexar_last_error)
+ * if a device-side wait timed out in any previous call. */
+int flexar_comm_check(flexar_comm_t comm);
+/* Describe the algorithm the communicator would run for (count, dtype). */
+int flexar_comm_describe(flexar_comm_t comm, size_t count, int dtype, char* buf, size_t buflen);
+
+/* ---- in-process group: nranks ranks on ONE device in ONE process ---------------
+ * Every rank's workgroups run in a single launch (rank = blockIdx / grid), so the
+ * complete multi-rank device protocol (flags, parity, staging, all algorithms) runs
+ * on one GPU without IPC — used by tests and by calibration sweeps. */
+int flexar_group_create(int nranks, int device, size_t workspace_bytes, flexar_comm_t* comms_out);
+int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* ins, void* const* outs, size_t count,
+                           int dtype, int op, void* hip_stream, const char* algo, float scale);
+
+/* ---- standalone device reduction kernel ----------------------------------- */
+/* dst[i] = scale * OP_k srcs[k][i], k < nsrc (1..64), fp32 accumulation for 16/8-bit floats. */
+int flexar_reduce(void* dst, const void* const* srcs, int nsrc, size_t count, int dtype, int op, float scale,
+                  void* hip_stream);
+/* Same on host memory (OpenMP-free vectorised loop) — the CPU path's reduction. */
+int flexar_reduce_host(void* dst, const void* const* srcs, int nsrc, size_t count, int dtype, int op,
+                       float scale);
+
+/* ---- host-only planning utilities (no GPU needed) ------------------------ */
+/* Parse an FT_TOPO string for nranks with the reference's rules (any 1 -> ring, unset -> flat,
+ * product must equal nranks; trailing/duplicate separators tolerated). Writes a canonical spec
+ * ("ring" or "tree:a,b,c") into out. Returns FLEXAR_ERR_INVALID on a bad topology. */
+int flexar_parse_ft_topo(const char* ft_topo, int nranks, char* out, size_t outlen);
+/* Number of ordered factorizations H(n) (reference topo_count/factor_count.py). */
+uint64_t flexar_count_factorizations(int n);
+/* Enumerate candidate plans for nranks as newline separated specs. */
+int flexar_enumerate_plans(int nranks, char* out, size_t outlen);
+/* Cost-model estimate (microseconds) of spec for (nranks, bytes). */
+double flexar_model_cost_us(const char* spec, int nranks, double bytes);
+/* Cost-model choice for (nranks, bytes) written to out. */
+int flexar_select_plan(int nranks, double bytes, char* out, size_t outlen);
+/* Reference cost model (cost_model/CostModel.h) score, fixed: returns the argmin spec and cost. */
+double flexar_legacy_cost(const char* widths_csv, int nranks, double chunk);
+/* Human-readable dump of rank's op program (like Operations::print_ops). */
+int flexar_plan_dump(const char* spec, int rank, int nranks, size_t count, int dtype, char* out, size_t outlen);
+/* Execute the exact op programs the GPU runs, on host memory with one thread per (rank, grid block).
+ * inputs/outputs: nranks host pointers each. in_place: outputs[r] already holds the input.
+ * Returns 0 on success. Used to validate every algorithm/topology without a GPU. */
+int flexar_simulate(const char* spec, int nranks, size_t count, int dtype, int op, const void* const* inputs,
+                    void* const* outputs, int grid, int ncalls, int in_place, float scale);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* FLEXAR_FLEXAR_H */

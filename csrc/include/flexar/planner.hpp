@@ -1,0 +1,418 @@
+// Host-side planner: compiles an AlgoSpec into the per-rank op program
+// (program.hpp) that the gfx950 executor kernel, the host simulator and the
+// host shared-memory engine all run unchanged.
+//
+// Schedules (same mathematics as the reference, different mechanics):
+//  * TREE (FlexTree mixed radix; flat = {N}; RHD = {2,..,2}):
+//      reference Send_Ops/Recv_Ops (mpi_mod.hpp:147-214) + tree_allreduce
+//      (mpi_mod.hpp:952-1111). Stage s, g = prod(w_<s), G = g*w_s: rank r's
+//      group = ranks differing only in mixed-radix digit s; RS sends member p the
+//      blocks k == p (mod G) and reduces the blocks k == r (mod G) with fan-in w_s;
+//      AG replays the stages in reverse.
+//      New: staging slot per (stage, sender digit, block) so a payload lands at
+//      an explicit offset (no tag matching, no global barrier); optional fusion
+//      writes a stage's reduce output straight into the next stage's receiver
+//      and multicasts all-gather blocks to every later-stage member at once.
+//  * RING: reference ring_allreduce (mpi_mod.hpp:1113-1163): N-1 RS steps with
+//      block (v - i) mod N, then N-1 AG steps. New: reduce-and-forward fusion
+//      (the reduced partial is written directly into the right neighbour's
+//      staging) and C arc-disjoint channels so C xGMI links run concurrently.
+//  * ONESHOT: new (small messages): multicast the whole buffer to every peer,
+//      one wait, fan-in-N reduce.
+#pragma once
+
+#include <stdint.h>
+
+#include <algorithm>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "flexar/program.hpp"
+#include "flexar/topology.hpp"
+
+namespace flexar {
+
+struct Program {
+  std::vector<Op> ops;
+  std::vector<uint32_t> chan_start;  // nchan + 1 entries into ops
+  uint32_t nchan = 1;
+  uint64_t stg_elems = 0;            // staging elements needed per parity
+  uint32_t nslots = 0;
+  uint64_t count = 0;
+  uint32_t esize = 0;
+  std::string desc;
+};
+
+class Planner {
+ public:
+  Planner(uint32_t nranks, uint32_t rank, uint64_t count, uint32_t esize, float final_scale)
+      : N(nranks), r(rank), count(count), esize(esize), scale(final_scale) {
+    align = kStageAlignBytes / esize;
+    if (align == 0) align = 1;
+  }
+
+  bool build(const AlgoSpec& spec, Program* P, std::string* err) {
+    prog = P;
+    *P = Program();
+    P->count = count;
+    P->esize = esize;
+    P->chan_start.push_back(0);
+    stg = 0;
+    if (N == 1) {  // reference: memcpy unless in place (mpi_mod.hpp:1181-1188)
+      if (count) xfer(count, {loc(BUF_IN, r, 0)}, {loc(BUF_OUT, r, 0)}, scale);
+      finish_channel();
+      P->desc = "copy";
+    } else if (spec.kind == AlgoKind::RING) {
+      int C = std::max(1, std::min(spec.channels, max_ring_channels(N)));
+      if (2ull * (N - 1) * C > kMaxSlots) { if (err) *err = "too many ring channels"; return false; }
+      build_ring(C);
+      P->desc = spec.str();
+    } else if (spec.kind == AlgoKind::TREE) {
+      long prod = 1;
+      for (int w : spec.widths) prod *= w;
+      if (spec.widths.empty() || prod != (long)N) { if (err) *err = "tree widths do not multiply to N"; return false; }
+      if (2 * spec.widths.size() > kMaxSlots) { if (err) *err = "too many stages"; return false; }
+      for (int w : spec.widths)
+        if (w < 2) { if (err) *err = "tree width < 2"; return false; }
+      build_tree(spec.widths, spec.ag == AgMode::PULL, spec.fuse);
+      P->desc = spec.str();
+    } else if (spec.kind == AlgoKind::ONESHOT) {
+      build_oneshot();
+      P->desc = spec.str();
+    } else {
+      if (err) *err = "planner needs a concrete algorithm (not auto)";
+      return false;
+    }
+    P->stg_elems = stg;
+    P->nchan = (uint32_t)P->chan_start.size() - 1;
+    return true;
+  }
+
+ private:
+  uint32_t N, r;
+  uint64_t count;
+  uint32_t esize;
+  float scale;
+  uint64_t align;
+  uint64_t stg = 0;
+  Program* prog = nullptr;
+
+  static Loc loc(uint16_t buf, uint32_t rank, uint64_t off) {
+    Loc l;
+    l.buf = buf;
+    l.rank = (uint16_t)rank;
+    l.pad = 0;
+    l.off = off;
+    return l;
+  }
+  uint64_t round_up(uint64_t x) const { return (x + align - 1) / align * align; }
+  uint64_t alloc(uint64_t elems) {
+    uint64_t o = stg;
+    stg += round_up(elems);
+    return o;
+  }
+  void finish_channel() { prog->chan_start.push_back((uint32_t)prog->ops.size()); }
+
+  void push(const Op& o) { prog->ops.push_back(o); }
+
+  static Op blank(uint16_t kind) {
+    Op o;
+    memset(&o, 0, sizeof(o));
+    o.kind = kind;
+    o.scale = 1.0f;
+    return o;
+  }
+
+  void sync_op(uint16_t kind, const std::vector<uint32_t>& peers, uint32_t slot) {
+    if (slot + 1 > prog->nslots) prog->nslots = slot + 1;
+    for (size_t i = 0; i < peers.size(); i += kMaxPeersPerOp) {
+      Op o = blank(kind);
+      o.slot = slot;
+      size_t n = std::min<size_t>(kMaxPeersPerOp, peers.size() - i);
+      o.npeers = (uint16_t)n;
+      for (size_t j = 0; j < n; ++j) o.peers[j] = (uint16_t)peers[i + j];
+      if (n) push(o);
+    }
+  }
+  void signal(const std::vector<uint32_t>& peers, uint32_t slot) { sync_op(OP_SIGNAL, peers, slot); }
+  void wait(const std::vector<uint32_t>& peers, uint32_t slot) { sync_op(OP_WAIT, peers, slot); }
+
+  // dsts = scale * OP(srcs). Splits fan-in > kMaxSrc through a local temp and
+  // fan-out > kMaxDst into follow-up copies from the first (local) destination.
+  void xfer(uint64_t len, std::vector<Loc> srcs, std::vector<Loc> dsts, float sc) {
+    if (len == 0 || srcs.empty() || dsts.empty()) return;
+    if (srcs.size() > kMaxSrc) {
+      Loc tmp = loc(BUF_STG, r, alloc(len));
+      std::vector<Loc> first(srcs.begin(), srcs.begin() + kMaxSrc);
+      emit_xfer(len, first, {tmp}, 1.0f);
+      size_t i = kMaxSrc;
+      while (srcs.size() - i > kMaxSrc - 1) {
+        std::vector<Loc> nxt{tmp};
+        nxt.insert(nxt.end(), srcs.begin() + i, srcs.begin() + i + (kMaxSrc - 1));
+        emit_xfer(len, nxt, {tmp}, 1.0f);
+        i += kMaxSrc - 1;
+      }
+      std::vector<Loc> last{tmp};
+      last.insert(last.end(), srcs.begin() + i, srcs.end());
+      srcs = last;
+    }
+    if (dsts.size() > kMaxDst) {
+      // keep a local destination first so the overflow copies read local memory
+      std::stable_partition(dsts.begin(), dsts.end(), [&](const Loc& l) { return l.rank == r; });
+      std::vector<Loc> head(dsts.begin(), dsts.begin() + kMaxDst);
+      emit_xfer(len, srcs, head, sc);
+      Loc from = head[0];
+      for (size_t i = kMaxDst; i < dsts.size(); i += kMaxDst) {
+        std::vector<Loc> more(dsts.begin() + i, dsts.begin() + std::min(dsts.size(), i + kMaxDst));
+        emit_xfer(len, {from}, more, 1.0f);
+      }
+      return;
+    }
+    emit_xfer(len, srcs, dsts, sc);
+  }
+  void emit_xfer(uint64_t len, const std::vector<Loc>& srcs, const std::vector<Loc>& dsts, float sc) {
+    Op o = blank(OP_XFER);
+    o.len = len;
+    o.scale = sc;
+    o.nsrc = (uint8_t)srcs.size();
+    o.ndst = (uint8_t)dsts.size();
+    for (size_t i = 0; i < srcs.size(); ++i) o.src[i] = srcs[i];
+    for (size_t i = 0; i < dsts.size(); ++i) o.dst[i] = dsts[i];
+    push(o);
+  }
+
+  // ------------------------------------------------------------------ ring
+  void build_ring(int C) {
+    // Partition the buffer into C aligned channel ranges.
+    uint64_t per = round_up((count + C - 1) / C);
+    uint32_t slots_per = 2 * (N - 1);
+    for (int c = 0; c < C; ++c) {
+      uint64_t c_off = std::min<uint64_t>(count, (uint64_t)c * per);
+      uint64_t c_cnt = std::min<uint64_t>(count - c_off, per);
+      std::vector<int> ord = ring_order(N, c);
+      uint32_t v = 0;
+      for (uint32_t p = 0; p < N; ++p)
+        if ((uint32_t)ord[p] == r) v = p;
+      uint32_t right = ord[(v + 1) % N], left = ord[(v + N - 1) % N];
+      uint64_t split = round_up((c_cnt + N - 1) / N);
+      auto boff = [&](uint32_t k) { return c_off + (uint64_t)k * split; };
+      auto blen = [&](uint32_t k) -> uint64_t {
+        uint64_t s = (uint64_t)k * split;
+        return s >= c_cnt ? 0 : std::min(split, c_cnt - s);
+      };
+      // Every rank computes the same staging layout (same sequence of allocs).
+      uint64_t base = alloc(2ull * (N - 1) * split);
+      auto rs_off = [&](uint32_t i) { return base + (uint64_t)i * split; };
+      auto ag_off = [&](uint32_t i) { return base + (uint64_t)(N - 1 + i) * split; };
+      uint32_t slot0 = c * slots_per;
+      auto mod = [&](long x) { return (uint32_t)(((x % (long)N) + N) % N); };
+
+      uint32_t b0 = v;
+      xfer(blen(b0), {loc(BUF_IN, r, boff(b0))}, {loc(BUF_STG, right, rs_off(0))}, 1.0f);
+      signal({right}, slot0 + 0);
+      for (uint32_t i = 0; i + 1 < N; ++i) {
+        wait({left}, slot0 + i);
+        uint32_t b = mod((long)v - 1 - (long)i);
+        std::vector<Loc> srcs{loc(BUF_IN, r, boff(b)), loc(BUF_STG, r, rs_off(i))};
+        if (i + 2 < N) {
+          xfer(blen(b), srcs, {loc(BUF_STG, right, rs_off(i + 1))}, 1.0f);
+        } else {  // owned block (v + 1): final value -> OUT and start the all-gather
+          xfer(blen(b), srcs, {loc(BUF_OUT, r, boff(b)), loc(BUF_STG, right, ag_off(0))}, scale);
+        }
+        signal({right}, slot0 + i + 1);
+      }
+      for (uint32_t i = 0; i + 1 < N; ++i) {
+        wait({left}, slot0 + (N - 1) + i);
+        uint32_t b = mod((long)v - (long)i);
+        if (i + 2 < N) {
+          xfer(blen(b), {loc(BUF_STG, r, ag_off(i))}, {loc(BUF_OUT, r, boff(b)), loc(BUF_STG, right, ag_off(i + 1))},
+               1.0f);
+          signal({right}, slot0 + N + i);
+        } else {
+          xfer(blen(b), {loc(BUF_STG, r, ag_off(i))}, {loc(BUF_OUT, r, boff(b))}, 1.0f);
+        }
+      }
+      finish_channel();
+    }
+  }
+
+  // ------------------------------------------------------------------ tree
+  struct Stage {
+    uint32_t w, g, G, base, myj;
+    std::vector<uint32_t> members;  // index j -> rank
+    std::vector<uint32_t> others() const {
+      std::vector<uint32_t> o;
+      for (uint32_t jj = 1; jj < w; ++jj) o.push_back(members[(myj + jj) % w]);  // rotated: spreads links
+      return o;
+    }
+  };
+
+  void build_tree(const std::vector<int>& widths, bool pull, bool fuse) {
+    const uint32_t S = (uint32_t)widths.size();
+    uint64_t split = round_up((count + N - 1) / N);
+    auto blen = [&](uint32_t k) -> uint64_t {
+      uint64_t s = (uint64_t)k * split;
+      return s >= count ? 0 : std::min(split, count - s);
+    };
+    auto boff = [&](uint32_t k) { return (uint64_t)k * split; };
+
+    std::vector<Stage> st(S);
+    uint32_t g = 1;
+    for (uint32_t s = 0; s < S; ++s) {
+      Stage& x = st[s];
+      x.w = widths[s];
+      x.g = g;
+      x.G = g * x.w;
+      x.base = r / x.G * x.G + r % g;
+      x.myj = (r / g) % x.w;
+      for (uint32_t j = 0; j < x.w; ++j) x.members.push_back(x.base + j * g);
+      g = x.G;
+    }
+    auto digit = [&](uint32_t rank, uint32_t s) { return (rank / st[s].g) % st[s].w; };
+    // blocks of member p at stage s: k == p (mod G_s)
+    auto blocks_of = [&](uint32_t p, uint32_t s) {
+      std::vector<uint32_t> b;
+      for (uint32_t k = p % st[s].G; k < N; k += st[s].G) b.push_back(k);
+      return b;
+    };
+    // Staging layout (identical on every rank): rs[s], ag[s] (push) or pub (pull).
+    std::vector<uint64_t> rs_base(S), ag_base(S);
+    for (uint32_t s = 0; s < S; ++s) rs_base[s] = alloc((uint64_t)st[s].w * (N / st[s].G) * split);
+    uint64_t pub_base = 0;
+    if (pull) pub_base = alloc((uint64_t)N * split);
+    else
+      for (uint32_t s = 0; s < S; ++s) ag_base[s] = alloc((uint64_t)st[s].w * (N / st[s].G) * split);
+    auto rs_off = [&](uint32_t s, uint32_t j, uint32_t k) {
+      return rs_base[s] + ((uint64_t)j * (N / st[s].G) + k / st[s].G) * split;
+    };
+    auto ag_off = [&](uint32_t s, uint32_t j, uint32_t k) {
+      return ag_base[s] + ((uint64_t)j * (N / st[s].G) + k / st[s].G) * split;
+    };
+    auto pub_off = [&](uint32_t k) { return pub_base + (uint64_t)k * split; };
+    // rank in stage-s group of `r` that owns block k after stage s
+    auto owner_at = [&](uint32_t k, uint32_t s) { return st[s].base + digit(k, s) * st[s].g; };
+
+    // ---------------- reduce-scatter
+    for (uint32_t s = 0; s < S; ++s) {
+      const Stage& x = st[s];
+      uint16_t cur = (s == 0) ? BUF_IN : BUF_OUT;
+      bool sends_fused = fuse && s > 0;  // previous stage already wrote our sends into the receivers
+      if (!sends_fused) {
+        for (uint32_t p : x.others())
+          for (uint32_t k : blocks_of(p, s))
+            xfer(blen(k), {loc(cur, r, boff(k))}, {loc(BUF_STG, p, rs_off(s, x.myj, k))}, 1.0f);
+      }
+      signal(x.others(), s);
+      wait(x.others(), s);
+      bool last = (s + 1 == S);
+      for (uint32_t k : blocks_of(r, s)) {
+        std::vector<Loc> srcs{loc(cur, r, boff(k))};
+        for (uint32_t jj = 1; jj < x.w; ++jj) {
+          uint32_t j = (x.myj + jj) % x.w;
+          srcs.push_back(loc(BUF_STG, r, rs_off(s, j, k)));
+        }
+        std::vector<Loc> dsts;
+        if (!last) {
+          uint32_t p = owner_at(k, s + 1);
+          if (fuse && p != r) dsts.push_back(loc(BUF_STG, p, rs_off(s + 1, st[s + 1].myj, k)));
+          else dsts.push_back(loc(BUF_OUT, r, boff(k)));
+          xfer(blen(k), srcs, dsts, 1.0f);
+        } else {
+          dsts.push_back(loc(BUF_OUT, r, boff(k)));
+          if (pull) {
+            dsts.push_back(loc(BUF_STG, r, pub_off(k)));
+          } else if (fuse) {  // multicast the final block to every member of every AG stage
+            for (uint32_t t = 0; t < S; ++t)
+              for (uint32_t p : st[t].others()) dsts.push_back(loc(BUF_STG, p, ag_off(t, st[t].myj, k)));
+          }
+          xfer(blen(k), srcs, dsts, scale);
+        }
+      }
+    }
+    // ---------------- all-gather (stages in reverse)
+    for (int si = (int)S - 1; si >= 0; --si) {
+      uint32_t s = (uint32_t)si;
+      const Stage& x = st[s];
+      uint32_t slot = S + s;
+      if (pull) {
+        signal(x.others(), slot);  // my pub holds blocks_of(r, s)
+        wait(x.others(), slot);
+        for (uint32_t p : x.others())
+          for (uint32_t k : blocks_of(p, s)) {
+            std::vector<Loc> dsts{loc(BUF_OUT, r, boff(k))};
+            if (s > 0) dsts.push_back(loc(BUF_STG, r, pub_off(k)));
+            xfer(blen(k), {loc(BUF_STG, p, pub_off(k))}, dsts, 1.0f);
+          }
+      } else {
+        if (!fuse) {
+          for (uint32_t k : blocks_of(r, s)) {
+            std::vector<Loc> dsts;
+            for (uint32_t p : x.others()) dsts.push_back(loc(BUF_STG, p, ag_off(s, x.myj, k)));
+            xfer(blen(k), {loc(BUF_OUT, r, boff(k))}, dsts, 1.0f);
+          }
+        }
+        signal(x.others(), slot);
+        wait(x.others(), slot);
+        for (uint32_t p : x.others()) {
+          uint32_t j = digit(p, s);
+          for (uint32_t k : blocks_of(p, s)) {
+            std::vector<Loc> dsts{loc(BUF_OUT, r, boff(k))};
+            if (fuse)  // forward to every member of every lower AG stage right away
+              for (uint32_t t = 0; t < s; ++t)
+                for (uint32_t q : st[t].others()) dsts.push_back(loc(BUF_STG, q, ag_off(t, st[t].myj, k)));
+            xfer(blen(k), {loc(BUF_STG, r, ag_off(s, j, k))}, dsts, 1.0f);
+          }
+        }
+      }
+    }
+    finish_channel();
+  }
+
+  // ------------------------------------------------------------------ oneshot
+  void build_oneshot() {
+    uint64_t cnt_al = round_up(count);
+    uint64_t base = alloc((uint64_t)N * cnt_al);
+    std::vector<uint32_t> peers;
+    for (uint32_t jj = 1; jj < N; ++jj) peers.push_back((r + jj) % N);
+    std::vector<Loc> dsts;
+    for (uint32_t p : peers) dsts.push_back(loc(BUF_STG, p, base + (uint64_t)r * cnt_al));
+    xfer(count, {loc(BUF_IN, r, 0)}, dsts, 1.0f);
+    signal(peers, 0);
+    wait(peers, 0);
+    std::vector<Loc> srcs{loc(BUF_IN, r, 0)};
+    for (uint32_t p : peers) srcs.push_back(loc(BUF_STG, r, base + (uint64_t)p * cnt_al));
+    xfer(count, srcs, {loc(BUF_OUT, r, 0)}, scale);
+    finish_channel();
+  }
+};
+
+// Human-readable program dump (the reference's Operations::print_ops, mpi_mod.hpp:107-144).
+inline std::string dump_program(const Program& P, uint32_t rank) {
+  static const char* bn[] = {"IN", "OUT", "STG"};
+  std::ostringstream ss;
+  ss << "rank " << rank << " program '" << P.desc << "': " << P.ops.size() << " ops, " << P.nchan
+     << " channel(s), staging " << P.stg_elems << " elems/parity, " << P.nslots << " flag slots\n";
+  for (uint32_t c = 0; c < P.nchan; ++c) {
+    ss << "channel " << c << ":\n";
+    for (uint32_t i = P.chan_start[c]; i < P.chan_start[c + 1]; ++i) {
+      const Op& o = P.ops[i];
+      if (o.kind == OP_XFER) {
+        ss << "  XFER len=" << o.len << (o.scale != 1.0f ? " scale" : "") << " [";
+        for (int k = 0; k < o.nsrc; ++k)
+          ss << (k ? " + " : "") << bn[o.src[k].buf] << "@" << o.src[k].rank << ":" << o.src[k].off;
+        ss << "] -> [";
+        for (int k = 0; k < o.ndst; ++k)
+          ss << (k ? ", " : "") << bn[o.dst[k].buf] << "@" << o.dst[k].rank << ":" << o.dst[k].off;
+        ss << "]\n";
+      } else {
+        ss << (o.kind == OP_SIGNAL ? "  SIGNAL" : "  WAIT  ") << " slot=" << o.slot << " peers=";
+        for (int k = 0; k < o.npeers; ++k) ss << (k ? "," : "") << o.peers[k];
+        ss << "\n";
+      }
+    }
+  }
+  return ss.str();
+}
+
+}  // namespace flexar

@@ -1,0 +1,256 @@
+// Topology / algorithm specs, the FT_TOPO compatibility parser and the plan
+// enumerator.
+//
+// Reference parity:
+//  * get_stages()            allreduce_over_mpi/mpi_mod.hpp:880-929  -> parse_ft_topo()
+//    (unset -> one flat stage {N}; any 1 -> ring; product must equal N).
+//    Defect D4 (trailing separator re-pushes the last token and aborts) is fixed:
+//    empty tokens are ignored. Errors are returned, never exit(1).
+//  * getWidth/_getWidth       cost_model/GetWidth.h:1-47             -> ordered_factorizations()
+//    Defect D11 fixed: the single factorization [N] is a real flat candidate, ring is its own
+//    candidate instead of the "1*N"/"N*1" aliasing.
+//  * get_factor_count         topo_count/factor_count.py:1-15        -> count_factorizations()
+//  * isPrimeNumber / getPrimeFactor  cost_model/IsPrimeNumber.h, GetPrimeFactor.h -> is_prime(), prime_factors()
+#pragma once
+
+#include <stdint.h>
+
+#include <cctype>
+#include <cstdlib>
+#include <sstream>
+#include <string>
+#include <vector>
+
+namespace flexar {
+
+enum class AlgoKind { AUTO, RING, TREE, ONESHOT };
+enum class AgMode { AUTO, PUSH, PULL };
+
+struct AlgoSpec {
+  AlgoKind kind = AlgoKind::AUTO;
+  std::vector<int> widths;  // TREE stage widths, product == nranks
+  int channels = 1;         // RING: number of arc-disjoint rings
+  AgMode ag = AgMode::AUTO; // TREE: all-gather direction
+  bool fuse = true;         // fuse reduce->forward (tree RS / AG multicast)
+
+  std::string str() const {
+    std::ostringstream ss;
+    switch (kind) {
+      case AlgoKind::AUTO: ss << "auto"; break;
+      case AlgoKind::ONESHOT: ss << "oneshot"; break;
+      case AlgoKind::RING: ss << "ring"; if (channels > 1) ss << ":" << channels; break;
+      case AlgoKind::TREE:
+        ss << "tree:";
+        for (size_t i = 0; i < widths.size(); ++i) ss << (i ? "," : "") << widths[i];
+        break;
+    }
+    if (kind == AlgoKind::TREE && ag == AgMode::PULL) ss << "+pull";
+    if (kind == AlgoKind::TREE && ag == AgMode::PUSH) ss << "+push";
+    if (!fuse) ss << "+nofuse";
+    return ss.str();
+  }
+};
+
+inline bool is_prime(long n) {
+  if (n < 2) return false;
+  for (long i = 2; i * i <= n; ++i)
+    if (n % i == 0) return false;
+  return true;
+}
+
+inline std::vector<int> prime_factors(int n) {
+  std::vector<int> f;
+  for (int p = 2; (long)p * p <= n; ++p)
+    while (n % p == 0) { f.push_back(p); n /= p; }
+  if (n > 1) f.push_back(n);
+  return f;
+}
+
+// Ordered factorizations of n into factors >= 2 (n >= 2). H(n) of them.
+inline void ordered_factorizations_rec(int n, std::vector<int>& cur, std::vector<std::vector<int>>& out,
+                                       size_t limit) {
+  if (n == 1) {
+    if (!cur.empty()) out.push_back(cur);
+    return;
+  }
+  for (int f = 2; f <= n && out.size() < limit; ++f) {
+    if (n % f) continue;
+    cur.push_back(f);
+    ordered_factorizations_rec(n / f, cur, out, limit);
+    cur.pop_back();
+  }
+}
+inline std::vector<std::vector<int>> ordered_factorizations(int n, size_t limit = 100000) {
+  std::vector<std::vector<int>> out;
+  std::vector<int> cur;
+  if (n >= 2) ordered_factorizations_rec(n, cur, out, limit);
+  return out;
+}
+
+// H(n): number of ordered factorizations (memoised DP, not the reference's exponential recursion).
+inline uint64_t count_factorizations(int n) {
+  if (n <= 0) return 0;
+  std::vector<uint64_t> h(n + 1, 0);
+  h[1] = 1;
+  for (int m = 2; m <= n; ++m)
+    for (int f = 2; f <= m; ++f)
+      if (m % f == 0) h[m] += h[m / f];
+  return h[n];
+}
+
+inline std::vector<std::string> split_tokens(const std::string& s) {
+  std::vector<std::string> toks;
+  std::string cur;
+  for (char c : s) {
+    if (c == ',' || c == '*' || std::isspace((unsigned char)c)) {
+      if (!cur.empty()) toks.push_back(cur), cur.clear();
+    } else {
+      cur.push_back(c);
+    }
+  }
+  if (!cur.empty()) toks.push_back(cur);
+  return toks;
+}
+
+inline bool parse_int_list(const std::string& s, std::vector<int>* out, std::string* err) {
+  out->clear();
+  for (const auto& t : split_tokens(s)) {
+    char* end = nullptr;
+    long v = strtol(t.c_str(), &end, 10);
+    if (!end || *end != '\0' || v <= 0 || v > 1 << 20) {
+      if (err) *err = "invalid width '" + t + "'";
+      return false;
+    }
+    out->push_back((int)v);
+  }
+  return true;
+}
+
+// FT_TOPO semantics of the reference (mpi_mod.hpp:880-929).
+inline bool parse_ft_topo(const char* ft_topo, int nranks, AlgoSpec* spec, std::string* err) {
+  *spec = AlgoSpec();
+  std::string s = ft_topo ? ft_topo : "";
+  std::vector<int> w;
+  if (!parse_int_list(s, &w, err)) return false;
+  if (w.empty()) {  // unset / empty -> one flat stage
+    spec->kind = AlgoKind::TREE;
+    spec->widths = {nranks};
+    return true;
+  }
+  for (int x : w)
+    if (x == 1) {  // any 1 selects the ring (mpi_mod.hpp:907-910)
+      spec->kind = AlgoKind::RING;
+      return true;
+    }
+  long prod = 1;
+  for (int x : w) prod *= x;
+  if (prod != nranks) {
+    if (err) *err = "invalid FT_TOPO '" + s + "': product " + std::to_string(prod) + " != world size " +
+                    std::to_string(nranks);
+    return false;
+  }
+  spec->kind = AlgoKind::TREE;
+  spec->widths = w;
+  return true;
+}
+
+// Algorithm spec strings (see flexar.h).
+inline bool parse_algo(const std::string& raw, int nranks, AlgoSpec* spec, std::string* err) {
+  *spec = AlgoSpec();
+  std::string s = raw;
+  // suffix modifiers
+  for (;;) {
+    size_t p = s.rfind('+');
+    if (p == std::string::npos) break;
+    std::string mod = s.substr(p + 1);
+    s = s.substr(0, p);
+    if (mod == "pull") spec->ag = AgMode::PULL;
+    else if (mod == "push") spec->ag = AgMode::PUSH;
+    else if (mod == "nofuse") spec->fuse = false;
+    else if (mod == "fuse") spec->fuse = true;
+    else { if (err) *err = "unknown algorithm modifier '+" + mod + "'"; return false; }
+  }
+  std::string head = s, arg;
+  size_t c = s.find(':');
+  if (c != std::string::npos) head = s.substr(0, c), arg = s.substr(c + 1);
+  if (head.empty() || head == "auto") { spec->kind = AlgoKind::AUTO; return true; }
+  if (head == "oneshot") { spec->kind = AlgoKind::ONESHOT; return true; }
+  if (head == "ring") {
+    spec->kind = AlgoKind::RING;
+    if (!arg.empty()) {
+      std::vector<int> v;
+      if (!parse_int_list(arg, &v, err) || v.size() != 1) { if (err && err->empty()) *err = "ring:C expects one integer"; return false; }
+      spec->channels = v[0];
+    }
+    return true;
+  }
+  if (head == "flat" || head == "twoshot") { spec->kind = AlgoKind::TREE; spec->widths = {nranks}; return true; }
+  if (head == "rhd") {
+    if (nranks < 2 || (nranks & (nranks - 1))) { if (err) *err = "rhd needs a power-of-two world size"; return false; }
+    spec->kind = AlgoKind::TREE;
+    for (int n = nranks; n > 1; n >>= 1) spec->widths.push_back(2);
+    return true;
+  }
+  if (head == "tree") {
+    std::vector<int> w;
+    if (!parse_int_list(arg, &w, err)) return false;
+    long prod = 1;
+    for (int x : w) {
+      if (x < 2) { if (err) *err = "tree widths must be >= 2"; return false; }
+      prod *= x;
+    }
+    if (w.empty() || prod != nranks) { if (err) *err = "tree widths must multiply to the world size"; return false; }
+    spec->kind = AlgoKind::TREE;
+    spec->widths = w;
+    return true;
+  }
+  if (head == "ft") {
+    const char* env = getenv("FT_TOPO");
+    AgMode ag = spec->ag; bool fuse = spec->fuse;
+    if (!parse_ft_topo(env ? env : arg.c_str(), nranks, spec, err)) return false;
+    spec->ag = ag; spec->fuse = fuse;
+    return true;
+  }
+  if (err) *err = "unknown algorithm '" + raw + "'";
+  return false;
+}
+
+// Ring orders for multi-channel rings: directed cycles r -> r + d (mod N) with gcd(d, N) = 1 are
+// Hamiltonian and pairwise arc-disjoint, so C channels drive C distinct outgoing xGMI links per GPU.
+inline int gcd_int(int a, int b) { while (b) { int t = a % b; a = b; b = t; } return a; }
+inline std::vector<int> ring_steps(int nranks) {
+  std::vector<int> steps;
+  if (nranks <= 1) return steps;
+  // interleave d and N-d so channel pairs use both directions of the same links last
+  for (int d = 1; d < nranks; ++d)
+    if (gcd_int(d, nranks) == 1) steps.push_back(d);
+  return steps;
+}
+inline int max_ring_channels(int nranks) { int n = (int)ring_steps(nranks).size(); return n < 1 ? 1 : n; }
+// order[c][pos] = rank at position pos of ring c
+inline std::vector<int> ring_order(int nranks, int channel) {
+  std::vector<int> st = ring_steps(nranks);
+  int d = st.empty() ? 1 : st[channel % st.size()];
+  std::vector<int> ord(nranks);
+  for (int p = 0; p < nranks; ++p) ord[p] = (int)(((long)p * d) % nranks);
+  return ord;
+}
+
+// Candidate plans for the selector: ring (1..C channels), every ordered factorization as a tree,
+// and the one-shot.
+inline std::vector<AlgoSpec> enumerate_plans(int nranks) {
+  std::vector<AlgoSpec> out;
+  if (nranks <= 1) return out;
+  AlgoSpec os; os.kind = AlgoKind::ONESHOT; out.push_back(os);
+  int maxc = max_ring_channels(nranks);
+  for (int c = 1; c <= maxc; c *= 2) {
+    AlgoSpec r; r.kind = AlgoKind::RING; r.channels = c; out.push_back(r);
+  }
+  if (maxc > 1 && (maxc & (maxc - 1))) { AlgoSpec r; r.kind = AlgoKind::RING; r.channels = maxc; out.push_back(r); }
+  for (auto& w : ordered_factorizations(nranks, 4096)) {
+    AlgoSpec t; t.kind = AlgoKind::TREE; t.widths = w; out.push_back(t);
+  }
+  return out;
+}
+
+}  // namespace flexar

@@ -1,0 +1,215 @@
+// Host-only part of the C API: errors, planning utilities, the reference
+// cost model, the program dump, the CPU simulator of the device protocol and
+// the host reduction. Compiled by the plain host C++ compiler (no HIP).
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "flexar/cost_model.hpp"
+#include "flexar/flexar.h"
+#include "flexar/host_exec.hpp"
+#include "flexar/planner.hpp"
+#include "internal.hpp"
+
+namespace flexar {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+static int copy_out(const std::string& s, char* out, size_t outlen) {
+  if (!out || outlen == 0) return FLEXAR_ERR_INVALID;
+  size_t n = std::min(outlen - 1, s.size());
+  memcpy(out, s.data(), n);
+  out[n] = 0;
+  return s.size() < outlen ? 0 : FLEXAR_ERR_NOMEM;
+}
+
+struct RankBarrier {
+  std::mutex m;
+  std::condition_variable cv;
+  int count = 0, gen = 0, n = 0;
+  void arrive_and_wait() {
+    std::unique_lock<std::mutex> lk(m);
+    int g = gen;
+    if (++count == n) {
+      count = 0;
+      ++gen;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return gen != g; });
+    }
+  }
+};
+
+struct SimRun {
+  template <typename T, typename OP>
+  static int run(const std::vector<Program>& progs, int nranks, int grid, int ncalls, int in_place,
+                 const void* const* inputs, void* const* outputs, size_t count) {
+    const size_t es = sizeof(T);
+    uint64_t stg_elems = 0;
+    uint32_t nslots = 1;
+    for (auto& p : progs) {
+      stg_elems = std::max<uint64_t>(stg_elems, p.stg_elems);
+      nslots = std::max<uint32_t>(nslots, p.nslots);
+    }
+    uint64_t half = (stg_elems * es + 255) / 256 * 256;
+    std::vector<std::vector<char>> stg(nranks, std::vector<char>(2 * half + 256, (char)0xA5));  // poison
+    size_t nflags = (size_t)nslots * nranks * grid;
+    std::vector<std::unique_ptr<std::atomic<uint64_t>[]>> flags(nranks);
+    for (int r = 0; r < nranks; ++r) {
+      flags[r].reset(new std::atomic<uint64_t>[nflags]);
+      for (size_t i = 0; i < nflags; ++i) flags[r][i].store(0);
+    }
+    std::vector<HostExecCtx> ctx(nranks);
+    for (int r = 0; r < nranks; ++r) {
+      HostExecCtx& c = ctx[r];
+      c.rank = r;
+      c.local[BUF_IN] = in_place ? (char*)outputs[r] : (char*)inputs[r];
+      c.local[BUF_OUT] = (char*)outputs[r];
+      c.local[BUF_STG] = stg[r].data();
+      for (int p = 0; p < nranks; ++p) {
+        c.peer_stg.push_back(stg[p].data());
+        c.peer_flags.push_back(flags[p].get());
+      }
+      c.ranks_stride = nranks;
+      c.blocks_stride = grid;
+      c.stg_half_bytes = half;
+      c.timeout_s = 30.0;
+    }
+    std::vector<RankBarrier> bars(nranks);
+    for (auto& b : bars) b.n = grid;
+    std::atomic<int> rc{0};
+    std::vector<std::thread> th;
+    for (int r = 0; r < nranks; ++r)
+      for (int b = 0; b < grid; ++b)
+        th.emplace_back([&, r, b] {
+          for (int e = 1; e <= ncalls; ++e) {
+            if (in_place) {  // kernel boundary: rank r re-loads its input before each call
+              bars[r].arrive_and_wait();
+              if (b == 0) memcpy(outputs[r], inputs[r], count * es);
+              bars[r].arrive_and_wait();
+            }
+            int x = HostExec<T, OP>::run(progs[r], ctx[r], (uint32_t)b, (uint32_t)grid, (uint64_t)e);
+            if (x) rc.store(x);
+            bars[r].arrive_and_wait();  // all workgroups of rank r finish call e before e + 1 starts
+            if (rc.load()) return;
+          }
+        });
+    for (auto& t : th) t.join();
+    if (rc.load()) set_error("simulated wait timed out (deadlock in the program?)");
+    return rc.load();
+  }
+};
+
+struct HostReduce {
+  template <typename T, typename OP>
+  static int run(void* dst, const void* const* srcs, int nsrc, size_t count, float scale) {
+    std::vector<const T*> s(nsrc);
+    for (int i = 0; i < nsrc; ++i) s[i] = (const T*)srcs[i];
+    T* d = (T*)dst;
+    host_reduce_span<T, OP>(&d, 1, s.data(), nsrc, count, scale);
+    return 0;
+  }
+};
+
+static bool spec_for(const char* spec, int nranks, double bytes, AlgoSpec* s, std::string* err) {
+  if (!parse_algo(spec ? spec : "auto", nranks, s, err)) return false;
+  if (s->kind == AlgoKind::AUTO) *s = select_plan(XgmiModel::from_env(), nranks, bytes);
+  if (s->kind == AlgoKind::TREE && s->ag == AgMode::AUTO) s->ag = AgMode::PULL;
+  return true;
+}
+
+}  // namespace flexar
+
+using namespace flexar;
+
+extern "C" {
+
+const char* flexar_version(void) {
+  static char v[32];
+  snprintf(v, sizeof(v), "%d.%d.%d", FLEXAR_VERSION_MAJOR, FLEXAR_VERSION_MINOR, FLEXAR_VERSION_PATCH);
+  return v;
+}
+const char* flexar_last_error(void) { return g_last_error.c_str(); }
+size_t flexar_dtype_size(int dtype) { return dtype_size(dtype); }
+
+int flexar_parse_ft_topo(const char* ft_topo, int nranks, char* out, size_t outlen) {
+  AlgoSpec s;
+  std::string err;
+  if (!parse_ft_topo(ft_topo, nranks, &s, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  return copy_out(s.str(), out, outlen);
+}
+
+uint64_t flexar_count_factorizations(int n) { return count_factorizations(n); }
+
+int flexar_enumerate_plans(int nranks, char* out, size_t outlen) {
+  std::string s;
+  for (auto& p : enumerate_plans(nranks)) s += p.str() + "\n";
+  return copy_out(s, out, outlen);
+}
+
+double flexar_model_cost_us(const char* spec, int nranks, double bytes) {
+  AlgoSpec s;
+  std::string err;
+  if (!spec_for(spec, nranks, bytes, &s, &err)) { set_error(err); return -1.0; }
+  return XgmiModel::from_env().cost_us(s, nranks, bytes);
+}
+
+int flexar_select_plan(int nranks, double bytes, char* out, size_t outlen) {
+  if (nranks < 1) return FLEXAR_ERR_INVALID;
+  return copy_out(select_plan(XgmiModel::from_env(), nranks, bytes).str(), out, outlen);
+}
+
+double flexar_legacy_cost(const char* widths_csv, int nranks, double chunk) {
+  std::vector<int> w;
+  std::string err;
+  if (!parse_int_list(widths_csv ? widths_csv : "", &w, &err) || w.empty()) { set_error(err); return -1.0; }
+  return legacy_cost(w, nranks, chunk);
+}
+
+int flexar_plan_dump(const char* spec, int rank, int nranks, size_t count, int dtype, char* out, size_t outlen) {
+  size_t es = dtype_size(dtype);
+  if (!es || rank < 0 || rank >= nranks) { set_error("bad arguments"); return FLEXAR_ERR_INVALID; }
+  AlgoSpec s;
+  std::string err;
+  if (!spec_for(spec, nranks, (double)count * es, &s, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  Program P;
+  Planner pl(nranks, rank, count, (uint32_t)es, 1.0f);
+  if (!pl.build(s, &P, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  return copy_out(dump_program(P, rank), out, outlen);
+}
+
+int flexar_simulate(const char* spec, int nranks, size_t count, int dtype, int op, const void* const* inputs,
+                    void* const* outputs, int grid, int ncalls, int in_place, float scale) {
+  size_t es = dtype_size(dtype);
+  if (!es || nranks < 1 || nranks > 64 || grid < 1 || grid > 64 || ncalls < 1 || !inputs || !outputs) {
+    set_error("bad simulate arguments");
+    return FLEXAR_ERR_INVALID;
+  }
+  if (!op_supported(dtype, op)) { set_error("unsupported dtype/op"); return FLEXAR_ERR_UNSUPPORTED; }
+  AlgoSpec s;
+  std::string err;
+  if (!spec_for(spec, nranks, (double)count * es, &s, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  float fs = scale * (op == FLEXAR_AVG ? 1.0f / (float)nranks : 1.0f);
+  std::vector<Program> progs(nranks);
+  for (int r = 0; r < nranks; ++r) {
+    Planner pl(nranks, r, count, (uint32_t)es, fs);
+    if (!pl.build(s, &progs[r], &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+    if (progs[r].nchan > (uint32_t)grid) { set_error("grid must be >= number of channels"); return FLEXAR_ERR_INVALID; }
+  }
+  if (grid % progs[0].nchan) { set_error("grid must be a multiple of the channel count"); return FLEXAR_ERR_INVALID; }
+  return dispatch_dtype_op<SimRun>(dtype, op, progs, nranks, grid, ncalls, in_place, inputs, outputs, count);
+}
+
+int flexar_reduce_host(void* dst, const void* const* srcs, int nsrc, size_t count, int dtype, int op, float scale) {
+  if (!dst || !srcs || nsrc < 1) { set_error("bad reduce arguments"); return FLEXAR_ERR_INVALID; }
+  float fs = scale * (op == FLEXAR_AVG ? 1.0f / (float)nsrc : 1.0f);
+  return dispatch_dtype_op<HostReduce>(dtype, op, dst, srcs, nsrc, count, fs);
+}
+
+}  // extern "C"

@@ -1,0 +1,70 @@
+// Instantiation helper included by each k_<dtype>.hip.
+#pragma once
+
+#include <string>
+
+#include "internal.hpp"
+#include "launch.hpp"
+
+namespace flexar {
+
+template <typename T, typename OP>
+inline int launch_one(const LaunchArgs& a) {
+  switch (a.kind) {
+    case LAUNCH_EXEC:
+      hipLaunchKernelGGL((exec_kernel<T, OP>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
+      break;
+    case LAUNCH_GROUP:
+      hipLaunchKernelGGL((exec_group_kernel<T, OP>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0, a.stream,
+                         a.d_ctxs, (uint32_t)a.grid);
+      break;
+    case LAUNCH_REDUCE:
+      hipLaunchKernelGGL((reduce_kernel<T, OP>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.srcs, a.nsrc,
+                         a.dst, a.n, a.scale, a.vec);
+      break;
+    default:
+      return FLEXAR_ERR_INVALID;
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(std::string("kernel launch: ") + hipGetErrorString(e));
+    return FLEXAR_ERR_HIP;
+  }
+  return 0;
+}
+
+template <typename T>
+inline int launch_float(int op, const LaunchArgs& a) {
+  switch (op) {
+    case FLEXAR_SUM: case FLEXAR_AVG: return launch_one<T, OpSum>(a);
+    case FLEXAR_PROD: return launch_one<T, OpProd>(a);
+    case FLEXAR_MAX: return launch_one<T, OpMax>(a);
+    case FLEXAR_MIN: return launch_one<T, OpMin>(a);
+    default: return FLEXAR_ERR_UNSUPPORTED;
+  }
+}
+
+template <typename T>
+inline int launch_int(int op, const LaunchArgs& a) {
+  switch (op) {
+    case FLEXAR_SUM: return launch_one<T, OpSum>(a);
+    case FLEXAR_PROD: return launch_one<T, OpProd>(a);
+    case FLEXAR_MAX: return launch_one<T, OpMax>(a);
+    case FLEXAR_MIN: return launch_one<T, OpMin>(a);
+    case FLEXAR_BAND: return launch_one<T, OpBand>(a);
+    case FLEXAR_BOR: return launch_one<T, OpBor>(a);
+    case FLEXAR_BXOR: return launch_one<T, OpBxor>(a);
+    default: return FLEXAR_ERR_UNSUPPORTED;
+  }
+}
+
+}  // namespace flexar
+
+#define FX_DEFINE_FLOAT_LAUNCH(T, NAME) \
+  namespace flexar {                    \
+  int launch_##NAME(int op, const LaunchArgs& a) { return launch_float<T>(op, a); } \
+  }
+#define FX_DEFINE_INT_LAUNCH(T, NAME) \
+  namespace flexar {                  \
+  int launch_##NAME(int op, const LaunchArgs& a) { return launch_int<T>(op, a); } \
+  }
