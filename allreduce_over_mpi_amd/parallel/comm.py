@@ -1,0 +1,170 @@
+"""Device communicators over the native flexar runtime.
+
+* :class:`Communicator` — one rank per process / per GPU (the production path).
+  Bootstrap: every rank exports its workspace IPC handles, the bytes are
+  all-gathered through ``torch.distributed`` (any backend: gloo or RCCL), then
+  each rank maps its peers' workspaces. After that an allreduce is a single
+  stream-ordered kernel launch with no host involvement — the reference's
+  ``MPI_Allreduce_FT`` (allreduce_over_mpi/mpi_mod.hpp:1167-1221) on
+  GPU-resident tensors.
+* :class:`LocalGroup` — ``n`` ranks inside ONE process on ONE GPU, all ranks in
+  one launch. Runs the complete multi-rank device protocol without IPC; used by
+  the GPU test-suite and for calibration.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+from .. import _native as nv
+
+
+def _stream_handle(stream=None) -> int:
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def _require_cuda(t, what="tensor"):
+    if not t.is_cuda:
+        raise nv.FlexarError(1, f"{what} must be a ROCm device tensor")
+    if not t.is_contiguous():
+        raise nv.FlexarError(1, f"{what} must be contiguous")
+
+
+class Communicator:
+    """flexar communicator for the calling rank of a ``torch.distributed`` group."""
+
+    def __init__(self, group=None, device: Optional[int] = None, workspace_bytes: int = 0,
+                 algo: Optional[str] = None, rank: Optional[int] = None, world_size: Optional[int] = None):
+        import torch
+        import torch.distributed as dist
+
+        self._lib = nv.lib()
+        if rank is None or world_size is None:
+            if dist.is_available() and dist.is_initialized():
+                rank = dist.get_rank(group)
+                world_size = dist.get_world_size(group)
+            else:
+                rank, world_size = 0, 1
+        self.rank, self.world_size = int(rank), int(world_size)
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        self.group = group
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            nv.check(self._lib.flexar_comm_create(self.rank, self.world_size, self.device, int(workspace_bytes),
+                                                  ctypes.byref(h)), "comm_create")
+        self._h = h
+        if self.world_size > 1:
+            hs = int(self._lib.flexar_handle_size())
+            buf = ctypes.create_string_buffer(hs)
+            nv.check(self._lib.flexar_comm_export(self._h, buf), "comm_export")
+            gathered = [None] * self.world_size
+            dist.all_gather_object(gathered, bytes(buf.raw), group=group)
+            allb = b"".join(gathered)
+            nv.check(self._lib.flexar_comm_connect(self._h, allb), "comm_connect")
+            # everyone has mapped everyone before the first collective
+            dist.barrier(group=group)
+        if algo:
+            self.set_algo(algo)
+
+    # ------------------------------------------------------------------ config
+    def set_algo(self, spec: str):
+        nv.check(self._lib.flexar_comm_set_algo(self._h, spec.encode()), "set_algo")
+
+    def set_grid(self, grid: int):
+        nv.check(self._lib.flexar_comm_set_grid(self._h, int(grid), 0), "set_grid")
+
+    def describe(self, count: int, dtype) -> str:
+        b = ctypes.create_string_buffer(512)
+        nv.check(self._lib.flexar_comm_describe(self._h, int(count), nv.dtype_code(dtype), b, 512), "describe")
+        return b.value.decode()
+
+    def check(self):
+        nv.check(self._lib.flexar_comm_check(self._h), "comm_check")
+
+    # ------------------------------------------------------------------ collectives
+    def all_reduce(self, tensor, op="sum", out=None, algo: Optional[str] = None, scale: float = 1.0, stream=None):
+        """Allreduce ``tensor`` (in place unless ``out`` is given). Returns the result tensor."""
+        _require_cuda(tensor)
+        dst = tensor if out is None else out
+        if out is not None:
+            _require_cuda(out, "out")
+            if out.numel() != tensor.numel() or out.dtype != tensor.dtype:
+                raise nv.FlexarError(1, "out must match tensor in size and dtype")
+        rc = self._lib.flexar_allreduce_ex(self._h, tensor.data_ptr(), dst.data_ptr(), tensor.numel(),
+                                           nv.dtype_code(tensor.dtype), nv.op_code(op), _stream_handle(stream),
+                                           algo.encode() if algo else None, float(scale))
+        nv.check(rc, "allreduce")
+        return dst
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.flexar_comm_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class LocalGroup:
+    """``nranks`` flexar ranks on one GPU in one process (single-launch group execution)."""
+
+    def __init__(self, nranks: int, device: Optional[int] = None, workspace_bytes: int = 64 << 20):
+        import torch
+
+        self._lib = nv.lib()
+        self.nranks = int(nranks)
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        arr = (ctypes.c_void_p * self.nranks)()
+        with torch.cuda.device(self.device):
+            nv.check(self._lib.flexar_group_create(self.nranks, self.device, int(workspace_bytes), arr), "group_create")
+        self._comms = arr
+
+    def set_grid(self, grid: int):
+        for r in range(self.nranks):
+            nv.check(self._lib.flexar_comm_set_grid(self._comms[r], int(grid), 0), "set_grid")
+
+    def describe(self, count: int, dtype, rank: int = 0) -> str:
+        b = ctypes.create_string_buffer(512)
+        nv.check(self._lib.flexar_comm_describe(self._comms[rank], int(count), nv.dtype_code(dtype), b, 512),
+                 "describe")
+        return b.value.decode()
+
+    def all_reduce(self, tensors: Sequence, op="sum", outs: Optional[Sequence] = None, algo: Optional[str] = None,
+                   scale: float = 1.0, stream=None):
+        if len(tensors) != self.nranks:
+            raise nv.FlexarError(1, "need one tensor per rank")
+        for t in tensors:
+            _require_cuda(t)
+        outs = list(tensors) if outs is None else list(outs)
+        ins = (ctypes.c_void_p * self.nranks)(*[t.data_ptr() for t in tensors])
+        ous = (ctypes.c_void_p * self.nranks)(*[t.data_ptr() for t in outs])
+        rc = self._lib.flexar_group_allreduce(self._comms, self.nranks, ins, ous, tensors[0].numel(),
+                                              nv.dtype_code(tensors[0].dtype), nv.op_code(op), _stream_handle(stream),
+                                              algo.encode() if algo else None, float(scale))
+        nv.check(rc, "group_allreduce")
+        return outs
+
+    def check(self):
+        for r in range(self.nranks):
+            nv.check(self._lib.flexar_comm_check(self._comms[r]), f"rank {r}")
+
+    def close(self):
+        if getattr(self, "_comms", None) is not None:
+            for r in range(self.nranks):
+                if self._comms[r]:
+                    self._lib.flexar_comm_destroy(self._comms[r])
+                    self._comms[r] = None
+            self._comms = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,240 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: allreduce bus bandwidth on N MI355X GPUs (one rank per GPU).
+
+Metric and config are BASELINE.json's: "allreduce bus bandwidth (GB/s) vs buffer
+bytes, fp32/bf16, at 1/2/4/8 MI355X", headline buffer = config #2 (fp32,
+256 MiB). The reference's own driver (allreduce_over_mpi/benchmark.cpp:147-215)
+times MPI_Allreduce_FT with MPI_Barrier + MPI_Wtime on rank 0 only; here every
+rank is timed over K steps bracketed by barrier + device synchronize on both
+sides and the MAX over ranks is reported.
+
+    python bench.py --gpus 1 --steps 20 --warmup 5
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+        --master-addr 127.0.0.1 --master-port 29500 bench.py --gpus 8
+
+busbw = (bytes / t) * 2 (N - 1) / N (rccl-tests convention). For N = 1 the
+factor is 0 (no inter-GPU traffic), so the N = 1 line reports algbw of the
+out-of-place allreduce (a device copy through the flexar kernel) and says so.
+Data: synthetic torch.randn buffers seeded per rank. Every run first checks the
+flexar result against RCCL's (torch.distributed "nccl") on the same inputs.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+# the reference (FlexTree ring, FT_TOPO=1) at N=2, 256 MiB fp32 = 3.15 GB/s busbw
+# (measured locally on CPU/MPICH — the reference publishes no numbers).
+BASELINE_BUSBW_256MIB = 3.15
+
+
+def log(rank, *a):
+    if rank == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--size-mb", type=float, default=256.0, help="buffer MiB per rank")
+    ap.add_argument("--dtype", default="float32", choices=["float32", "bfloat16", "float16"])
+    ap.add_argument("--algo", default="auto", help="flexar algorithm spec or 'auto' (tuned at start-up)")
+    ap.add_argument("--no-rccl", action="store_true", help="skip the RCCL comparison run")
+    ap.add_argument("--no-tune", action="store_true", help="use the cost model instead of the start-up tuner")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    if args.gpus != world:
+        log(rank, f"note: --gpus {args.gpus} but WORLD_SIZE={world}; benchmarking {world} rank(s)")
+
+    from allreduce_over_mpi_amd.parallel.comm import Communicator
+    from allreduce_over_mpi_amd.utils.perf import algbw_gbps, busbw_gbps
+
+    dtype = getattr(torch, args.dtype)
+    esize = torch.tensor([], dtype=dtype).element_size()
+    nbytes = int(args.size_mb * (1 << 20))
+    count = nbytes // esize
+    nbytes = count * esize
+
+    comm = Communicator(workspace_bytes=max(512 << 20, 2 * nbytes + (64 << 20)))
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + rank)
+    x = torch.randn(count, device=dev, dtype=torch.float32, generator=gen).to(dtype)
+    y = torch.empty_like(x)
+
+    def max_over_ranks(v: float) -> float:
+        if world == 1:
+            return v
+        t = torch.tensor([v], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    # ---------------------------------------------------------------- correctness vs RCCL
+    ref = x.clone()
+    if world > 1:
+        dist.all_reduce(ref)
+    tol = (1e-5 if dtype == torch.float32 else 2e-2) * math.sqrt(world) * 4
+
+    def check(spec):
+        comm.all_reduce(x, out=y, algo=None if spec == "auto" else spec)
+        torch.cuda.synchronize()
+        err = float((y.float() - ref.float()).abs().max().item())
+        scale = float(ref.float().abs().max().item()) + 1e-6
+        ok = err <= tol * scale
+        return ok, err
+
+    def timed(spec, iters, warm=1):
+        a = None if spec == "auto" else spec
+        for _ in range(warm):
+            comm.all_reduce(x, out=y, algo=a)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            comm.all_reduce(x, out=y, algo=a)
+        torch.cuda.synchronize()
+        return max_over_ranks(time.perf_counter() - t0) / iters
+
+    # ---------------------------------------------------------------- start-up tuner
+    algo = args.algo
+    tune_log = {}
+    if world > 1 and algo == "auto" and not args.no_tune:
+        from allreduce_over_mpi_amd import _native as nv
+
+        cands = ["flat+pull", "flat+push"]
+        maxc = len([d for d in range(1, world) if math.gcd(d, world) == 1])
+        cands += ["ring"] + [f"ring:{c}" for c in (2, 4, 8) if c <= maxc]
+        if world > 2 and (world & (world - 1)) == 0:
+            cands += ["rhd+pull"]
+        best, best_t = None, float("inf")
+        for spec in cands:
+            try:
+                ok, err = check(spec)
+                okv = max_over_ranks(0.0 if ok else 1.0) == 0.0
+                if not okv:
+                    tune_log[spec] = f"WRONG (max err {err:.3g})"
+                    log(rank, f"tuner: {spec} produced wrong results (err {err:.3g}); excluded")
+                    continue
+                t = timed(spec, 3)
+                tune_log[spec] = round(busbw_gbps(nbytes, t, world), 2)
+                log(rank, f"tuner: {spec:12s} {t*1e3:8.3f} ms  busbw {busbw_gbps(nbytes, t, world):8.1f} GB/s")
+                if t < best_t:
+                    best, best_t = spec, t
+            except nv.FlexarError as e:
+                tune_log[spec] = f"error: {e}"
+                log(rank, f"tuner: {spec} failed: {e}")
+        if best is None:
+            raise SystemExit("no flexar algorithm produced correct results")
+        # grid size for the winner
+        best_grid, best_gt = 0, best_t
+        for g in (32, 64, 128):
+            comm.set_grid(g)
+            t = timed(best, 3)
+            tune_log[f"{best}@grid{g}"] = round(busbw_gbps(nbytes, t, world), 2)
+            if t < best_gt:
+                best_grid, best_gt = g, t
+        comm.set_grid(best_grid)
+        algo = best
+        log(rank, f"tuner: selected {algo} grid={best_grid or 'auto'}")
+
+    ok, err = check(algo)
+    if max_over_ranks(0.0 if ok else 1.0) != 0.0:
+        raise SystemExit(f"flexar result mismatch vs RCCL (max err {err:.3g})")
+    desc = comm.describe(count, dtype) if algo == "auto" else algo
+    log(rank, f"correctness vs {'RCCL' if world > 1 else 'input'}: max err {err:.3g} (ok); running {desc}")
+
+    # ---------------------------------------------------------------- timed region
+    a = None if algo == "auto" else algo
+    for _ in range(args.warmup):
+        comm.all_reduce(x, out=y, algo=a)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        comm.all_reduce(x, out=y, algo=a)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    comm.check()
+    t_step = elapsed / max(1, args.steps)
+
+    rccl_busbw = None
+    if world > 1 and not args.no_rccl:
+        z = x.clone()
+        for _ in range(max(1, args.warmup)):
+            dist.all_reduce(z)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            dist.all_reduce(z)
+        torch.cuda.synchronize()
+        dist.barrier()
+        rt = max_over_ranks(time.perf_counter() - t1) / max(1, args.steps)
+        rccl_busbw = round(busbw_gbps(nbytes, rt, world), 2)
+
+    algbw = algbw_gbps(nbytes, t_step)
+    busbw = busbw_gbps(nbytes, t_step, world)
+    value = busbw if world > 1 else algbw
+    out = {
+        "metric": "allreduce bus bandwidth (GB/s)",
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(t_step * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / BASELINE_BUSBW_256MIB, 2) if (world > 1 and args.size_mb == 256.0) else None,
+        "dtype": {"float32": "fp32", "bfloat16": "bf16", "float16": "fp16"}[args.dtype],
+        "data": "synthetic (torch.randn per rank, seeded); result checked against RCCL before timing",
+        "config": {
+            "model": f"allreduce {args.dtype} {args.size_mb:g}MiB buffer per rank (BASELINE config #2)",
+            "global_batch": nbytes,
+            "seq_len": None,
+            "parallelism": f"dp{world}",
+            "algorithm": desc,
+        },
+        "busbw_GBps": round(busbw, 2),
+        "algbw_GBps": round(algbw, 2),
+        "aggregate_busbw_GBps": round(busbw * world, 2),
+        "rccl_busbw_GBps": rccl_busbw,
+        "tuner": tune_log or None,
+    }
+    if world == 1:
+        out["note"] = ("N=1: busbw factor 2(N-1)/N is 0; value = algbw of the out-of-place allreduce "
+                       "(device copy through the flexar executor kernel)")
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    comm.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -62,6 +62,8 @@ struct DevProgram {
   uint32_t* d_chan = nullptr;
 };
 
+static const uint32_t kGroupMaxBlocks = 256;
+
 static uint64_t env_u64(const char* name, uint64_t dflt) {
   const char* e = getenv(name);
   if (!e || !*e) return dflt;
@@ -469,6 +471,9 @@ int flexar_group_create(int nranks, int device, size_t workspace_bytes, flexar_c
     int rc = flexar_comm_create(r, nranks, device, workspace_bytes, &comms[r]);
     if (rc) return rc;
     comms[r]->group_member = true;
+    // every rank's workgroups share one launch and spin on each other: keep the whole grid
+    // co-resident (exec_group_kernel: 1 workgroup of 512 threads per CU at its VGPR count)
+    comms[r]->max_grid = std::max(1, (int)kGroupMaxBlocks / nranks);
   }
   for (int r = 0; r < nranks; ++r) {
     for (int p = 0; p < nranks; ++p) {
@@ -519,7 +524,10 @@ int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
       grid = r == 0 ? g : grid;
       if (g != grid) { set_error("group ranks disagree on grid"); return FLEXAR_ERR_STATE; }
     }
-    if ((uint64_t)grid * nranks > kMaxGridBlocks * 4) { set_error("group grid too large"); return FLEXAR_ERR_INVALID; }
+    if ((uint64_t)grid * nranks > kGroupMaxBlocks) {
+      set_error("group grid too large: ranks x grid must stay <= 256 co-resident workgroups");
+      return FLEXAR_ERR_INVALID;
+    }
     FX_HIP(hipMemcpyAsync(d_ctx, h.data(), sizeof(DevCtx) * nranks, hipMemcpyHostToDevice, st));
     LaunchArgs la;
     la.kind = LAUNCH_GROUP;

@@ -1,0 +1,174 @@
+"""gfx950 kernels on a real MI355X: the standalone reduction kernel and the
+complete multi-rank allreduce protocol (LocalGroup: N ranks in one launch on
+one GPU — flags, epochs, parity staging, every algorithm) against plain
+PyTorch fp32/fp64 references of the same op.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _seq_ref(srcs, op="sum", scale=1.0):
+    """Sequential fp32 reduction in source order (the kernel's order), then one rounding."""
+    acc = srcs[0].float()
+    for s in srcs[1:]:
+        f = s.float()
+        acc = {"sum": acc + f, "max": torch.maximum(acc, f), "min": torch.minimum(acc, f), "prod": acc * f}[op]
+    return acc * scale if scale != 1.0 else acc
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64])
+@pytest.mark.parametrize("nsrc", [1, 2, 3, 5, 8, 12])
+@pytest.mark.parametrize("n", [1, 37, 4099, 1 << 20])
+def test_reduce_kernel_float(cuda, dtype, nsrc, n):
+    from allreduce_over_mpi_amd.ops import reduce
+
+    g = torch.Generator(device=cuda).manual_seed(nsrc * 1000 + n)
+    srcs = [torch.randn(n, device=cuda, generator=g).to(dtype) for _ in range(nsrc)]
+    out = reduce(srcs, "sum")
+    torch.cuda.synchronize()
+    want = _seq_ref(srcs)
+    if dtype in (torch.float32, torch.float64) or nsrc <= 8:
+        # single pass: fp32 (fp64) accumulate in source order, one rounding
+        torch.testing.assert_close(out.double(), want.to(dtype).double(), rtol=0, atol=0) if dtype != torch.float64 \
+            else torch.testing.assert_close(out, sum(s for s in srcs[1:]) + srcs[0], rtol=1e-12, atol=1e-12)
+    else:
+        torch.testing.assert_close(out.float(), want, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float8_e4m3fn, torch.float8_e5m2])
+def test_reduce_kernel_fp8_scaled(cuda, dtype):
+    """fp8 (OCP, gfx950-native) with fused post-scale: fp32 accumulate, one saturating RNE rounding."""
+    from allreduce_over_mpi_amd.ops import reduce
+
+    g = torch.Generator(device=cuda).manual_seed(5)
+    srcs = [(torch.randn(1 << 16, device=cuda, generator=g) * 4).to(dtype) for _ in range(8)]
+    out = reduce(srcs, "sum", scale=0.125)
+    torch.cuda.synchronize()
+    want = (_seq_ref(srcs) * 0.125).to(dtype)
+    assert torch.equal(out.view(torch.uint8), want.view(torch.uint8))
+
+
+@pytest.mark.parametrize("op", ["sum", "max", "min", "band", "bor", "bxor", "prod"])
+def test_reduce_kernel_int(cuda, op):
+    from allreduce_over_mpi_amd.ops import reduce
+
+    g = torch.Generator(device=cuda).manual_seed(3)
+    srcs = [torch.randint(0, 1000, (10007,), device=cuda, generator=g, dtype=torch.int32) for _ in range(4)]
+    out = reduce(srcs, op)
+    acc = srcs[0].clone()
+    for s in srcs[1:]:
+        acc = {"sum": acc + s, "max": torch.maximum(acc, s), "min": torch.minimum(acc, s), "band": acc & s,
+               "bor": acc | s, "bxor": acc ^ s, "prod": acc * s}[op]
+    assert torch.equal(out, acc)
+
+
+def _specs(n):
+    from allreduce_over_mpi_amd import _native as nv
+
+    base = ["flat", "flat+push", "ring", "oneshot"]
+    base += [p for p in nv.enumerate_plans(n) if p.startswith("tree:") or p.startswith("ring:")]
+    base += [p + "+push" for p in nv.enumerate_plans(n) if p.startswith("tree:") and "," in p]
+    return sorted(set(base))
+
+
+@pytest.fixture(scope="module")
+def groups(cuda):
+    from allreduce_over_mpi_amd.parallel import LocalGroup
+
+    gs = {n: LocalGroup(n, workspace_bytes=64 << 20) for n in (2, 3, 4, 8)}
+    yield gs
+    for g in gs.values():
+        g.close()
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
+def test_group_allreduce_all_algorithms_f32(cuda, groups, n):
+    grp = groups[n]
+    for spec in _specs(n):
+        for size in (1, 35, 1000, 65539, (1 << 20) + 5):
+            g = torch.Generator(device=cuda).manual_seed(size + n)
+            xs = [torch.randn(size, device=cuda, generator=g) for _ in range(n)]
+            ref = torch.stack([x.double() for x in xs]).sum(0)
+            for in_place in (False, True):
+                ins = [x.clone() for x in xs]
+                outs = None if in_place else [torch.empty_like(x) for x in xs]
+                for _ in range(3):  # both staging parities + epoch progression
+                    if in_place:
+                        for i, x in zip(ins, xs):
+                            i.copy_(x)
+                    res = grp.all_reduce(ins, "sum", outs=outs, algo=spec)
+                    torch.cuda.synchronize()
+                    for r, o in enumerate(res):
+                        err = (o.double() - ref).abs().max().item()
+                        assert err < 1e-4 * math.sqrt(n), f"{spec} n={n} size={size} rank={r} inplace={in_place} err={err}"
+    grp.check()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.int32, torch.float64])
+def test_group_allreduce_dtypes(cuda, groups, dtype):
+    n = 8
+    grp = groups[n]
+    g = torch.Generator(device=cuda).manual_seed(11)
+    if dtype == torch.int32:
+        xs = [torch.randint(-1000, 1000, (300007,), device=cuda, generator=g, dtype=dtype) for _ in range(n)]
+    else:
+        xs = [torch.randn(300007, device=cuda, generator=g).to(dtype) for _ in range(n)]
+    ref = torch.stack([x.double() for x in xs]).sum(0)
+    for spec in ("flat", "ring:4", "rhd", "tree:2,4+push", "oneshot"):
+        outs = grp.all_reduce([x.clone() for x in xs], "sum", algo=spec)
+        torch.cuda.synchronize()
+        for o in outs:
+            if dtype == torch.int32:
+                assert torch.equal(o.double(), ref)
+            else:
+                tol = 1e-9 if dtype == torch.float64 else (2e-2 if dtype == torch.bfloat16 else 4e-3) * 8
+                torch.testing.assert_close(o.double(), ref, rtol=tol, atol=tol)
+
+
+def test_group_flat_bf16_single_rounding(cuda, groups):
+    """flat = one reduction stage: every rank gets the fp32-accumulated sum rounded once."""
+    n = 8
+    grp = groups[n]
+    g = torch.Generator(device=cuda).manual_seed(12)
+    xs = [torch.randn(65536, device=cuda, generator=g).to(torch.bfloat16) for _ in range(n)]
+    outs = grp.all_reduce([x.clone() for x in xs], "sum", algo="flat")
+    exact = torch.stack([x.double() for x in xs]).sum(0)
+    for o in outs:
+        assert (o.double() - exact).abs().max().item() <= (exact.abs() * 2 ** -8).max().item() + 1e-6
+
+
+def test_group_avg_and_fp8(cuda, groups):
+    n = 4
+    grp = groups[n]
+    g = torch.Generator(device=cuda).manual_seed(13)
+    xs = [torch.randn(4096, device=cuda, generator=g) for _ in range(n)]
+    outs = grp.all_reduce([x.clone() for x in xs], "avg", algo="flat")
+    ref = torch.stack(xs).mean(0)
+    for o in outs:
+        torch.testing.assert_close(o, ref, rtol=1e-5, atol=1e-6)
+    # fp8 e4m3 gradient allreduce with fused 1/N post-scale (BASELINE config #5)
+    x8 = [(x * 8).to(torch.float8_e4m3fn) for x in xs]
+    outs = grp.all_reduce([x.clone() for x in x8], "avg", algo="flat")
+    exact = (torch.stack([x.float() for x in x8]).sum(0) / n)
+    for o in outs:
+        assert torch.equal(o.view(torch.uint8), exact.to(torch.float8_e4m3fn).view(torch.uint8)) or \
+            (o.float() - exact).abs().max().item() <= 0.0625 * exact.abs().max().item()
+
+
+def test_communicator_single_rank(cuda):
+    from allreduce_over_mpi_amd.parallel import Communicator
+
+    c = Communicator(rank=0, world_size=1, workspace_bytes=16 << 20)
+    x = torch.randn(12345, device=cuda)
+    y = torch.empty_like(x)
+    c.all_reduce(x, out=y)
+    torch.cuda.synchronize()
+    assert torch.equal(x, y)
+    c.all_reduce(x, op="avg", out=y, scale=2.0)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(y, 2 * x)
+    c.close()

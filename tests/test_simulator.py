@@ -1,0 +1,137 @@
+"""Every algorithm / topology / geometry executed by the CPU simulator of the
+device protocol (the exact op programs the gfx950 kernel runs, one thread per
+(rank, workgroup), real flags/epochs/parity) against a numpy reference.
+
+Mirrors the survey's black-box verification of the reference:
+sizes {1,5,35,1000,1001,65539}, in/out of place, N = 2..8 on every topology,
+primes, N = 21 (where the reference's flat fan-in > 20 produced garbage, D3).
+"""
+import numpy as np
+import pytest
+
+SIZES = [1, 5, 35, 1000, 1001, 65539]
+
+
+def topologies(n):
+    from allreduce_over_mpi_amd import _native as nv
+
+    out = ["flat", "flat+push", "ring", "oneshot", "flat+nofuse"]
+    out += [p for p in nv.enumerate_plans(n) if p.startswith("tree:") or p.startswith("ring:")]
+    out += [p + "+push" for p in nv.enumerate_plans(n) if p.startswith("tree:") and "," in p]
+    return sorted(set(out))
+
+
+def ref_sum(ins):
+    return np.sum(np.stack(ins).astype(np.float64), 0)
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 6, 7, 8])
+def test_all_topologies_f32(nv, n):
+    rng = np.random.default_rng(n)
+    for spec in topologies(n):
+        chans = int(spec.split(":")[1].split("+")[0]) if spec.startswith("ring:") else 1
+        for size in SIZES:
+            ins = [rng.standard_normal(size).astype(np.float32) for _ in range(n)]
+            for in_place in (False, True):
+                outs = nv.simulate(spec, ins, grid=max(2, chans) if chans == 1 else chans * 2, ncalls=3,
+                                   in_place=in_place)
+                ref = ref_sum(ins)
+                for r, o in enumerate(outs):
+                    np.testing.assert_allclose(o, ref, rtol=1e-5, atol=1e-4, err_msg=f"{spec} n={n} size={size} r={r}")
+
+
+@pytest.mark.parametrize("n,spec", [(21, "flat"), (21, "tree:3,7"), (21, "ring"), (16, "tree:2,2,2,2"),
+                                    (16, "tree:4,4+push"), (12, "tree:2,3,2"), (9, "tree:3,3")])
+def test_wide_and_prime(nv, n, spec):
+    rng = np.random.default_rng(7)
+    ins = [rng.integers(-1000, 1000, 4099).astype(np.int64) for _ in range(n)]
+    outs = nv.simulate(spec, ins, grid=2, ncalls=2)
+    ref = np.sum(np.stack(ins), 0)
+    for o in outs:
+        np.testing.assert_array_equal(o, ref)
+
+
+@pytest.mark.parametrize("op", ["sum", "prod", "max", "min", "band", "bor", "bxor"])
+@pytest.mark.parametrize("dt", ["int32", "uint8", "int64", "int16"])
+def test_integer_ops(nv, op, dt):
+    rng = np.random.default_rng(1)
+    n = 4
+    ins = [rng.integers(0, 100, 777).astype(dt) for _ in range(n)]
+    fn = {"sum": np.add, "prod": np.multiply, "max": np.maximum, "min": np.minimum, "band": np.bitwise_and,
+          "bor": np.bitwise_or, "bxor": np.bitwise_xor}[op]
+    ref = ins[0].copy()
+    for x in ins[1:]:
+        ref = fn(ref, x).astype(dt)
+    for spec in ("flat", "ring", "rhd", "oneshot"):
+        outs = nv.simulate(spec, ins, op=op, grid=3, ncalls=2)
+        for o in outs:
+            np.testing.assert_array_equal(o, ref, err_msg=f"{spec} {op} {dt}")
+
+
+def test_float_ops_and_avg(nv):
+    rng = np.random.default_rng(2)
+    n = 8
+    ins = [rng.standard_normal(3001).astype(np.float64) for _ in range(n)]
+    st = np.stack(ins)
+    for op, ref in (("max", st.max(0)), ("min", st.min(0)), ("avg", st.mean(0)), ("sum", st.sum(0))):
+        for spec in ("flat", "ring:4", "tree:2,4", "oneshot"):
+            outs = nv.simulate(spec, ins, op=op, grid=4, ncalls=2)
+            for o in outs:
+                np.testing.assert_allclose(o, ref, rtol=1e-12, atol=1e-12, err_msg=f"{spec} {op}")
+    outs = nv.simulate("flat", ins, op="sum", grid=2, scale=0.5)
+    np.testing.assert_allclose(outs[0], st.sum(0) * 0.5, rtol=1e-12)
+
+
+def test_unsupported_combinations(nv):
+    ins = [np.ones(8, np.float32)] * 2
+    with pytest.raises(nv.FlexarError):
+        nv.simulate("flat", ins, op="band")   # bitwise on floats (reference: exit(1))
+    ins = [np.ones(8, np.int32)] * 2
+    with pytest.raises(nv.FlexarError):
+        nv.simulate("flat", ins, op="avg")
+
+
+def _bf16_bits(x):
+    import torch
+
+    return torch.from_numpy(x).to(torch.bfloat16).view(torch.int16).numpy().view(np.uint16)
+
+
+def _from_bf16_bits(b):
+    import torch
+
+    return torch.from_numpy(b.view(np.int16)).view(torch.bfloat16).float().numpy()
+
+
+def test_bf16_fp32_accumulation(nv):
+    rng = np.random.default_rng(3)
+    n = 8
+    xs = [rng.standard_normal(5000).astype(np.float32) for _ in range(n)]
+    bits = [_bf16_bits(x) for x in xs]
+    exact = np.sum(np.stack([_from_bf16_bits(b) for b in bits]).astype(np.float64), 0)
+    for spec in ("flat", "oneshot"):  # single reduction stage: exactly one rounding
+        outs = nv.simulate_typed(spec, bits, "bfloat16", grid=2)
+        got = _from_bf16_bits(outs[0])
+        import torch
+
+        want = torch.from_numpy(exact.astype(np.float32)).to(torch.bfloat16).float().numpy()
+        np.testing.assert_array_equal(got, want)
+
+
+def test_bytes_moved_is_bandwidth_optimal(nv):
+    """Remote bytes per rank = 2 (N-1)/N * S for ring/tree (the key structural fact)."""
+    import re
+
+    n, count = 8, 1 << 20
+    for spec in ("flat+push", "flat+pull", "ring", "ring:4", "rhd+push", "tree:2,4+push", "tree:4,2+pull"):
+        dump = nv.plan_dump(spec, 3, n, count)
+        moved = 0
+        for line in dump.splitlines():
+            m = re.match(r"\s+XFER len=(\d+).*\[(.*)\] -> \[(.*)\]", line)
+            if not m:
+                continue
+            ln = int(m.group(1))
+            srcs, dsts = m.group(2), m.group(3)
+            moved += ln * sum(1 for d in dsts.split(", ") if "@3:" not in d)      # remote writes
+            moved += ln * sum(1 for s in srcs.split(" + ") if "@3:" not in s)     # remote reads
+        assert moved == 2 * (n - 1) * count // n, (spec, moved)

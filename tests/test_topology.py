@@ -1,0 +1,90 @@
+"""Topology parsing, enumeration and the cost models (host only).
+
+Reference behaviour pinned from SURVEY.md §2.5/§4.2 (verified by running the
+reference): FT_TOPO unset -> flat {N}; any 1 -> ring; product != N -> error;
+'2,2,2,' failed in the reference (defect D4) and is accepted here.
+"""
+import pytest
+
+
+def test_ft_topo_reference_rules(nv):
+    assert nv.parse_ft_topo(None, 8) == "tree:8"
+    assert nv.parse_ft_topo("", 8) == "tree:8"
+    assert nv.parse_ft_topo("2,2,2", 8) == "tree:2,2,2"
+    assert nv.parse_ft_topo("2 2 2", 8) == "tree:2,2,2"
+    assert nv.parse_ft_topo("2, 2,2", 8) == "tree:2,2,2"
+    assert nv.parse_ft_topo("2,4", 8) == "tree:2,4"
+    assert nv.parse_ft_topo("4,1,2", 8) == "ring"      # any 1 -> ring (mpi_mod.hpp:907-910)
+    assert nv.parse_ft_topo("1", 5) == "ring"
+    assert nv.parse_ft_topo("2,3", 6) == "tree:2,3"
+
+
+def test_ft_topo_d4_fixed(nv):
+    # reference: trailing separator re-pushes the last token -> 'invalid FT_TOPO' exit(1)
+    assert nv.parse_ft_topo("2,2,2,", 8) == "tree:2,2,2"
+    assert nv.parse_ft_topo(",2,,4,", 8) == "tree:2,4"
+
+
+@pytest.mark.parametrize("bad,n", [("2,3", 8), ("0", 8), ("3", 8), ("2,x", 8), ("-2,-4", 8)])
+def test_ft_topo_invalid(nv, bad, n):
+    with pytest.raises(nv.FlexarError):
+        nv.parse_ft_topo(bad, n)
+
+
+def test_factor_count_matches_reference_tool(nv):
+    from allreduce_over_mpi_amd.utils.topology import get_factor_count
+
+    # reference topo_count/factor_count.py: recursive H(n)
+    def ref(num):
+        if num == 0:
+            return 0
+        if num == 1:
+            return 1
+        return sum(ref(num // i) for i in range(2, num + 1) if num % i == 0)
+
+    for n in list(range(0, 65)) + [96, 128, 340]:
+        assert nv.count_factorizations(n) == ref(n) == get_factor_count(n), n
+    # survey: 5 / 9 / 45 reference candidates for N = 8 / 16 / 340 (= H(N) + 1 with [N] duplicated)
+    assert [nv.count_factorizations(n) + 1 for n in (8, 16, 340)] == [5, 9, 45]
+
+
+def test_enumerate_plans(nv):
+    p8 = nv.enumerate_plans(8)
+    assert "tree:8" in p8 and "tree:2,2,2" in p8 and "tree:2,4" in p8 and "tree:4,2" in p8
+    assert "ring" in p8 and "ring:4" in p8 and "oneshot" in p8
+    trees = [p for p in p8 if p.startswith("tree:")]
+    assert len(trees) == nv.count_factorizations(8)
+    p7 = nv.enumerate_plans(7)  # prime: flat tree + rings
+    assert "tree:7" in p7 and "ring:6" in p7
+    assert nv.enumerate_plans(1) == []
+
+
+def test_legacy_cost_model_worked_example(nv):
+    # N = 8, s = 100, 2*2*2 = 3 x 0.008 + 0.105 + 0.595 = 0.724
+    assert nv.legacy_cost([2, 2, 2], 8, 100) == pytest.approx(0.724, abs=1e-9)
+    # reference picks '1*8' (= flat) for N <= 9 at s = 100: flat must be the argmin among trees
+    from allreduce_over_mpi_amd.utils.topology import legacy_best
+
+    assert legacy_best(8, 100)[0] == [8]
+    assert legacy_best(16, 100)[0] == [2, 8]   # survey table: N=16, s=100 -> 2*8
+    assert legacy_best(64, 100)[0] == [8, 8]   # survey table: N=64, s=100 -> 8*8
+
+
+def test_xgmi_selector_prefers_all_links(nv):
+    # On a fully connected 8-GPU mesh the flat stage drives 7 links; it must beat 1-link plans for big buffers.
+    big = 256 << 20
+    assert nv.model_cost_us("flat", 8, big) < nv.model_cost_us("ring", 8, big)
+    assert nv.model_cost_us("flat", 8, big) < nv.model_cost_us("rhd", 8, big)
+    assert nv.select_plan(8, big).startswith("tree:8")
+    # tiny buffers: a single stage (oneshot) beats 2(N-1) ring hops
+    assert nv.model_cost_us("oneshot", 8, 4096) < nv.model_cost_us("ring", 8, 4096)
+    assert nv.select_plan(8, 4096) == "oneshot"
+
+
+def test_algo_spec_errors(nv):
+    with pytest.raises(nv.FlexarError):
+        nv.model_cost_us("rhd", 6, 1e6)        # not a power of two
+    with pytest.raises(nv.FlexarError):
+        nv.model_cost_us("tree:2,2", 8, 1e6)   # product != N
+    with pytest.raises(nv.FlexarError):
+        nv.model_cost_us("bogus", 8, 1e6)
