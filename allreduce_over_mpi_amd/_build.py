@@ -88,5 +88,78 @@ def build(verbose: bool = False, force: bool = False) -> str:
     return LIB_PATH
 
 
+BIN_DIR = os.path.join(REPO, "bin")
+MPI_HOME = os.environ.get("FLEXAR_MPI_HOME", "/opt/conda")
+TOOLS = {
+    # name: (sources, needs MPI, needs RCCL)
+    "flexar_bench": (["bench/flexar_bench.cpp"], True, True),
+    "test_mpi_allreduce": (["tests/cpp/test_mpi_allreduce.cpp"], True, False),
+    "flexar_plan": (["tools/flexar_plan.cpp"], False, False),
+}
+
+
+def mpi_available() -> bool:
+    return os.path.exists(os.path.join(MPI_HOME, "include", "mpi.h")) and \
+        os.path.exists(os.path.join(MPI_HOME, "lib", "libmpi.so.12"))
+
+
+def _mpi_libdir() -> str:
+    """A private dir with only the MPI runtime libs (MPI_HOME/lib also ships an old libstdc++)."""
+    d = os.path.join(BIN_DIR, "mpilib")
+    os.makedirs(d, exist_ok=True)
+    for name in ("libmpi.so.12", "libgfortran.so.4", "libquadmath.so.0"):
+        src = os.path.join(MPI_HOME, "lib", name)
+        dst = os.path.join(d, name)
+        if os.path.exists(src) and not os.path.lexists(dst):
+            os.symlink(src, dst)
+    return d
+
+
+def git_version() -> str:
+    try:
+        return subprocess.run(["git", "-C", REPO, "describe", "--always", "--dirty"], stdout=subprocess.PIPE,
+                              stderr=subprocess.DEVNULL, text=True).stdout.strip() or "unknown"
+    except Exception:
+        return "unknown"
+
+
+def build_tools(names=None, verbose: bool = False):
+    """Build the C++ executables (benchmark driver, MPI test harness, planner CLI) into bin/."""
+    lib = build(verbose=verbose)
+    os.makedirs(BIN_DIR, exist_ok=True)
+    names = names or list(TOOLS)
+    built = {}
+    jobs = []
+    for name in names:
+        srcs, need_mpi, need_rccl = TOOLS[name]
+        if need_mpi and not mpi_available():
+            continue
+        out = os.path.join(BIN_DIR, name)
+        srcp = [os.path.join(REPO, x) for x in srcs]
+        deps = srcp + _deps()
+        if os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps) and \
+                os.path.getmtime(lib) <= os.path.getmtime(out):
+            built[name] = out
+            continue
+        # host-only C++ (HIP runtime API + MPI): the plain host compiler, linked against libamdhip64
+        cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-D__HIP_PLATFORM_AMD__",
+               "-I" + os.path.join(ROCM, "include"), "-I" + INCLUDE, "-DFLEXAR_GIT_VERSION=\"%s\"" % git_version(), *srcp,
+               "-o", out, "-L" + LIB_DIR, "-lflexar", "-Wl,-rpath,$ORIGIN/../allreduce_over_mpi_amd/_lib", "-L" + os.path.join(ROCM, "lib"),
+               "-lamdhip64", "-Wl,-rpath," + os.path.join(ROCM, "lib"), "-lpthread"]
+        if need_mpi:
+            cmd.insert(5, "-I" + os.path.join(MPI_HOME, "include"))
+            d = _mpi_libdir()
+            cmd += [os.path.join(d, "libmpi.so.12"), "-Wl,-rpath,$ORIGIN/mpilib", "-Wl,-rpath-link," + d]
+        if need_rccl:
+            cmd += ["-L" + os.path.join(ROCM, "lib"), "-lrccl"]
+        jobs.append((name, out, cmd))
+    with cf.ThreadPoolExecutor(max(1, min(len(jobs), 4))) as ex:
+        for (name, out, _), res in zip(jobs, ex.map(lambda j: _run(j[2]), jobs)):
+            built[name] = out
+    return built
+
+
 if __name__ == "__main__":
     build(verbose=True, force="--force" in sys.argv)
+    if "--tools" in sys.argv:
+        print(build_tools(verbose=True))

@@ -132,6 +132,10 @@ int flexar_reduce(void* dst, const void* const* srcs, int nsrc, size_t count, in
 int flexar_reduce_host(void* dst, const void* const* srcs, int nsrc, size_t count, int dtype, int op,
                        float scale);
 
+/* ---- helpers --------------------------------------------------------------- */
+int flexar_pointer_is_device(const void* p); /* 1 if p is device memory */
+int flexar_current_device(void);
+
 /* ---- host-only planning utilities (no GPU needed) ------------------------ */
 /* Parse an FT_TOPO string for nranks with the reference's rules (any 1 -> ring, unset -> flat,
  * product must equal nranks; trailing/duplicate separators tolerated). Writes a canonical spec

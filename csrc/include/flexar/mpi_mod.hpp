@@ -1,0 +1,505 @@
+// flexar MPI compatibility layer: MPI_Allreduce_FT for MPI applications.
+//
+// Reference: allreduce_over_mpi/mpi_mod.hpp (the whole header), whose entry
+//   int MPI_Allreduce_FT(const void*, void*, int, MPI_Datatype, MPI_Op, MPI_Comm)
+// (mpi_mod.hpp:1167-1221) reduces HOST buffers with MPI_Isend/Irecv +
+// MPI_Barrier per stage + an OpenMP reduce, topology from FT_TOPO.
+//
+// Same signature and FT_TOPO semantics here, new mechanics:
+//  * DEVICE buffers (hipMalloc'd): routed to the flexar GPU communicator —
+//    workspaces exchanged once with MPI_Allgather, then one executor kernel
+//    per call over xGMI (see flexar.h). Cached per MPI_Comm (attribute).
+//  * HOST buffers, all ranks on one node: the same op programs executed by the
+//    host engine (host_exec.hpp) over an MPI-3 shared-memory window — direct
+//    loads/stores into peers' staging + atomic epoch flags; no barriers.
+//  * HOST buffers across nodes: the push-form op program translated to
+//    point-to-point messages, ONE coalesced message per (peer, stage) instead
+//    of one MPI_Isend per block (reference defect: mpi_mod.hpp:679-702).
+// Fixed reference defects: D1 (leaked requests), D2 (OOB src table), D3
+// (fan-in > 20 garbage), D4 (FT_TOPO trailing separator), D7 (count is still
+// `int` in the compatible signature; MPI_Allreduce_FT_large takes size_t),
+// D8 (per-call allocations/getenv: plans and windows are cached).
+// Define FLEXAR_MPI_INTERPOSE before including to also shadow MPI_Allreduce
+// in this translation unit (the reference's default integration mode).
+#pragma once
+
+#include <mpi.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "flexar/cost_model.hpp"
+#include "flexar/flexar.h"
+#include "flexar/host_exec.hpp"
+#include "flexar/planner.hpp"
+
+extern "C" int flexar_pointer_is_device(const void* p);  // libflexar: hipPointerGetAttributes
+
+namespace flexar {
+namespace mpi {
+
+inline int dtype_of(MPI_Datatype dt) {
+  if (dt == MPI_FLOAT) return FLEXAR_FLOAT32;
+  if (dt == MPI_DOUBLE) return FLEXAR_FLOAT64;
+  if (dt == MPI_INT8_T || dt == MPI_SIGNED_CHAR || dt == MPI_CHAR) return FLEXAR_INT8;
+  if (dt == MPI_UINT8_T || dt == MPI_UNSIGNED_CHAR || dt == MPI_BYTE) return FLEXAR_UINT8;
+  if (dt == MPI_INT16_T || dt == MPI_SHORT) return FLEXAR_INT16;
+  if (dt == MPI_UINT16_T || dt == MPI_UNSIGNED_SHORT) return FLEXAR_UINT16;
+  if (dt == MPI_INT32_T || dt == MPI_INT) return FLEXAR_INT32;
+  if (dt == MPI_UINT32_T || dt == MPI_UNSIGNED) return FLEXAR_UINT32;
+  if (dt == MPI_INT64_T || dt == MPI_LONG_LONG_INT || dt == MPI_LONG_LONG || dt == MPI_LONG) return FLEXAR_INT64;
+  if (dt == MPI_UINT64_T || dt == MPI_UNSIGNED_LONG_LONG || dt == MPI_UNSIGNED_LONG) return FLEXAR_UINT64;
+  if (dt == MPI_C_BOOL) return FLEXAR_BOOL;
+  return -1;
+}
+
+inline int op_of(MPI_Op op) {
+  if (op == MPI_SUM) return FLEXAR_SUM;
+  if (op == MPI_PROD) return FLEXAR_PROD;
+  if (op == MPI_MAX) return FLEXAR_MAX;
+  if (op == MPI_MIN) return FLEXAR_MIN;
+  if (op == MPI_BAND) return FLEXAR_BAND;
+  if (op == MPI_BOR) return FLEXAR_BOR;
+  if (op == MPI_BXOR) return FLEXAR_BXOR;
+  return -1;
+}
+
+// Persistent worker pool: workgroup g (1..G-1) of the host engine runs on worker g-1.
+class Pool {
+ public:
+  explicit Pool(int n) : n_(n) {
+    for (int i = 0; i < n_; ++i) th_.emplace_back([this, i] { loop(i); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int size() const { return n_; }
+  // run fn(i) on workers 0..k-1 and fn(k) on the caller... caller passes its own share separately
+  template <typename F>
+  void run(int k, F&& fn) {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      job_ = fn;
+      active_ = k;
+      pending_ = k;
+      ++gen_;
+    }
+    cv_.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> lk(m_);
+    done_cv_.wait(lk, [&] { return pending_ == 0; });
+  }
+
+ private:
+  void loop(int i) {
+    int seen = 0;
+    for (;;) {
+      std::function<void(int)> job;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (stop_) return;
+        if (i >= active_) continue;
+        job = job_;
+      }
+      job(i);
+      {
+        std::lock_guard<std::mutex> lk(m_);
+        if (--pending_ == 0) done_cv_.notify_all();
+      }
+    }
+  }
+  int n_;
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_cv_;
+  std::function<void(int)> job_;
+  int gen_ = 0, active_ = 0, pending_ = 0;
+  bool stop_ = false;
+};
+
+constexpr uint32_t kHostMaxGrid = 16;
+
+// Per-rank translation of the push-form program into coalesced p2p messages.
+struct P2PPlan {
+  // for every peer: the (off, len) STG regions it writes into this rank, grouped by the slot of
+  // the SIGNAL that publishes them, in program order (the payload order of its message).
+  std::map<std::pair<int, uint32_t>, std::vector<std::pair<uint64_t, uint64_t>>> incoming;
+  std::map<std::pair<int, uint32_t>, uint64_t> incoming_elems;
+  std::map<std::pair<int, uint32_t>, uint64_t> outgoing_elems;
+};
+
+struct HostComm {
+  MPI_Comm comm = MPI_COMM_NULL;
+  int rank = 0, size = 1;
+  bool shared = false;
+  MPI_Win win = MPI_WIN_NULL;
+  size_t cap = 0;           // staging bytes per parity
+  size_t flag_bytes = 0;
+  std::vector<char*> stg;   // per rank staging base (shared mode)
+  std::vector<std::atomic<uint64_t>*> flags;
+  std::vector<uint64_t> epochs = std::vector<uint64_t>(kHostMaxGrid, 0);
+  std::map<std::string, std::unique_ptr<Program>> plans;
+  std::map<std::string, std::unique_ptr<P2PPlan>> p2p;
+  std::vector<char> p2p_stg, outbox, inbox;
+  std::unique_ptr<Pool> pool;
+  XgmiModel model = XgmiModel::from_env();
+  int threads = 1;
+
+  ~HostComm() {
+    if (win != MPI_WIN_NULL) MPI_Win_free(&win);
+    if (comm != MPI_COMM_NULL) MPI_Comm_free(&comm);
+  }
+
+  void init(MPI_Comm parent) {
+    MPI_Comm_dup(parent, &comm);
+    MPI_Comm_rank(comm, &rank);
+    MPI_Comm_size(comm, &size);
+    MPI_Comm node;
+    MPI_Comm_split_type(comm, MPI_COMM_TYPE_SHARED, rank, MPI_INFO_NULL, &node);
+    int nsz = 0;
+    MPI_Comm_size(node, &nsz);
+    MPI_Comm_free(&node);
+    shared = (nsz == size) && getenv("FLEXAR_MPI_P2P") == nullptr;
+    const char* t = getenv("FLEXAR_HOST_THREADS");
+    threads = t ? atoi(t) : 1;
+    if (threads < 1) threads = 1;
+    if (threads > (int)kHostMaxGrid) threads = kHostMaxGrid;
+    if (threads > 1) pool.reset(new Pool(threads - 1));
+  }
+
+  // (Re)allocate the shared window so one parity half holds `need` bytes. Collective.
+  void ensure_window(size_t need) {
+    if (!shared || (win != MPI_WIN_NULL && need <= cap)) return;
+    if (win != MPI_WIN_NULL) MPI_Win_free(&win);
+    cap = std::max<size_t>(need, size_t(1) << 20);
+    cap = (cap + 4095) / 4096 * 4096;
+    flag_bytes = (size_t)kMaxSlots * size * kHostMaxGrid * sizeof(uint64_t);
+    flag_bytes = (flag_bytes + 4095) / 4096 * 4096;
+    char* base = nullptr;
+    MPI_Win_allocate_shared((MPI_Aint)(flag_bytes + 2 * cap), 1, MPI_INFO_NULL, comm, &base, &win);
+    memset(base, 0, flag_bytes);
+    stg.assign(size, nullptr);
+    flags.assign(size, nullptr);
+    for (int r = 0; r < size; ++r) {
+      MPI_Aint sz;
+      int du;
+      char* p = nullptr;
+      MPI_Win_shared_query(win, r, &sz, &du, &p);
+      flags[r] = reinterpret_cast<std::atomic<uint64_t>*>(p);
+      stg[r] = p + flag_bytes;
+    }
+    std::fill(epochs.begin(), epochs.end(), 0);
+    MPI_Barrier(comm);  // flags zeroed everywhere before anyone signals
+  }
+};
+
+inline std::string plan_key(const AlgoSpec& s, size_t count, size_t es, float fs) {
+  char b[256];
+  uint32_t u;
+  memcpy(&u, &fs, 4);
+  snprintf(b, sizeof(b), "%s|%zu|%zu|%08x", s.str().c_str(), count, es, u);
+  return b;
+}
+
+inline int resolve_algo(HostComm& h, double bytes, AlgoSpec* s) {
+  std::string err;
+  const char* a = getenv("FLEXAR_ALGO");
+  if (a && *a) {
+    if (!parse_algo(a, h.size, s, &err)) { fprintf(stderr, "[flexar] bad FLEXAR_ALGO: %s\n", err.c_str()); return 1; }
+  } else if (!parse_ft_topo(getenv("FT_TOPO"), h.size, s, &err)) {  // reference semantics, read per call
+    fprintf(stderr, "[flexar] %s\n", err.c_str());
+    return 1;
+  }
+  if (s->kind == AlgoKind::AUTO) *s = select_plan(h.model, h.size, bytes);
+  if (s->kind == AlgoKind::TREE && (!h.shared || s->ag == AgMode::AUTO)) s->ag = AgMode::PUSH;
+  return 0;
+}
+
+template <typename T, typename OP>
+struct ShmRun {
+  static int run(HostComm& h, const Program& P, const void* in, void* out, int grid) {
+    HostExecCtx c;
+    c.rank = h.rank;
+    c.local[BUF_IN] = (char*)in;
+    c.local[BUF_OUT] = (char*)out;
+    c.local[BUF_STG] = h.stg[h.rank];
+    c.peer_stg = h.stg;
+    c.peer_flags = h.flags;
+    c.ranks_stride = h.size;
+    c.blocks_stride = kHostMaxGrid;
+    c.stg_half_bytes = h.cap;
+    std::atomic<int> rc{0};
+    auto body = [&](int g) {
+      uint64_t e = ++h.epochs[g];
+      int x = HostExec<T, OP>::run(P, c, (uint32_t)g, (uint32_t)grid, e);
+      if (x) rc.store(x);
+    };
+    if (grid > 1) h.pool->run(grid - 1, [&](int i) { body(i + 1); });
+    body(0);
+    if (grid > 1) h.pool->wait();
+    return rc.load();
+  }
+};
+
+// Build the p2p message plan for rank h.rank: replay every peer's program to learn what it
+// writes into us and under which SIGNAL slot it publishes it.
+inline std::unique_ptr<P2PPlan> build_p2p(HostComm& h, const AlgoSpec& s, size_t count, size_t es, float fs) {
+  std::unique_ptr<P2PPlan> pp(new P2PPlan);
+  std::string err;
+  for (int p = 0; p < h.size; ++p) {
+    Program Q;
+    Planner pl(h.size, p, count, (uint32_t)es, fs);
+    pl.build(s, &Q, &err);
+    std::map<int, std::vector<std::pair<uint64_t, uint64_t>>> pend;  // dst rank -> regions since its last signal
+    for (const Op& o : Q.ops) {
+      if (o.kind == OP_XFER) {
+        for (int d = 0; d < o.ndst; ++d)
+          if (o.dst[d].rank != (uint16_t)p) pend[o.dst[d].rank].push_back({o.dst[d].off, o.len});
+      } else if (o.kind == OP_SIGNAL) {
+        for (int k = 0; k < o.npeers; ++k) {
+          int q = o.peers[k];
+          uint64_t tot = 0;
+          for (auto& rg : pend[q]) tot += rg.second;
+          if (q == h.rank) {
+            pp->incoming[{p, o.slot}] = pend[q];
+            pp->incoming_elems[{p, o.slot}] = tot;
+          }
+          if (p == h.rank) pp->outgoing_elems[{q, o.slot}] = tot;
+          pend[q].clear();
+        }
+      }
+    }
+  }
+  return pp;
+}
+
+template <typename T, typename OP>
+struct P2PRun {
+  static int run(HostComm& h, const Program& P, const P2PPlan& pp, const void* in, void* out) {
+    const size_t es = sizeof(T);
+    char* stg = h.p2p_stg.data();
+    auto addr = [&](const Loc& l) -> char* {
+      if (l.buf == BUF_STG) return stg + l.off * es;
+      return (l.buf == BUF_IN ? (char*)in : (char*)out) + l.off * es;
+    };
+    // outbox: per-peer running buffers (sized by the plan), kept alive until Waitall
+    std::map<int, std::vector<char>> box;
+    std::vector<MPI_Request> reqs;
+    std::vector<std::vector<char>> sent;
+    for (const Op& o : P.ops) {
+      if (o.kind == OP_XFER) {
+        const T* srcs[kMaxSrc];
+        T* dsts[kMaxDst];
+        int nloc = 0;
+        for (int k = 0; k < o.nsrc; ++k) srcs[k] = (const T*)addr(o.src[k]);
+        std::vector<int> remote;
+        for (int d = 0; d < o.ndst; ++d) {
+          if (o.dst[d].rank == (uint16_t)h.rank) dsts[nloc++] = (T*)addr(o.dst[d]);
+          else remote.push_back(o.dst[d].rank);
+        }
+        for (int q : remote) {
+          auto& b = box[q];
+          size_t at = b.size();
+          b.resize(at + o.len * es);
+          dsts[nloc++] = (T*)(b.data() + at);
+        }
+        host_reduce_span<T, OP>(dsts, nloc, srcs, o.nsrc, o.len, o.scale);
+      } else if (o.kind == OP_SIGNAL) {
+        for (int k = 0; k < o.npeers; ++k) {
+          int q = o.peers[k];
+          sent.emplace_back(std::move(box[q]));
+          box[q].clear();
+          reqs.emplace_back();
+          MPI_Isend(sent.back().data(), (int)sent.back().size(), MPI_BYTE, q, (int)o.slot, h.comm, &reqs.back());
+        }
+      } else if (o.kind == OP_WAIT) {
+        for (int k = 0; k < o.npeers; ++k) {
+          int p = o.peers[k];
+          auto key = std::make_pair(p, o.slot);
+          auto it = pp.incoming.find(key);
+          uint64_t tot = pp.incoming_elems.count(key) ? pp.incoming_elems.at(key) : 0;
+          h.inbox.resize(std::max<size_t>(h.inbox.size(), tot * es + 1));
+          MPI_Recv(h.inbox.data(), (int)(tot * es), MPI_BYTE, p, (int)o.slot, h.comm, MPI_STATUS_IGNORE);
+          if (it != pp.incoming.end()) {
+            size_t at = 0;
+            for (auto& rg : it->second) {
+              memcpy(stg + rg.first * es, h.inbox.data() + at, rg.second * es);
+              at += rg.second * es;
+            }
+          }
+        }
+      }
+    }
+    if (!reqs.empty()) MPI_Waitall((int)reqs.size(), reqs.data(), MPI_STATUSES_IGNORE);  // D1: every send completed
+    return 0;
+  }
+};
+
+struct Dispatch {
+  template <typename T, typename OP>
+  static int run(HostComm& h, const Program& P, const P2PPlan* pp, const void* in, void* out, int grid) {
+    if (pp) return P2PRun<T, OP>::run(h, P, *pp, in, out);
+    return ShmRun<T, OP>::run(h, P, in, out, grid);
+  }
+};
+
+inline int keyval() {
+  static int kv = MPI_KEYVAL_INVALID;
+  if (kv == MPI_KEYVAL_INVALID) {
+    auto del = [](MPI_Comm, int, void* attr, void*) -> int {
+      delete static_cast<HostComm*>(attr);
+      return MPI_SUCCESS;
+    };
+    MPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, del, &kv, nullptr);
+  }
+  return kv;
+}
+
+inline HostComm* host_comm(MPI_Comm comm) {
+  int flag = 0;
+  void* v = nullptr;
+  MPI_Comm_get_attr(comm, keyval(), &v, &flag);
+  if (flag) return static_cast<HostComm*>(v);
+  HostComm* h = new HostComm;
+  h->init(comm);
+  MPI_Comm_set_attr(comm, keyval(), h);
+  return h;
+}
+
+// ---- device buffers: flexar GPU communicator bootstrapped over MPI ------------------------------
+struct DevHolder {
+  flexar_comm_t c = nullptr;
+  ~DevHolder() {
+    if (c) flexar_comm_destroy(c);
+  }
+};
+inline int dev_keyval() {
+  static int kv = MPI_KEYVAL_INVALID;
+  if (kv == MPI_KEYVAL_INVALID) {
+    auto del = [](MPI_Comm, int, void* attr, void*) -> int {
+      delete static_cast<DevHolder*>(attr);
+      return MPI_SUCCESS;
+    };
+    MPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, del, &kv, nullptr);
+  }
+  return kv;
+}
+extern "C" int flexar_current_device(void);
+inline flexar_comm_t device_comm(MPI_Comm comm) {
+  int flag = 0;
+  void* v = nullptr;
+  MPI_Comm_get_attr(comm, dev_keyval(), &v, &flag);
+  if (flag) return static_cast<DevHolder*>(v)->c;
+  int rank, size;
+  MPI_Comm_rank(comm, &rank);
+  MPI_Comm_size(comm, &size);
+  DevHolder* d = new DevHolder;
+  int rc = flexar_comm_create(rank, size, flexar_current_device(), 0, &d->c);
+  if (rc) { fprintf(stderr, "[flexar] comm_create: %s\n", flexar_last_error()); abort(); }
+  size_t hs = flexar_handle_size();
+  std::vector<char> mine(hs), all(hs * size);
+  flexar_comm_export(d->c, mine.data());
+  MPI_Allgather(mine.data(), (int)hs, MPI_BYTE, all.data(), (int)hs, MPI_BYTE, comm);
+  if (flexar_comm_connect(d->c, all.data())) { fprintf(stderr, "[flexar] connect: %s\n", flexar_last_error()); abort(); }
+  MPI_Barrier(comm);
+  MPI_Comm_set_attr(comm, dev_keyval(), d);
+  return d->c;
+}
+
+inline int allreduce(const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype datatype, MPI_Op mop,
+                     MPI_Comm comm) {
+  const int dt = dtype_of(datatype), op = op_of(mop);
+  if (dt < 0 || op < 0 || !op_supported(dt, op)) {
+    fprintf(stderr, "[flexar] MPI_Allreduce_FT: unsupported datatype/op\n");
+    return MPI_ERR_OP;
+  }
+  const bool in_place = (sendbuf == MPI_IN_PLACE);
+  const void* in = in_place ? recvbuf : sendbuf;
+  int size;
+  MPI_Comm_size(comm, &size);
+  const size_t es = dtype_size(dt);
+  if (count == 0) return MPI_SUCCESS;
+  if (flexar_pointer_is_device(recvbuf)) {
+    flexar_comm_t c = device_comm(comm);
+    int rc = flexar_allreduce(c, in, recvbuf, count, dt, op, nullptr);
+    if (rc) { fprintf(stderr, "[flexar] allreduce: %s\n", flexar_last_error()); return MPI_ERR_OTHER; }
+    return MPI_SUCCESS;  // stream-ordered on the default stream, like a CUDA-aware MPI
+  }
+  if (size <= 1) {  // reference: memcpy unless in place (mpi_mod.hpp:1181-1188)
+    if (!in_place) memcpy(recvbuf, sendbuf, count * es);
+    return MPI_SUCCESS;
+  }
+  HostComm* h = host_comm(comm);
+  AlgoSpec s;
+  if (resolve_algo(*h, (double)count * es, &s)) return MPI_ERR_ARG;
+  const std::string key = plan_key(s, count, es, 1.0f);
+  auto it = h->plans.find(key);
+  if (it == h->plans.end()) {
+    std::unique_ptr<Program> P(new Program);
+    Planner pl(h->size, h->rank, count, (uint32_t)es, 1.0f);
+    std::string err;
+    if (!pl.build(s, P.get(), &err)) { fprintf(stderr, "[flexar] %s\n", err.c_str()); return MPI_ERR_ARG; }
+    it = h->plans.emplace(key, std::move(P)).first;
+  }
+  const Program& P = *it->second;
+  const P2PPlan* pp = nullptr;
+  int grid = 1;
+  if (h->shared) {
+    h->ensure_window(P.stg_elems * es);
+    uint64_t bytes = count * es;
+    grid = h->threads;
+    while (grid > 1 && bytes / grid < (1u << 20)) --grid;  // >= 1 MiB per host workgroup
+    grid = std::max<int>(grid, (int)P.nchan);
+    grid = (grid + P.nchan - 1) / P.nchan * P.nchan;
+    if (grid > (int)kHostMaxGrid || (grid > 1 && (!h->pool || h->pool->size() < grid - 1))) {
+      if (grid > 1 && (!h->pool || h->pool->size() < grid - 1)) h->pool.reset(new Pool(grid - 1));
+    }
+  } else {
+    auto jt = h->p2p.find(key);
+    if (jt == h->p2p.end()) jt = h->p2p.emplace(key, build_p2p(*h, s, count, es, 1.0f)).first;
+    pp = jt->second.get();
+    h->p2p_stg.resize(std::max<size_t>(h->p2p_stg.size(), P.stg_elems * es + 64));
+  }
+  int rc = dispatch_dtype_op<Dispatch>(dt, op, *h, P, pp, in, recvbuf, grid);
+  return rc == 0 ? MPI_SUCCESS : MPI_ERR_OTHER;
+}
+
+}  // namespace mpi
+}  // namespace flexar
+
+// ---- public entry points ----------------------------------------------------------------------
+inline int MPI_Allreduce_FT(const void* sendbuf, void* recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
+                            MPI_Comm comm) {
+  if (count < 0) return MPI_ERR_COUNT;
+  return flexar::mpi::allreduce(sendbuf, recvbuf, (size_t)count, datatype, op, comm);
+}
+// size_t count: a 4 GiB bf16 tensor fits (defect D7).
+inline int MPI_Allreduce_FT_large(const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype datatype,
+                                  MPI_Op op, MPI_Comm comm) {
+  return flexar::mpi::allreduce(sendbuf, recvbuf, count, datatype, op, comm);
+}
+
+#ifdef FLEXAR_MPI_INTERPOSE
+// Route this translation unit's MPI_Allreduce calls to flexar (reference mpi_mod.hpp:1169-1171 shadowed
+// the symbol with a static function, which conflicts with mpi.h's extern declaration; a macro does not).
+#define MPI_Allreduce MPI_Allreduce_FT
+#endif

@@ -542,6 +542,23 @@ int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
   return 0;
 }
 
+// ---- pointer / device helpers (used by the MPI compatibility layer) ---------------------------
+int flexar_pointer_is_device(const void* p) {
+  if (!p) return 0;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // host pointers unknown to HIP report an error: clear it
+    return 0;
+  }
+  return a.type == hipMemoryTypeDevice ? 1 : 0;
+}
+
+int flexar_current_device(void) {
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) return 0;
+  return d;
+}
+
 // ---- standalone reduction kernel --------------------------------------------------------------
 int flexar_reduce(void* dst, const void* const* srcs, int nsrc, size_t count, int dtype, int op, float scale,
                   void* stream) {

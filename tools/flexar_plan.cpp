@@ -1,0 +1,101 @@
+// flexar_plan — the offline topology tool of the reference, rebuilt on the
+// runtime's own planner/selector (so the tool and the library cannot disagree).
+//
+// Reference: cost_model/main.cpp:1-27 (sweep N = 1..999 -> numofstru.csv),
+// CostModel.h (argmin printout), ChooseWidth.h (prime N -> N+1 / N-1 structures),
+// PrintTreeStructure.h ("a*b*c" printing), timer.h (stopwatch).
+//
+//   flexar_plan model N [bytes]      every candidate plan: reference cost (chunk = bytes/1MiB) and
+//                                    xGMI model cost (us); marks both argmins
+//   flexar_plan choose N             reference ChooseWidth: structures for N (and N +- 1 if N is prime)
+//   flexar_plan sweep [NMAX]         reference main.cpp: "#structures,microseconds" per N (CSV to stdout)
+//   flexar_plan dump SPEC N RANK [COUNT]   per-rank op program (Operations::print_ops equivalent)
+//   flexar_plan select N BYTES       the runtime's choice
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "flexar/cost_model.hpp"
+#include "flexar/planner.hpp"
+#include "flexar/topology.hpp"
+
+using namespace flexar;
+
+static std::string star(const std::vector<int>& w) {
+  std::string s;
+  for (size_t i = 0; i < w.size(); ++i) s += (i ? "*" : "") + std::to_string(w[i]);
+  return s;
+}
+
+static int usage() {
+  fprintf(stderr,
+          "usage: flexar_plan model N [bytes] | choose N | sweep [NMAX] | dump SPEC N RANK [COUNT] | select N BYTES\n");
+  return 2;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) return usage();
+  std::string cmd = argv[1];
+  XgmiModel m = XgmiModel::from_env();
+  if (cmd == "model" && argc >= 3) {
+    int n = atoi(argv[2]);
+    double bytes = argc > 3 ? atof(argv[3]) : 100.0 * (1 << 20);
+    double chunk = bytes / (1 << 20);
+    printf("%-22s %14s %14s\n", "plan", "legacy_cost", "xgmi_us");
+    std::string best_l, best_x;
+    double bl = 1e300, bx = 1e300;
+    for (auto& s : enumerate_plans(n)) {
+      double x = m.cost_us(s, n, bytes);
+      double l = s.kind == AlgoKind::TREE ? legacy_cost(s.widths, n, chunk) : -1;
+      printf("%-22s %14.4f %14.2f\n", s.str().c_str(), l, x);
+      if (l >= 0 && l < bl) bl = l, best_l = star(s.widths);
+      if (x < bx) bx = x, best_x = s.str();
+    }
+    printf("the optimized tree structure for %d total nodes should be (reference model): %s\n", n, best_l.c_str());
+    printf("xGMI runtime model choice for %.0f bytes: %s (%.2f us)\n", bytes, best_x.c_str(), bx);
+    return 0;
+  }
+  if (cmd == "choose" && argc >= 3) {
+    int n = atoi(argv[2]);
+    auto show = [](int k, const char* suffix) {
+      for (auto& w : ordered_factorizations(k)) printf("%s%s\n", star(w).c_str(), suffix);
+    };
+    if (!is_prime(n)) show(n, "");
+    show(n + 1, "-1");  // one lonely rank short of the structure (reference PrintTreeStructure_right)
+    show(n - 1, "+1");  // one lonely rank beyond it
+    return 0;
+  }
+  if (cmd == "sweep") {
+    int nmax = argc > 2 ? atoi(argv[2]) : 999;
+    printf("N,structures,microseconds\n");
+    for (int n = 1; n <= nmax; ++n) {
+      auto t0 = std::chrono::steady_clock::now();
+      auto plans = enumerate_plans(n);
+      double best = 1e300;
+      for (auto& s : plans) best = std::min(best, m.cost_us(s, n, 100.0 * (1 << 20)));
+      double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+      printf("%d,%zu,%.1f\n", n, plans.size(), us);
+    }
+    return 0;
+  }
+  if (cmd == "dump" && argc >= 5) {
+    AlgoSpec s;
+    std::string err;
+    int n = atoi(argv[3]), r = atoi(argv[4]);
+    uint64_t count = argc > 5 ? strtoull(argv[5], nullptr, 0) : 1 << 20;
+    if (!parse_algo(argv[2], n, &s, &err)) { fprintf(stderr, "%s\n", err.c_str()); return 1; }
+    if (s.kind == AlgoKind::AUTO) s = select_plan(m, n, count * 4.0);
+    Program P;
+    Planner pl(n, r, count, 4, 1.0f);
+    if (!pl.build(s, &P, &err)) { fprintf(stderr, "%s\n", err.c_str()); return 1; }
+    fputs(dump_program(P, r).c_str(), stdout);
+    return 0;
+  }
+  if (cmd == "select" && argc >= 4) {
+    printf("%s\n", select_plan(m, atoi(argv[2]), atof(argv[3])).str().c_str());
+    return 0;
+  }
+  return usage();
+}
