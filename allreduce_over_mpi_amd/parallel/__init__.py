@@ -1,1 +1,1 @@
-from .comm import Communicator, LocalGroup  # noqa: F401
+from .comm import Communicator, LocalGroup, store_exchange  # noqa: F401

@@ -1,0 +1,213 @@
+"""torch.distributed backend ``"flexar"`` and a DDP communication hook.
+
+The reference integrates by shadowing ``MPI_Allreduce`` in every translation
+unit that includes its header (allreduce_over_mpi/mpi_mod.hpp:1169-1171), so an
+MPI-based DL framework transparently uses FlexTree for gradient allreduce. The
+PyTorch-ROCm equivalent is a c10d backend:
+
+    import allreduce_over_mpi_amd.parallel.backend  # registers "flexar"
+    dist.init_process_group("flexar", ...)            # or "cuda:flexar,cpu:gloo"
+
+* ``allreduce`` / ``allreduce_coalesced`` on ROCm tensors run the flexar executor
+  kernel (stream-ordered on the current stream, no host sync);
+* every other collective (broadcast, all-gather, reduce-scatter, all-to-all,
+  barrier, send/recv) and unsupported dtypes/ops delegate to an internal RCCL
+  group (``FLEXAR_PG_FALLBACK=nccl``, default) or gloo; CPU tensors use gloo.
+
+``flexar_allreduce_hook`` is the lighter-weight alternative: keep RCCL as the
+process group and route only DDP's gradient buckets through flexar.
+"""
+from __future__ import annotations
+
+import os
+from datetime import timedelta
+
+import torch
+import torch.distributed as dist
+from torch._C._distributed_c10d import _create_work_from_future
+from torch._C._distributed_c10d import (AllgatherOptions, AllreduceCoalescedOptions, AllreduceOptions, AllToAllOptions,
+                                        BarrierOptions, BroadcastOptions, ReduceScatterOptions)
+
+from .. import _native as nv
+from .comm import Communicator, store_exchange
+
+_FLEXAR_DTYPES = {torch.float32, torch.float16, torch.bfloat16, torch.float64, torch.float8_e4m3fn,
+                  torch.float8_e5m2, torch.int8, torch.uint8, torch.int16, torch.int32, torch.int64, torch.bool}
+
+
+def _redop_name(op) -> str | None:
+    R = dist.ReduceOp
+    table = [(R.SUM, "sum"), (R.AVG, "avg"), (R.PRODUCT, "prod"), (R.MIN, "min"), (R.MAX, "max"),
+             (R.BAND, "band"), (R.BOR, "bor"), (R.BXOR, "bxor")]
+    for k, v in table:
+        try:
+            if op == k:
+                return v
+        except Exception:
+            pass
+    return None
+
+
+def _done_work(result):
+    fut = torch.futures.Future()
+    fut.set_result(result)
+    return _create_work_from_future(fut)
+
+
+class FlexarProcessGroup(dist.ProcessGroup):
+    """c10d ProcessGroup whose device allreduce is the flexar executor kernel."""
+
+    def __init__(self, store, rank: int, world_size: int, timeout: timedelta):
+        super().__init__(rank, world_size)
+        self._rank, self._world = rank, world_size
+        self._store = store
+        self._timeout = timeout
+        self._comm: Communicator | None = None
+        self._gloo = dist.ProcessGroupGloo(dist.PrefixStore("flexar_gloo/", store), rank, world_size, timeout)
+        self._fallback_kind = os.environ.get("FLEXAR_PG_FALLBACK", "nccl").lower()
+        self._gpu_fallback = None
+        self.algo = os.environ.get("FLEXAR_ALGO") or None
+        self.stats = {"flexar_allreduce": 0, "fallback": 0}
+
+    # ------------------------------------------------------------------ plumbing
+    def getBackendName(self):
+        return "flexar"
+
+    def size(self):
+        return self._world
+
+    def rank(self):
+        return self._rank
+
+    def __repr__(self):
+        return f"FlexarProcessGroup(rank={self._rank}, size={self._world})"
+
+    def comm(self, device: int | None = None) -> Communicator:
+        if self._comm is None:
+            dev = torch.cuda.current_device() if device is None else device
+            self._comm = Communicator(device=dev, rank=self._rank, world_size=self._world,
+                                      exchange=store_exchange(self._store, self._rank, self._world, "flexar_comm"))
+        return self._comm
+
+    def _fallback(self, tensors):
+        if tensors and tensors[0].is_cuda:
+            if self._gpu_fallback is None:
+                pre = dist.PrefixStore("flexar_fb/", self._store)
+                if self._fallback_kind == "gloo":
+                    self._gpu_fallback = dist.ProcessGroupGloo(pre, self._rank, self._world, self._timeout)
+                else:
+                    opts = dist.ProcessGroupNCCL.Options()
+                    self._gpu_fallback = dist.ProcessGroupNCCL(pre, self._rank, self._world, opts)
+            self.stats["fallback"] += 1
+            return self._gpu_fallback
+        return self._gloo
+
+    # ------------------------------------------------------------------ allreduce (flexar)
+    def _flexar_ok(self, tensors, opname):
+        return (opname is not None and all(t.is_cuda and t.is_contiguous() and t.dtype in _FLEXAR_DTYPES
+                                           for t in tensors)
+                and nv.lib() is not None and (opname != "avg" or tensors[0].is_floating_point())
+                and not (opname in ("band", "bor", "bxor") and tensors[0].is_floating_point()))
+
+    def allreduce(self, tensor_list, opts=AllreduceOptions()):
+        opname = _redop_name(opts.reduceOp)
+        if not self._flexar_ok(tensor_list, opname):
+            return self._fallback(tensor_list).allreduce(tensor_list, opts)
+        comm = self.comm(tensor_list[0].device.index)
+        for t in tensor_list:
+            if t.dtype == torch.bool:
+                t8 = t.view(torch.uint8)
+                boolop = {"sum": "max", "max": "max", "bor": "max", "avg": "max", "prod": "min", "min": "min",
+                          "band": "min", "bxor": "bxor"}[opname]
+                comm.all_reduce(t8, op=boolop, algo=self.algo)
+            else:
+                comm.all_reduce(t, op=opname, algo=self.algo)
+            self.stats["flexar_allreduce"] += 1
+        return _done_work(tensor_list)
+
+    def allreduce_coalesced(self, tensor_list, opts=AllreduceCoalescedOptions()):
+        o = AllreduceOptions()
+        o.reduceOp = opts.reduceOp
+        return self.allreduce(tensor_list, o)
+
+    # ------------------------------------------------------------------ delegated collectives
+    def barrier(self, opts=BarrierOptions()):
+        return self._gloo.barrier(opts)
+
+    def broadcast(self, tensor_list, opts=BroadcastOptions()):
+        return self._fallback(tensor_list).broadcast(tensor_list, opts)
+
+    def allgather(self, output_tensors, input_tensor, opts=AllgatherOptions()):
+        return self._fallback(input_tensor).allgather(output_tensors, input_tensor, opts)
+
+    def _allgather_base(self, output_tensor, input_tensor, opts=AllgatherOptions()):
+        return self._fallback([input_tensor])._allgather_base(output_tensor, input_tensor, opts)
+
+    def allgather_into_tensor_coalesced(self, output_tensors, input_tensors, opts=AllgatherOptions()):
+        return self._fallback(input_tensors).allgather_into_tensor_coalesced(output_tensors, input_tensors, opts)
+
+    def reduce_scatter(self, output_tensors, input_tensors, opts=ReduceScatterOptions()):
+        return self._fallback(output_tensors).reduce_scatter(output_tensors, input_tensors, opts)
+
+    def _reduce_scatter_base(self, output_tensor, input_tensor, opts=ReduceScatterOptions()):
+        return self._fallback([input_tensor])._reduce_scatter_base(output_tensor, input_tensor, opts)
+
+    def reduce_scatter_tensor_coalesced(self, output_tensors, input_tensors, opts=ReduceScatterOptions()):
+        return self._fallback(input_tensors).reduce_scatter_tensor_coalesced(output_tensors, input_tensors, opts)
+
+    def alltoall_base(self, output, input, output_split_sizes, input_split_sizes, opts=AllToAllOptions()):
+        return self._fallback([input]).alltoall_base(output, input, output_split_sizes, input_split_sizes, opts)
+
+    def alltoall(self, output_tensors, input_tensors, opts=AllToAllOptions()):
+        return self._fallback(input_tensors).alltoall(output_tensors, input_tensors, opts)
+
+    def send(self, tensors, dst, tag=0):
+        return self._fallback(tensors).send(tensors, dst, tag)
+
+    def recv(self, tensors, src, tag=0):
+        return self._fallback(tensors).recv(tensors, src, tag)
+
+    def recv_anysource(self, tensors, tag=0):
+        return self._fallback(tensors).recv_anysource(tensors, tag)
+
+    def scatter(self, output_tensors, input_tensors, opts=None):
+        fb = self._fallback(output_tensors)
+        return fb.scatter(output_tensors, input_tensors, opts) if opts is not None else \
+            fb.scatter(output_tensors, input_tensors)
+
+    def gather(self, output_tensors, input_tensors, opts=None):
+        fb = self._fallback(input_tensors)
+        return fb.gather(output_tensors, input_tensors, opts) if opts is not None else \
+            fb.gather(output_tensors, input_tensors)
+
+
+def _create_flexar_pg(store, rank, world_size, timeout):
+    return FlexarProcessGroup(store, rank, world_size, timeout)
+
+
+def register():
+    if "FLEXAR" not in dist.Backend._plugins:
+        dist.Backend.register_backend("flexar", _create_flexar_pg, devices=["cpu", "cuda"])
+
+
+register()
+
+
+# ---------------------------------------------------------------------- DDP communication hook
+class FlexarHookState:
+    """State for :func:`flexar_allreduce_hook`: a flexar Communicator over the DDP process group."""
+
+    def __init__(self, process_group=None, algo: str | None = None, communicator: Communicator | None = None):
+        self.comm = communicator or Communicator(group=process_group)
+        self.algo = algo
+        self.calls = 0
+
+
+def flexar_allreduce_hook(state: FlexarHookState, bucket: dist.GradBucket) -> torch.futures.Future[torch.Tensor]:
+    """DDP comm hook: average the gradient bucket with the flexar executor kernel (in place, current stream)."""
+    buf = bucket.buffer()
+    state.comm.all_reduce(buf, op="avg" if buf.is_floating_point() else "sum", algo=state.algo)
+    state.calls += 1
+    fut = torch.futures.Future()
+    fut.set_result(buf)
+    return fut

@@ -38,7 +38,10 @@ class Communicator:
     """flexar communicator for the calling rank of a ``torch.distributed`` group."""
 
     def __init__(self, group=None, device: Optional[int] = None, workspace_bytes: int = 0,
-                 algo: Optional[str] = None, rank: Optional[int] = None, world_size: Optional[int] = None):
+                 algo: Optional[str] = None, rank: Optional[int] = None, world_size: Optional[int] = None,
+                 exchange=None):
+        """``exchange(bytes) -> list[bytes]`` all-gathers the handle bytes (default: torch.distributed
+        all_gather_object on ``group``; :func:`store_exchange` bootstraps from a c10d Store)."""
         import torch
         import torch.distributed as dist
 
@@ -61,12 +64,16 @@ class Communicator:
             hs = int(self._lib.flexar_handle_size())
             buf = ctypes.create_string_buffer(hs)
             nv.check(self._lib.flexar_comm_export(self._h, buf), "comm_export")
-            gathered = [None] * self.world_size
-            dist.all_gather_object(gathered, bytes(buf.raw), group=group)
-            allb = b"".join(gathered)
-            nv.check(self._lib.flexar_comm_connect(self._h, allb), "comm_connect")
-            # everyone has mapped everyone before the first collective
-            dist.barrier(group=group)
+            if exchange is None:
+                gathered = [None] * self.world_size
+                dist.all_gather_object(gathered, bytes(buf.raw), group=group)
+                allb = b"".join(gathered)
+                nv.check(self._lib.flexar_comm_connect(self._h, allb), "comm_connect")
+                dist.barrier(group=group)  # everyone has mapped everyone before the first collective
+            else:
+                allb = b"".join(exchange(bytes(buf.raw)))
+                nv.check(self._lib.flexar_comm_connect(self._h, allb), "comm_connect")
+                exchange(b"connected")
         if algo:
             self.set_algo(algo)
 
@@ -110,6 +117,19 @@ class Communicator:
             self.close()
         except Exception:
             pass
+
+
+def store_exchange(store, rank: int, world_size: int, prefix: str = "flexar"):
+    """An ``exchange`` callable over a c10d Store: every call is one all-gather round."""
+    state = {"round": 0}
+
+    def ex(data: bytes):
+        rnd = state["round"]
+        state["round"] += 1
+        store.set(f"{prefix}/{rnd}/{rank}", data)
+        return [bytes(store.get(f"{prefix}/{rnd}/{r}")) for r in range(world_size)]
+
+    return ex
 
 
 class LocalGroup:

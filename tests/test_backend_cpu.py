@@ -1,0 +1,61 @@
+"""The "flexar" c10d backend on CPU (gloo world of 2 processes): registration,
+CPU-tensor allreduce/broadcast/allgather/barrier plumbing through the Python
+ProcessGroup. (Device allreduce is covered by tests/test_gpu_backend.py.)"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import torch.distributed as dist
+
+        import allreduce_over_mpi_amd.parallel.backend as fb  # noqa: F401  registers "flexar"
+
+        dist.init_process_group("flexar", rank=rank, world_size=world)
+        assert dist.get_backend() == "flexar"
+        x = torch.arange(10, dtype=torch.float32) * (rank + 1)
+        dist.all_reduce(x)
+        y = torch.tensor([rank + 1], dtype=torch.int64)
+        dist.all_reduce(y, op=dist.ReduceOp.MAX)
+        b = torch.tensor([float(rank)]) if rank == 0 else torch.tensor([-1.0])
+        b[0] = 7.0 if rank == 0 else b[0]
+        dist.broadcast(b, src=0)
+        outs = [torch.zeros(2) for _ in range(world)]
+        dist.all_gather(outs, torch.full((2,), float(rank)))
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, x.tolist(), int(y.item()), float(b.item()), [o.tolist() for o in outs], None))
+    except Exception:
+        import traceback
+
+        q.put((rank, None, None, None, None, traceback.format_exc()))
+
+
+def test_flexar_backend_cpu_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(2)]
+    for p in ps:
+        p.join(60)
+    for rank, x, y, b, outs, err in res:
+        assert err is None, err
+        assert x == [float(i * 3) for i in range(10)]
+        assert y == 2 and b == 7.0
+        assert outs == [[0.0, 0.0], [1.0, 1.0]]
