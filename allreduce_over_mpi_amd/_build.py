@@ -20,9 +20,10 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(REPO, "csrc")
 INCLUDE = os.path.join(CSRC, "include")
-LIB_DIR = os.path.join(PKG_DIR, "_lib")
+LIB_DIR = os.environ.get("FLEXAR_LIB_DIR") or os.path.join(PKG_DIR, "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libflexar.so")
-BUILD_DIR = os.path.join(REPO, "build", "obj")
+BUILD_DIR = os.path.join(REPO, "build", "obj" + os.environ.get("FLEXAR_BUILD_TAG", ""))
+EXTRA_CFLAGS = os.environ.get("FLEXAR_EXTRA_CFLAGS", "").split()
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("FLEXAR_OFFLOAD_ARCH", "gfx950")
 
@@ -69,7 +70,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
     for s in hip:
         o = os.path.join(BUILD_DIR, os.path.basename(s) + ".o")
         objs.append(o)
-        jobs.append([_hipcc(), "--offload-arch=" + ARCH, "-munsafe-fp-atomics", *common, "-c", s, "-o", o])
+        jobs.append([_hipcc(), "--offload-arch=" + ARCH, "-munsafe-fp-atomics", *common, *EXTRA_CFLAGS, "-c", s, "-o", o])
     cxx = os.environ.get("CXX", "g++")
     for s in cpp:
         o = os.path.join(BUILD_DIR, os.path.basename(s) + ".o")

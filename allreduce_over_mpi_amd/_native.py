@@ -53,6 +53,7 @@ def _sig(lib):
         "flexar_allreduce_ex": (i, [vp, vp, vp, sz, i, i, vp, cp, f]),
         "flexar_comm_check": (i, [vp]),
         "flexar_comm_describe": (i, [vp, sz, i, cp, sz]),
+        "flexar_comm_stats": (i, [vp, cp, sz]),
         "flexar_group_create": (i, [i, i, sz, c.POINTER(vp)]),
         "flexar_group_allreduce": (i, [c.POINTER(vp), i, c.POINTER(vp), c.POINTER(vp), sz, i, i, vp, cp, f]),
         "flexar_reduce": (i, [vp, c.POINTER(vp), i, sz, i, i, f, vp]),

@@ -92,6 +92,14 @@ class Communicator:
     def check(self):
         nv.check(self._lib.flexar_comm_check(self._h), "comm_check")
 
+    def stats(self) -> dict:
+        """Call/byte counters; per-algorithm device time when FLEXAR_PROFILE=1 (synchronises those events)."""
+        import json
+
+        b = ctypes.create_string_buffer(1 << 16)
+        nv.check(self._lib.flexar_comm_stats(self._h, b, 1 << 16), "comm_stats")
+        return json.loads(b.value.decode())
+
     # ------------------------------------------------------------------ collectives
     def all_reduce(self, tensor, op="sum", out=None, algo: Optional[str] = None, scale: float = 1.0, stream=None):
         """Allreduce ``tensor`` (in place unless ``out`` is given). Returns the result tensor."""

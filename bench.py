@@ -46,7 +46,11 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--size-mb", type=float, default=256.0, help="buffer MiB per rank")
-    ap.add_argument("--dtype", default="float32", choices=["float32", "bfloat16", "float16"])
+    ap.add_argument("--dtype", default="float32", choices=["float32", "bfloat16", "float16", "float8_e4m3fn"])
+    ap.add_argument("--op", default="sum", choices=["sum", "avg"],
+                    help="avg = sum with the 1/N post-scale fused into the reduction (fp8 gradients)")
+    ap.add_argument("--sweep", default="", help="MIN:MAX bytes (e.g. 4K:4G): busbw table vs RCCL, x4 steps")
+    ap.add_argument("--sweep-out", default="", help="write sweep rows as JSON lines here (rank 0)")
     ap.add_argument("--algo", default="auto", help="flexar algorithm spec or 'auto' (tuned at start-up)")
     ap.add_argument("--no-rccl", action="store_true", help="skip the RCCL comparison run")
     ap.add_argument("--no-tune", action="store_true", help="use the cost model instead of the start-up tuner")
@@ -78,7 +82,10 @@ def main():
     comm = Communicator(workspace_bytes=max(512 << 20, 2 * nbytes + (64 << 20)))
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
-    x = torch.randn(count, device=dev, dtype=torch.float32, generator=gen).to(dtype)
+    x = torch.randn(count, device=dev, dtype=torch.float32, generator=gen)
+    if dtype == torch.float8_e4m3fn:
+        x = x * 8  # fp8 e4m3 range: |x| <= 448
+    x = x.to(dtype)
     y = torch.empty_like(x)
 
     def max_over_ranks(v: float) -> float:
@@ -89,13 +96,21 @@ def main():
         return float(t.item())
 
     # ---------------------------------------------------------------- correctness vs RCCL
-    ref = x.clone()
-    if world > 1:
-        dist.all_reduce(ref)
-    tol = (1e-5 if dtype == torch.float32 else 2e-2) * math.sqrt(world) * 4
+    op = args.op
+    if dtype == torch.float8_e4m3fn:  # RCCL reference computed in fp32 from the same fp8 inputs
+        ref = x.float()
+        if world > 1:
+            dist.all_reduce(ref)
+        ref = (ref / world if op == "avg" else ref).to(dtype)
+    else:
+        ref = x.clone()
+        if world > 1:
+            dist.all_reduce(ref, op=dist.ReduceOp.AVG if op == "avg" else dist.ReduceOp.SUM)
+    tol = {torch.float32: 1e-5, torch.bfloat16: 2e-2, torch.float16: 4e-3, torch.float8_e4m3fn: 0.13}[dtype]
+    tol = tol * math.sqrt(world) * 4 if dtype != torch.float8_e4m3fn else tol
 
     def check(spec):
-        comm.all_reduce(x, out=y, algo=None if spec == "auto" else spec)
+        comm.all_reduce(x, out=y, op=op, algo=None if spec == "auto" else spec)
         torch.cuda.synchronize()
         err = float((y.float() - ref.float()).abs().max().item())
         scale = float(ref.float().abs().max().item()) + 1e-6
@@ -105,13 +120,13 @@ def main():
     def timed(spec, iters, warm=1):
         a = None if spec == "auto" else spec
         for _ in range(warm):
-            comm.all_reduce(x, out=y, algo=a)
+            comm.all_reduce(x, out=y, op=op, algo=a)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
         for _ in range(iters):
-            comm.all_reduce(x, out=y, algo=a)
+            comm.all_reduce(x, out=y, op=op, algo=a)
         torch.cuda.synchronize()
         return max_over_ranks(time.perf_counter() - t0) / iters
 
@@ -166,14 +181,14 @@ def main():
     # ---------------------------------------------------------------- timed region
     a = None if algo == "auto" else algo
     for _ in range(args.warmup):
-        comm.all_reduce(x, out=y, algo=a)
+        comm.all_reduce(x, out=y, op=op, algo=a)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        comm.all_reduce(x, out=y, algo=a)
+        comm.all_reduce(x, out=y, op=op, algo=a)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -183,7 +198,7 @@ def main():
     t_step = elapsed / max(1, args.steps)
 
     rccl_busbw = None
-    if world > 1 and not args.no_rccl:
+    if world > 1 and not args.no_rccl and dtype != torch.float8_e4m3fn:
         z = x.clone()
         for _ in range(max(1, args.warmup)):
             dist.all_reduce(z)
@@ -211,10 +226,12 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": round(value / BASELINE_BUSBW_256MIB, 2) if (world > 1 and args.size_mb == 256.0) else None,
-        "dtype": {"float32": "fp32", "bfloat16": "bf16", "float16": "fp16"}[args.dtype],
+        "dtype": {"float32": "fp32", "bfloat16": "bf16", "float16": "fp16", "float8_e4m3fn": "fp8_e4m3"}[args.dtype],
         "data": "synthetic (torch.randn per rank, seeded); result checked against RCCL before timing",
         "config": {
-            "model": f"allreduce {args.dtype} {args.size_mb:g}MiB buffer per rank (BASELINE config #2)",
+            "model": f"allreduce {args.dtype} {args.size_mb:g}MiB buffer per rank"
+                     + (" (BASELINE config #2)" if args.dtype == "float32" and args.size_mb == 256 else ""),
+            "op": op,
             "global_batch": nbytes,
             "seq_len": None,
             "parallelism": f"dp{world}",
@@ -226,6 +243,8 @@ def main():
         "rccl_busbw_GBps": rccl_busbw,
         "tuner": tune_log or None,
     }
+    if args.sweep:
+        out["sweep"] = run_sweep(args, comm, world, rank, dev, dtype, op, dist, max_over_ranks)
     if world == 1:
         out["note"] = ("N=1: busbw factor 2(N-1)/N is 0; value = algbw of the out-of-place allreduce "
                        "(device copy through the flexar executor kernel)")
@@ -234,6 +253,56 @@ def main():
     comm.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def parse_bytes(v: str) -> int:
+    mult = {"K": 1 << 10, "M": 1 << 20, "G": 1 << 30}
+    v = v.strip().upper().rstrip("B")
+    return int(float(v[:-1]) * mult[v[-1]]) if v and v[-1] in mult else int(float(v))
+
+
+def run_sweep(args, comm, world, rank, dev, dtype, op, dist, max_over_ranks):
+    """busbw vs bytes, flexar (cost-model 'auto' choice) vs RCCL — BASELINE config #4."""
+    import torch
+
+    from allreduce_over_mpi_amd.utils.perf import busbw_gbps
+
+    lo, hi = (parse_bytes(t) for t in args.sweep.split(":"))
+    es = torch.tensor([], dtype=dtype).element_size()
+    rows = []
+    b = lo
+    while b <= hi:
+        n = max(1, b // es)
+        x = torch.randn(n, device=dev).to(dtype)
+        y = torch.empty_like(x)
+        iters = max(3, min(50, int(2e8 // max(b, 1))))
+
+        def t_of(fn):
+            for _ in range(2):
+                fn()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                fn()
+            torch.cuda.synchronize()
+            return max_over_ranks(time.perf_counter() - t0) / iters
+
+        tf = t_of(lambda: comm.all_reduce(x, out=y, op=op))
+        row = {"bytes": n * es, "algo": comm.describe(n, dtype).split(" ")[0], "flexar_us": round(tf * 1e6, 2),
+               "flexar_busbw": round(busbw_gbps(n * es, tf, world), 2)}
+        if world > 1 and dtype != torch.float8_e4m3fn and not args.no_rccl:
+            tr = t_of(lambda: dist.all_reduce(x))
+            row.update(rccl_us=round(tr * 1e6, 2), rccl_busbw=round(busbw_gbps(n * es, tr, world), 2))
+        rows.append(row)
+        log(rank, "sweep", json.dumps(row))
+        if rank == 0 and args.sweep_out:
+            with open(args.sweep_out, "a") as f:
+                f.write(json.dumps(dict(row, n_gpus=world, dtype=args.dtype)) + "\n")
+        del x, y
+        b *= 4
+    return rows
 
 
 if __name__ == "__main__":

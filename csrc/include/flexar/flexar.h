@@ -113,6 +113,8 @@ int flexar_allreduce_ex(flexar_comm_t comm, const void* sendbuf, void* recvbuf, 
 /* Non-blocking health check: returns FLEXAR_ERR_TIMEOUT (and fills flexar_last_error)
  * if a device-side wait timed out in any previous call. */
 int flexar_comm_check(flexar_comm_t comm);
+/* JSON statistics (calls, bytes; per-algorithm device time when FLEXAR_PROFILE=1). */
+int flexar_comm_stats(flexar_comm_t comm, char* buf, size_t buflen);
 /* Describe the algorithm the communicator would run for (count, dtype). */
 int flexar_comm_describe(flexar_comm_t comm, size_t count, int dtype, char* buf, size_t buflen);
 

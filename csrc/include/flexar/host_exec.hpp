@@ -79,17 +79,25 @@ struct HostExec {
       return c.local[l.buf] + l.off * sizeof(T);
     };
     for (uint32_t i = P.chan_start[ch]; i < P.chan_start[ch + 1]; ++i) {
-      const Op& o = P.ops[i];
-      if (o.kind == OP_XFER) {
-        uint64_t lo, hi;
-        slice_range(o.len, lb, nb, quantum, &lo, &hi);
-        if (hi <= lo) continue;
-        const T* srcs[kMaxSrc];
-        T* dsts[kMaxDst];
-        for (int k = 0; k < o.nsrc; ++k) srcs[k] = (const T*)addr(o.src[k]) + lo;
-        for (int k = 0; k < o.ndst; ++k) dsts[k] = (T*)addr(o.dst[k]) + lo;
-        host_reduce_span<T, OP>(dsts, o.ndst, srcs, o.nsrc, hi - lo, o.scale);
-      } else if (o.kind == OP_SIGNAL) {
+      const Op& o0 = P.ops[i];
+      if (o0.kind == OP_XFER) {
+        const uint32_t n = o0.run > 1 ? o0.run : 1;  // rotated run, as on the device
+        for (uint32_t k = 0; k < n; ++k) {
+          const Op& o = P.ops[i + (n > 1 ? (k + lb) % n : 0)];
+          uint64_t lo, hi;
+          slice_range(o.len, lb, nb, quantum, &lo, &hi);
+          if (hi <= lo) continue;
+          const T* srcs[kMaxSrc];
+          T* dsts[kMaxDst];
+          for (int q = 0; q < o.nsrc; ++q) srcs[q] = (const T*)addr(o.src[q]) + lo;
+          for (int q = 0; q < o.ndst; ++q) dsts[q] = (T*)addr(o.dst[q]) + lo;
+          host_reduce_span<T, OP>(dsts, o.ndst, srcs, o.nsrc, hi - lo, o.scale);
+        }
+        i += n - 1;
+        continue;
+      }
+      const Op& o = o0;
+      if (o.kind == OP_SIGNAL) {
         std::atomic_thread_fence(std::memory_order_release);
         for (int k = 0; k < o.npeers; ++k)
           c.peer_flags[o.peers[k]][host_flag_index(c, o.slot, c.rank, gblock)].store(epoch, std::memory_order_release);

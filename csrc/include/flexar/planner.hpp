@@ -71,11 +71,16 @@ class Planner {
     } else if (spec.kind == AlgoKind::TREE) {
       long prod = 1;
       for (int w : spec.widths) prod *= w;
-      if (spec.widths.empty() || prod != (long)N) { if (err) *err = "tree widths do not multiply to N"; return false; }
-      if (2 * spec.widths.size() > kMaxSlots) { if (err) *err = "too many stages"; return false; }
+      // product == N: plain tree. N/2 <= product < N: the N - product "lonely" ranks fold into
+      // partners first (the reference's intended-but-dead lonely-node path, mpi_mod.hpp:1075-1099).
+      if (spec.widths.empty() || prod > (long)N || 2 * prod < (long)N) {
+        if (err) *err = "tree widths must multiply to N (or to at least N/2 with lonely ranks)";
+        return false;
+      }
+      if (2 * spec.widths.size() + 2 > kMaxSlots) { if (err) *err = "too many stages"; return false; }
       for (int w : spec.widths)
         if (w < 2) { if (err) *err = "tree width < 2"; return false; }
-      build_tree(spec.widths, spec.ag == AgMode::PULL, spec.fuse);
+      build_tree_lonely(spec.widths, (uint32_t)prod, spec.ag == AgMode::PULL, spec.fuse);
       P->desc = spec.str();
     } else if (spec.kind == AlgoKind::ONESHOT) {
       build_oneshot();
@@ -86,7 +91,45 @@ class Planner {
     }
     P->stg_elems = stg;
     P->nchan = (uint32_t)P->chan_start.size() - 1;
+    mark_runs(*P, r);
     return true;
+  }
+
+  // Rotatable runs: maximal sequences of consecutive XFERs that each touch a remote rank and are
+  // pairwise independent in local memory (no overlap between one op's local destinations and
+  // another's local sources/destinations). Executed in a per-workgroup rotated order.
+  static void mark_runs(Program& P, uint32_t rank) {
+    auto remote = [&](const Op& o) {
+      for (int k = 0; k < o.nsrc; ++k) if (o.src[k].rank != rank) return true;
+      for (int k = 0; k < o.ndst; ++k) if (o.dst[k].rank != rank) return true;
+      return false;
+    };
+    auto ovl = [&](const Loc& a, uint64_t la, const Loc& b, uint64_t lb) {
+      return a.rank == rank && b.rank == rank && a.buf == b.buf && a.off < b.off + lb && b.off < a.off + la;
+    };
+    auto indep = [&](const Op& a, const Op& b) {
+      for (int i = 0; i < a.ndst; ++i) {
+        for (int j = 0; j < b.nsrc; ++j) if (ovl(a.dst[i], a.len, b.src[j], b.len)) return false;
+        for (int j = 0; j < b.ndst; ++j) if (ovl(a.dst[i], a.len, b.dst[j], b.len)) return false;
+      }
+      for (int i = 0; i < b.ndst; ++i)
+        for (int j = 0; j < a.nsrc; ++j) if (ovl(b.dst[i], b.len, a.src[j], a.len)) return false;
+      return true;
+    };
+    for (uint32_t c = 0; c < P.nchan; ++c) {
+      uint32_t i = P.chan_start[c], end = P.chan_start[c + 1];
+      while (i < end) {
+        uint32_t j = i;
+        while (j < end && P.ops[j].kind == OP_XFER && remote(P.ops[j]) && j - i < 0xffff) {
+          bool ok = true;
+          for (uint32_t k = i; k < j && ok; ++k) ok = indep(P.ops[k], P.ops[j]);
+          if (!ok) break;
+          ++j;
+        }
+        if (j - i > 1) P.ops[i].run = (uint16_t)(j - i);
+        i = (j > i) ? j : i + 1;
+      }
+    }
   }
 
  private:
@@ -248,7 +291,52 @@ class Planner {
     }
   };
 
-  void build_tree(const std::vector<int>& widths, bool pull, bool fuse) {
+  // Lonely folding around the tree: rank P + i (i < L = N - P) pushes its input to partner i,
+  // partner i pre-reduces it into OUT, runs the tree from OUT, then pushes the result back.
+  void build_tree_lonely(const std::vector<int>& widths, uint32_t P, bool pull, bool fuse) {
+    const uint32_t L = N - P, S = (uint32_t)widths.size();
+    // every span below uses the tree's block geometry, so each grid block touches exactly the
+    // slices it later reads/writes in the tree (no cross-workgroup dependency)
+    const uint64_t split = round_up((count + P - 1) / P);
+    auto blen = [&](uint32_t k) -> uint64_t {
+      uint64_t s0 = (uint64_t)k * split;
+      return s0 >= count ? 0 : std::min(split, count - s0);
+    };
+    uint64_t lone_in = 0, lone_out = 0;
+    if (L) {
+      lone_in = alloc((uint64_t)P * split);
+      lone_out = alloc((uint64_t)P * split);
+    }
+    const uint32_t s_in = 2 * S, s_out = 2 * S + 1;
+    if (r >= P) {  // lonely rank: ship input, wait for the result
+      uint32_t partner = r - P;
+      for (uint32_t k = 0; k < P; ++k)
+        xfer(blen(k), {loc(BUF_IN, r, k * split)}, {loc(BUF_STG, partner, lone_in + k * split)}, 1.0f);
+      signal({partner}, s_in);
+      wait({partner}, s_out);
+      for (uint32_t k = 0; k < P; ++k)
+        xfer(blen(k), {loc(BUF_STG, r, lone_out + k * split)}, {loc(BUF_OUT, r, k * split)}, 1.0f);
+      finish_channel();
+      return;
+    }
+    uint16_t first = BUF_IN;
+    if (r < L) {  // partner: fold the lonely rank's input in first
+      wait({r + P}, s_in);
+      for (uint32_t k = 0; k < P; ++k)
+        xfer(blen(k), {loc(BUF_IN, r, k * split), loc(BUF_STG, r, lone_in + k * split)}, {loc(BUF_OUT, r, k * split)},
+             1.0f);
+      first = BUF_OUT;
+    }
+    build_tree(widths, P, first, pull, fuse);
+    if (r < L) {
+      for (uint32_t k = 0; k < P; ++k)
+        xfer(blen(k), {loc(BUF_OUT, r, k * split)}, {loc(BUF_STG, r + P, lone_out + k * split)}, 1.0f);
+      signal({r + P}, s_out);
+    }
+    finish_channel();
+  }
+
+  void build_tree(const std::vector<int>& widths, const uint32_t N, uint16_t first, bool pull, bool fuse) {
     const uint32_t S = (uint32_t)widths.size();
     uint64_t split = round_up((count + N - 1) / N);
     auto blen = [&](uint32_t k) -> uint64_t {
@@ -296,7 +384,7 @@ class Planner {
     // ---------------- reduce-scatter
     for (uint32_t s = 0; s < S; ++s) {
       const Stage& x = st[s];
-      uint16_t cur = (s == 0) ? BUF_IN : BUF_OUT;
+      uint16_t cur = (s == 0) ? first : BUF_OUT;
       bool sends_fused = fuse && s > 0;  // previous stage already wrote our sends into the receivers
       if (!sends_fused) {
         for (uint32_t p : x.others())
@@ -366,7 +454,6 @@ class Planner {
         }
       }
     }
-    finish_channel();
   }
 
   // ------------------------------------------------------------------ oneshot

@@ -57,6 +57,10 @@ struct Op {
   uint16_t npeers;         // SIGNAL/WAIT
   uint16_t flags;          // XFER: kXferApplyOp (nsrc>1 implies reduction)
   uint16_t peers[kMaxPeersPerOp];
+  uint16_t run;            // >1 on the first op of a run of mutually independent XFERs: each
+                           // workgroup starts the run at a different op (lb % run), so at any
+                           // moment a rank's workgroups target different peers = all links busy
+  uint16_t pad16[3];
   Loc src[kMaxSrc];
   Loc dst[kMaxDst];
 };

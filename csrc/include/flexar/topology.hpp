@@ -199,7 +199,11 @@ inline bool parse_algo(const std::string& raw, int nranks, AlgoSpec* spec, std::
       if (x < 2) { if (err) *err = "tree widths must be >= 2"; return false; }
       prod *= x;
     }
-    if (w.empty() || prod != nranks) { if (err) *err = "tree widths must multiply to the world size"; return false; }
+    // product == N, or N/2 <= product < N with N - product lonely ranks folded into partners
+    if (w.empty() || prod > nranks || 2 * prod < nranks) {
+      if (err) *err = "tree widths must multiply to the world size (or >= half of it: lonely ranks)";
+      return false;
+    }
     spec->kind = AlgoKind::TREE;
     spec->widths = w;
     return true;
@@ -250,6 +254,12 @@ inline std::vector<AlgoSpec> enumerate_plans(int nranks) {
   for (auto& w : ordered_factorizations(nranks, 4096)) {
     AlgoSpec t; t.kind = AlgoKind::TREE; t.widths = w; out.push_back(t);
   }
+  // prime N: trees over N - 1 ranks plus one lonely rank (reference ChooseWidth.h, "+1" structures)
+  if (nranks > 3 && is_prime(nranks))
+    for (auto& w : ordered_factorizations(nranks - 1, 4096)) {
+      if (w.size() < 2) continue;
+      AlgoSpec t; t.kind = AlgoKind::TREE; t.widths = w; out.push_back(t);
+    }
   return out;
 }
 

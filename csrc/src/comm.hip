@@ -11,6 +11,7 @@
 //  * size_t counts (defect D7); unsupported dtype/op return an error code
 //    instead of exit(1); a device-side watchdog turns a stuck peer into
 //    FLEXAR_ERR_TIMEOUT instead of a hang.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <unistd.h>
 
@@ -64,6 +65,33 @@ struct DevProgram {
 
 static const uint32_t kGroupMaxBlocks = 256;
 
+// Optional roctx ranges (FLEXAR_ROCTX=1): resolved with dlopen so libflexar has no hard dependency.
+struct Roctx {
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+  Roctx() {
+    const char* e = getenv("FLEXAR_ROCTX");
+    if (!e || *e != '1') return;
+    void* h = dlopen("libroctx64.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/libroctx64.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return;
+    push = (int (*)(const char*))dlsym(h, "roctxRangePushA");
+    pop = (int (*)())dlsym(h, "roctxRangePop");
+    if (!push || !pop) push = nullptr, pop = nullptr;
+  }
+};
+static Roctx& roctx() {
+  static Roctx r;
+  return r;
+}
+
+// Per-call device timing (FLEXAR_PROFILE=1): hipEvent pairs resolved lazily by flexar_comm_stats.
+struct ProfRec {
+  std::string algo;
+  uint64_t bytes;
+  hipEvent_t a, b;
+};
+
 static uint64_t env_u64(const char* name, uint64_t dflt) {
   const char* e = getenv(name);
   if (!e || !*e) return dflt;
@@ -92,11 +120,18 @@ struct flexar_comm {
   int max_grid = 256;
   uint64_t min_block_bytes = 256 * 1024;
   uint64_t timeout_ticks = 0;
+  uint32_t fi_kind = 0, fi_slot = 0;
+  uint64_t fi_ticks = 0;
   XgmiModel model;
   TuneTable tune;
   bool have_tune = false;
   std::map<std::string, std::unique_ptr<DevProgram>> cache;
   std::mutex mu;
+  bool profile = false;
+  std::vector<ProfRec> prof_pending;
+  struct Agg { uint64_t calls = 0, bytes = 0; double ms = 0; };
+  std::map<std::string, Agg> prof;
+  uint64_t calls = 0, bytes = 0;
 };
 
 namespace flexar {
@@ -201,6 +236,9 @@ static void fill_ctx(flexar_comm* c, DevProgram* dp, const void* in, void* out, 
   x->err = c->err_dev;
   x->timeout_ticks = c->timeout_ticks;
   x->vec_ok = ((((uintptr_t)in) | ((uintptr_t)out)) & 15) == 0;
+  x->fi_kind = c->fi_kind;
+  x->fi_slot = c->fi_slot;
+  x->fi_ticks = c->fi_ticks;
 }
 
 // Split a call into pieces whose staging fits one parity half of the workspace.
@@ -275,7 +313,19 @@ static void init_defaults(flexar_comm* c) {
   if (c->max_grid < 1) c->max_grid = 1;
   if (c->max_grid > (int)kMaxGridBlocks) c->max_grid = kMaxGridBlocks;
   c->min_block_bytes = env_u64("FLEXAR_MIN_BLOCK_BYTES", 256 * 1024);
+  c->profile = env_u64("FLEXAR_PROFILE", 0) != 0;
   if (!c->min_block_bytes) c->min_block_bytes = 1;
+  // FLEXAR_FAULT_INJECT=delay:RANK:SLOT:MICROSECONDS | drop:RANK:SLOT  (tests / race hunting)
+  if (const char* fi = getenv("FLEXAR_FAULT_INJECT")) {
+    char kind[16] = {0};
+    int rk = -1, slot = 0;
+    double us = 0;
+    if (sscanf(fi, "%15[a-z]:%d:%d:%lf", kind, &rk, &slot, &us) >= 3 && rk == c->rank) {
+      c->fi_kind = strcmp(kind, "drop") == 0 ? 2 : 1;
+      c->fi_slot = (uint32_t)slot;
+      c->fi_ticks = (uint64_t)(us * 100.0);  // 100 MHz s_memrealtime
+    }
+  }
   const char* a = getenv("FLEXAR_ALGO");
   std::string err;
   if (a && *a) {
@@ -442,6 +492,16 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
   if ((rc = resolve_spec(c, algo, (double)count * es, &s))) return rc;
   uint64_t piece = count;
   if (c->nranks > 1 && (rc = plan_pieces(c, s, count, es, fs, &piece))) return rc;
+  const std::string sdesc = s.str();
+  if (roctx().push) roctx().push(("flexar allreduce " + sdesc + " " + std::to_string(count * es) + "B").c_str());
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  if (c->profile) {
+    FX_HIP(hipEventCreate(&ev0));
+    FX_HIP(hipEventCreate(&ev1));
+    FX_HIP(hipEventRecord(ev0, st));
+  }
+  c->calls++;
+  c->bytes += count * es;
   for (uint64_t off = 0; off < count; off += piece) {
     uint64_t n = std::min<uint64_t>(piece, count - off);
     DevProgram* dp = nullptr;
@@ -455,9 +515,45 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     la.grid = grid;
     la.stream = st;
     rc = launch_dtype(dtype, op, la);
-    if (rc) return rc;
+    if (rc) break;
   }
-  return 0;
+  if (c->profile) {
+    (void)hipEventRecord(ev1, st);
+    c->prof_pending.push_back(ProfRec{sdesc, (uint64_t)count * es, ev0, ev1});
+  }
+  if (roctx().pop) roctx().pop();
+  return rc;
+}
+
+// JSON statistics: calls/bytes overall and (FLEXAR_PROFILE=1) device time per algorithm.
+int flexar_comm_stats(flexar_comm_t c, char* buf, size_t buflen) {
+  if (!c || !buf) return FLEXAR_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  for (auto& p : c->prof_pending) {
+    float ms = 0;
+    if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      auto& a = c->prof[p.algo];
+      a.calls++;
+      a.bytes += p.bytes;
+      a.ms += ms;
+    }
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  c->prof_pending.clear();
+  std::string j = "{\"calls\": " + std::to_string(c->calls) + ", \"bytes\": " + std::to_string(c->bytes) +
+                  ", \"plans_cached\": " + std::to_string(c->cache.size()) + ", \"profile\": {";
+  bool first = true;
+  for (auto& kv : c->prof) {
+    char t[256];
+    snprintf(t, sizeof(t), "%s\"%s\": {\"calls\": %llu, \"bytes\": %llu, \"ms\": %.4f}", first ? "" : ", ",
+             kv.first.c_str(), (unsigned long long)kv.second.calls, (unsigned long long)kv.second.bytes, kv.second.ms);
+    j += t;
+    first = false;
+  }
+  j += "}}";
+  snprintf(buf, buflen, "%s", j.c_str());
+  return j.size() < buflen ? 0 : FLEXAR_ERR_NOMEM;
 }
 
 int flexar_allreduce(flexar_comm_t c, const void* in, void* out, size_t count, int dtype, int op, void* stream) {

@@ -39,10 +39,31 @@ struct DevCtx {
   uint32_t* err;                   // device pointer of a host-mapped error word
   uint64_t timeout_ticks;          // s_memrealtime ticks (100 MHz)
   uint32_t vec_ok;                 // IN/OUT base addresses 16-B aligned
+  // fault injection (tests only, FLEXAR_FAULT_INJECT): 1 = delay SIGNAL(slot) by fi_ticks, 2 = drop it
+  uint32_t fi_kind;
+  uint32_t fi_slot;
+  uint64_t fi_ticks;
 };
 
-__device__ FX_INLINE uint4 ld16(const char* p) { return *reinterpret_cast<const uint4*>(p); }
-__device__ FX_INLINE void st16(char* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
+// 16-byte vector memory ops (global_load/store_dwordx4). FLEXAR_NT_LOADS / FLEXAR_NT_STORES select the
+// streaming (nontemporal) cache policy for the once-touched payload bytes.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ FX_INLINE uint4 ld16(const char* p) {
+#if defined(FLEXAR_NT_LOADS)
+  u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+#else
+  u32x4 v = *reinterpret_cast<const u32x4*>(p);
+#endif
+  return uint4{v.x, v.y, v.z, v.w};
+}
+__device__ FX_INLINE void st16(char* p, uint4 x) {
+  u32x4 v = {x.x, x.y, x.z, x.w};
+#if defined(FLEXAR_NT_STORES)
+  __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+#else
+  *reinterpret_cast<u32x4*>(p) = v;
+#endif
+}
 
 template <typename T, typename OP, int K>
 __device__ FX_INLINE uint4 combine16(const uint4 (&x)[K], float scale, bool sc) {
@@ -140,6 +161,39 @@ __device__ FX_INLINE void st_flag(uint64_t* f, uint64_t v) {
 }
 
 template <typename T, typename OP>
+__device__ FX_INLINE void xfer_op(const DevCtx& c, const Op* o, uint32_t lb, uint32_t nb, uint32_t quantum,
+                                  uint64_t par) {
+  uint64_t lo, hi;
+  slice_range(o->len, lb, nb, quantum, &lo, &hi);
+  if (hi <= lo) return;
+  const int ns = o->nsrc, nd = o->ndst;
+  const char* s[kMaxSrc];
+  char* d[kMaxDst];
+  bool vec = true;
+#pragma unroll
+  for (int k = 0; k < kMaxSrc; ++k) {
+    s[k] = nullptr;
+    if (k < ns) {
+      const Loc l = o->src[k];
+      char* base = (l.buf == BUF_STG) ? c.peer_stg[l.rank] + par : c.local[l.buf];
+      s[k] = base + (l.off + lo) * sizeof(T);
+      vec &= (l.buf == BUF_STG) || c.vec_ok;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kMaxDst; ++k) {
+    d[k] = nullptr;
+    if (k < nd) {
+      const Loc l = o->dst[k];
+      char* base = (l.buf == BUF_STG) ? c.peer_stg[l.rank] + par : c.local[l.buf];
+      d[k] = base + (l.off + lo) * sizeof(T);
+      vec &= (l.buf == BUF_STG) || c.vec_ok;
+    }
+  }
+  xfer_dispatch<T, OP>(ns, s, d, nd, hi - lo, o->scale, vec);
+}
+
+template <typename T, typename OP>
 __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uint32_t grid) {
   __shared__ int s_abort;
   const uint32_t tid = threadIdx.x;
@@ -153,44 +207,31 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
   __syncthreads();
 
   const uint32_t i0 = c.chan_start[ch], i1 = c.chan_start[ch + 1];
-  for (uint32_t i = i0; i < i1; ++i) {
+  for (uint32_t i = i0; i < i1;) {
     const Op* o = c.ops + i;
     const uint16_t kind = o->kind;
     if (kind == OP_XFER) {
-      uint64_t lo, hi;
-      slice_range(o->len, lb, nb, quantum, &lo, &hi);
-      if (hi > lo) {
-        const int ns = o->nsrc, nd = o->ndst;
-        const char* s[kMaxSrc];
-        char* d[kMaxDst];
-        bool vec = true;
-#pragma unroll
-        for (int k = 0; k < kMaxSrc; ++k) {
-          s[k] = nullptr;
-          if (k < ns) {
-            const Loc l = o->src[k];
-            char* base = (l.buf == BUF_STG) ? c.peer_stg[l.rank] + par : c.local[l.buf];
-            s[k] = base + (l.off + lo) * sizeof(T);
-            vec &= (l.buf == BUF_STG) || c.vec_ok;
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < kMaxDst; ++k) {
-          d[k] = nullptr;
-          if (k < nd) {
-            const Loc l = o->dst[k];
-            char* base = (l.buf == BUF_STG) ? c.peer_stg[l.rank] + par : c.local[l.buf];
-            d[k] = base + (l.off + lo) * sizeof(T);
-            vec &= (l.buf == BUF_STG) || c.vec_ok;
-          }
-        }
-        xfer_dispatch<T, OP>(ns, s, d, nd, hi - lo, o->scale, vec);
+      // a run of independent XFERs starts at a per-workgroup offset: the workgroups of one rank
+      // spread over all peers (xGMI links) instead of marching through them in lockstep
+      const uint32_t n = o->run > 1 ? o->run : 1;
+      bool bar = false;
+      for (uint32_t k = 0; k < n; ++k) {
+        const Op* q = c.ops + i + (n > 1 ? (k + lb) % n : 0);
+        xfer_op<T, OP>(c, q, lb, nb, quantum, par);
+        bar |= (q->flags & kXferBarrierAfter) != 0;
       }
-      if (o->flags & kXferBarrierAfter) __syncthreads();
+      if (bar) __syncthreads();
+      i += n;
+      continue;
     } else if (kind == OP_SIGNAL) {
       // every storing wave drains, the workgroup meets, one wave releases at system scope
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      if (c.fi_kind && o->slot == c.fi_slot) {
+        if (c.fi_kind == 2) { ++i; continue; }  // dropped signal: peers must time out, not hang
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < c.fi_ticks) __builtin_amdgcn_s_sleep(8);
+      }
       if (tid < 64) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the flag must not overtake the write-back
@@ -217,6 +258,7 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
       __syncthreads();
       if (s_abort) break;
     }
+    ++i;
   }
   __syncthreads();
   if (tid == 0) c.epochs[b] = epoch;

@@ -1,0 +1,61 @@
+"""Failure detection and race robustness on a real MI355X:
+* a delayed peer (FLEXAR_FAULT_INJECT=delay) must not change results (flag protocol, not timing);
+* a peer that never signals (FLEXAR_FAULT_INJECT=drop) must surface as FLEXAR_ERR_TIMEOUT naming
+  the stuck slot/peer — never a hang (the reference blocks forever in MPI_Waitall/MPI_Barrier).
+Also the profiling counters (FLEXAR_PROFILE=1)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_delayed_peer_is_still_correct(cuda, monkeypatch):
+    from allreduce_over_mpi_amd.parallel import LocalGroup
+
+    monkeypatch.setenv("FLEXAR_FAULT_INJECT", "delay:1:0:3000")  # rank 1 signals stage 0 3 ms late
+    g = LocalGroup(4, workspace_bytes=32 << 20)
+    try:
+        for spec in ("flat", "ring", "rhd", "oneshot"):
+            xs = [torch.randn(100003, device=cuda) for _ in range(4)]
+            ref = torch.stack([x.double() for x in xs]).sum(0)
+            for _ in range(2):
+                outs = g.all_reduce([x.clone() for x in xs], algo=spec)
+                torch.cuda.synchronize()
+                for o in outs:
+                    assert (o.double() - ref).abs().max().item() < 1e-4, spec
+        g.check()
+    finally:
+        g.close()
+
+
+def test_dropped_signal_times_out(cuda, monkeypatch):
+    from allreduce_over_mpi_amd import FlexarError
+    from allreduce_over_mpi_amd.parallel import LocalGroup
+
+    monkeypatch.setenv("FLEXAR_FAULT_INJECT", "drop:2:0")
+    monkeypatch.setenv("FLEXAR_TIMEOUT_MS", "300")
+    g = LocalGroup(4, workspace_bytes=32 << 20)
+    try:
+        xs = [torch.randn(4096, device=cuda) for _ in range(4)]
+        with pytest.raises(FlexarError) as ei:
+            g.all_reduce(xs, algo="flat")
+            torch.cuda.synchronize()
+            g.check()
+        assert "timed out" in str(ei.value)
+    finally:
+        g.close()
+
+
+def test_profile_stats(cuda, monkeypatch):
+    from allreduce_over_mpi_amd.parallel import Communicator
+
+    monkeypatch.setenv("FLEXAR_PROFILE", "1")
+    c = Communicator(rank=0, world_size=1, workspace_bytes=8 << 20)
+    x = torch.randn(1 << 20, device=cuda)
+    for _ in range(3):
+        c.all_reduce(x, out=torch.empty_like(x))
+    st = c.stats()
+    assert st["calls"] == 3 and st["bytes"] == 3 * 4 * (1 << 20)
+    assert sum(v["calls"] for v in st["profile"].values()) == 3
+    assert all(v["ms"] > 0 for v in st["profile"].values())
+    c.close()

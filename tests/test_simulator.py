@@ -135,3 +135,18 @@ def test_bytes_moved_is_bandwidth_optimal(nv):
             moved += ln * sum(1 for d in dsts.split(", ") if "@3:" not in d)      # remote writes
             moved += ln * sum(1 for s in srcs.split(" + ") if "@3:" not in s)     # remote reads
         assert moved == 2 * (n - 1) * count // n, (spec, moved)
+
+
+@pytest.mark.parametrize("n,spec", [(7, "tree:2,3"), (7, "tree:3,2+push"), (5, "tree:2,2"), (7, "tree:6"),
+                                    (3, "tree:2"), (13, "tree:2,2,3"), (11, "tree:2,3+push+nofuse")])
+def test_lonely_ranks(nv, n, spec):
+    """Non-factorable N: trees over P >= N/2 ranks with N - P lonely ranks folded into partners
+    (the reference's lonely-node design, dead code there: mpi_mod.hpp:983-1099)."""
+    rng = np.random.default_rng(n)
+    for size in (1, 35, 1001, 65539):
+        ins = [rng.standard_normal(size).astype(np.float32) for _ in range(n)]
+        for in_place in (False, True):
+            outs = nv.simulate(spec, ins, grid=3, ncalls=3, in_place=in_place)
+            ref = ref_sum(ins)
+            for o in outs:
+                np.testing.assert_allclose(o, ref, rtol=1e-5, atol=1e-4)
