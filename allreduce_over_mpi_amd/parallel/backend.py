@@ -203,8 +203,10 @@ class FlexarHookState:
         self.calls = 0
 
 
-def flexar_allreduce_hook(state: FlexarHookState, bucket: dist.GradBucket) -> torch.futures.Future[torch.Tensor]:
-    """DDP comm hook: average the gradient bucket with the flexar executor kernel (in place, current stream)."""
+def flexar_allreduce_hook(state, bucket):
+    """DDP comm hook ``(FlexarHookState, dist.GradBucket) -> Future[Tensor]``: average the gradient
+    bucket with the flexar executor kernel (in place, on the current stream). (No annotations: this
+    module uses postponed evaluation and DDP compares the annotation objects.)"""
     buf = bucket.buffer()
     state.comm.all_reduce(buf, op="avg" if buf.is_floating_point() else "sum", algo=state.algo)
     state.calls += 1

@@ -85,6 +85,9 @@ def test_algo_spec_errors(nv):
     with pytest.raises(nv.FlexarError):
         nv.model_cost_us("rhd", 6, 1e6)        # not a power of two
     with pytest.raises(nv.FlexarError):
-        nv.model_cost_us("tree:2,2", 8, 1e6)   # product != N
+        nv.model_cost_us("tree:3", 8, 1e6)     # product < N/2
+    with pytest.raises(nv.FlexarError):
+        nv.model_cost_us("tree:4,4", 8, 1e6)   # product > N
+    assert nv.model_cost_us("tree:2,2", 8, 1e6) > 0  # 4 lonely ranks folded into 4 partners
     with pytest.raises(nv.FlexarError):
         nv.model_cost_us("bogus", 8, 1e6)
