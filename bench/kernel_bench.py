@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--what", default="reduce,group,copy")
     ap.add_argument("--out", default="")
     ap.add_argument("--reduce-mb", type=float, default=256)
+    ap.add_argument("--dtypes", default="float32,bfloat16,float8_e4m3fn")
+    ap.add_argument("--fanins", default="1,2,4,8")
+    ap.add_argument("--iters", type=int, default=20)
     args = ap.parse_args()
     import torch
 
@@ -57,13 +60,13 @@ def main():
 
     what = set(args.what.split(","))
     if "reduce" in what:
-        for dt in (torch.float32, torch.bfloat16, torch.float8_e4m3fn):
+        for dt in [getattr(torch, d) for d in args.dtypes.split(",")]:
             es = torch.tensor([], dtype=dt).element_size()
             n = int(args.reduce_mb * (1 << 20)) // es
-            for k in (1, 2, 4, 8):
+            for k in [int(f) for f in args.fanins.split(",")]:
                 srcs = [torch.randn(n, device=dev).to(dt) for _ in range(k)]
                 out = torch.empty_like(srcs[0])
-                t = timeit(lambda: reduce(srcs, "sum", out=out))
+                t = timeit(lambda: reduce(srcs, "sum", out=out), iters=args.iters)
                 emit(kind="reduce", dtype=str(dt).replace("torch.", ""), fanin=k, bytes_per_src=n * es,
                      us=round(t * 1e6, 2), eff_TBps=round((k + 1) * n * es / t / 1e12, 3))
                 del srcs, out

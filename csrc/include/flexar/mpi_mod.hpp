@@ -31,6 +31,7 @@
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -156,7 +157,7 @@ struct HostComm {
   size_t flag_bytes = 0;
   std::vector<char*> stg;   // per rank staging base (shared mode)
   std::vector<std::atomic<uint64_t>*> flags;
-  std::vector<uint64_t> epochs = std::vector<uint64_t>(kHostMaxGrid, 0);
+  uint64_t epoch = 0;  // one epoch per call for every host workgroup: uniform staging parity per call
   std::map<std::string, std::unique_ptr<Program>> plans;
   std::map<std::string, std::unique_ptr<P2PPlan>> p2p;
   std::vector<char> p2p_stg, outbox, inbox;
@@ -207,7 +208,7 @@ struct HostComm {
       flags[r] = reinterpret_cast<std::atomic<uint64_t>*>(p);
       stg[r] = p + flag_bytes;
     }
-    std::fill(epochs.begin(), epochs.end(), 0);
+    epoch = 0;
     MPI_Barrier(comm);  // flags zeroed everywhere before anyone signals
   }
 };
@@ -248,8 +249,8 @@ struct ShmRun {
     c.blocks_stride = kHostMaxGrid;
     c.stg_half_bytes = h.cap;
     std::atomic<int> rc{0};
+    const uint64_t e = ++h.epoch;
     auto body = [&](int g) {
-      uint64_t e = ++h.epochs[g];
       int x = HostExec<T, OP>::run(P, c, (uint32_t)g, (uint32_t)grid, e);
       if (x) rc.store(x);
     };

@@ -45,8 +45,13 @@ struct DevCtx {
   uint64_t fi_ticks;
 };
 
-// 16-byte vector memory ops (global_load/store_dwordx4). FLEXAR_NT_LOADS / FLEXAR_NT_STORES select the
-// streaming (nontemporal) cache policy for the once-touched payload bytes.
+// 16-byte vector memory ops (global_load/store_dwordx4). Payload bytes are touched once, so loads use
+// the streaming (nontemporal) policy by default: measured on MI355X (bench/kernel_bench.py, profiles/)
+// 6.0-6.5 TB/s vs 5.0-5.2 TB/s with the default policy for fan-in 1..8 reductions and copies.
+// FLEXAR_PLAIN_LOADS restores the default policy; FLEXAR_NT_STORES makes stores streaming too.
+#if !defined(FLEXAR_PLAIN_LOADS) && !defined(FLEXAR_NT_LOADS)
+#define FLEXAR_NT_LOADS 1
+#endif
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ FX_INLINE uint4 ld16(const char* p) {
 #if defined(FLEXAR_NT_LOADS)
@@ -67,6 +72,7 @@ __device__ FX_INLINE void st16(char* p, uint4 x) {
 
 template <typename T, typename OP, int K>
 __device__ FX_INLINE uint4 combine16(const uint4 (&x)[K], float scale, bool sc) {
+  if (K == 1 && !sc) return x[0];  // pure move: no decode/encode round trip (fp8/bf16 copies at HBM rate)
   using A = typename Elem<T>::acc;
   constexpr int E = 16 / sizeof(T);
   T v[E];
@@ -127,6 +133,13 @@ __device__ FX_INLINE void xfer_k(const char* const (&s)[kMaxSrc], char* const (&
   }
   // scalar tail (or whole span when a base address is not 16-B aligned)
   for (uint64_t i = nv * E + threadIdx.x; i < n; i += nt) {
+    if (K == 1 && !sc) {
+      const T y = reinterpret_cast<const T*>(s[0])[i];
+#pragma unroll
+      for (int dd = 0; dd < kMaxDst; ++dd)
+        if (dd < nd) reinterpret_cast<T*>(d[dd])[i] = y;
+      continue;
+    }
     A acc = Elem<T>::load(reinterpret_cast<const T*>(s[0])[i]);
 #pragma unroll
     for (int k = 1; k < K; ++k) acc = OP::apply(acc, Elem<T>::load(reinterpret_cast<const T*>(s[k])[i]));
@@ -261,7 +274,14 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
     ++i;
   }
   __syncthreads();
-  if (tid == 0) c.epochs[b] = epoch;
+  // Advance the epoch of EVERY epoch slot congruent to b (mod grid): after the call all
+  // kMaxGridBlocks slots hold the same value, so the next call — whatever its grid size — sees one
+  // uniform epoch and therefore one staging parity across all its workgroups (a lagging peer still in
+  // call k reads parity(k) while an eager rank in call k+1 writes parity(k+1)). No slot is read in
+  // this call by another workgroup: workgroup b2 reads only slot b2 < grid, and b2 == b (mod grid)
+  // implies b2 == b.
+  if (tid == 0)
+    for (uint32_t j = b; j < kMaxGridBlocks; j += grid) c.epochs[j] = epoch;
 }
 
 // Production launch: one rank per process, context by value.

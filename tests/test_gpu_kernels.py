@@ -172,3 +172,23 @@ def test_communicator_single_rank(cuda):
     torch.cuda.synchronize()
     torch.testing.assert_close(y, 2 * x)
     c.close()
+
+
+def test_group_varying_grid_between_calls(cuda, groups):
+    """Consecutive calls with different grid sizes must agree on one staging parity per call."""
+    n = 4
+    grp = groups[n]
+    g = torch.Generator(device=cuda).manual_seed(21)
+    try:
+        for it, (grid, size, spec) in enumerate([(8, 300001, "flat"), (32, 1 << 20, "flat"), (4, 5000, "ring"),
+                                                 (16, 777777, "rhd"), (8, 300001, "flat+push"), (64, 65536, "ring:2")]):
+            grp.set_grid(grid)
+            xs = [torch.randn(size, device=cuda, generator=g) for _ in range(n)]
+            ref = torch.stack([x.double() for x in xs]).sum(0)
+            outs = grp.all_reduce([x.clone() for x in xs], algo=spec)
+            torch.cuda.synchronize()
+            for o in outs:
+                assert (o.double() - ref).abs().max().item() < 1e-4, (it, grid, spec)
+        grp.check()
+    finally:
+        grp.set_grid(0)
