@@ -35,6 +35,8 @@
 
 namespace flexar {
 
+constexpr double kLLMaxBytes = 1 << 20;  // LL protocol only for latency-bound sizes
+
 struct XgmiModel {
   double alpha_launch_us = 6.0;  // kernel launch + first-touch
   double alpha_sync_us = 2.0;    // one cross-GPU signal->wait hop
@@ -69,6 +71,9 @@ struct XgmiModel {
     switch (s.kind) {
       case AlgoKind::ONESHOT:
         return alpha_launch_us + alpha_sync_us + fanout_us(S, N - 1) + reduce_us(N * S);
+      case AlgoKind::LL:  // flag-free 8-B {data, epoch} granules: half the hop cost, 2x the bytes
+        if (S > kLLMaxBytes) return 1e30;
+        return alpha_launch_us + 0.5 * alpha_sync_us + fanout_us(2 * S, N - 1) + reduce_us(2 * N * S);
       case AlgoKind::RING: {
         int C = s.channels < 1 ? 1 : s.channels;
         double blk = S / ((double)C * N);

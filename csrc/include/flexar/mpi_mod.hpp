@@ -231,6 +231,7 @@ inline int resolve_algo(HostComm& h, double bytes, AlgoSpec* s) {
     return 1;
   }
   if (s->kind == AlgoKind::AUTO) *s = select_plan(h.model, h.size, bytes);
+  if (s->kind == AlgoKind::LL) s->kind = AlgoKind::ONESHOT;  // LL granules are a device protocol
   if (s->kind == AlgoKind::TREE && (!h.shared || s->ag == AgMode::AUTO)) s->ag = AgMode::PUSH;
   return 0;
 }

@@ -85,6 +85,11 @@ class Planner {
     } else if (spec.kind == AlgoKind::ONESHOT) {
       build_oneshot();
       P->desc = spec.str();
+    } else if (spec.kind == AlgoKind::LL) {
+      // executed by the dedicated LL kernel (no op program): only the staging size is planned
+      stg = (uint64_t)N * ((count * esize + 3) / 4) * 8 / esize + align;
+      finish_channel();
+      P->desc = spec.str();
     } else {
       if (err) *err = "planner needs a concrete algorithm (not auto)";
       return false;
@@ -467,8 +472,10 @@ class Planner {
     xfer(count, {loc(BUF_IN, r, 0)}, dsts, 1.0f);
     signal(peers, 0);
     wait(peers, 0);
-    std::vector<Loc> srcs{loc(BUF_IN, r, 0)};
-    for (uint32_t p : peers) srcs.push_back(loc(BUF_STG, r, base + (uint64_t)p * cnt_al));
+    // every rank reduces the full buffer: sum in rank order so all ranks get bit-identical results
+    std::vector<Loc> srcs;
+    for (uint32_t p = 0; p < N; ++p)
+      srcs.push_back(p == r ? loc(BUF_IN, r, 0) : loc(BUF_STG, r, base + (uint64_t)p * cnt_al));
     xfer(count, srcs, {loc(BUF_OUT, r, 0)}, scale);
     finish_channel();
   }

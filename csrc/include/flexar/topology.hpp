@@ -23,7 +23,7 @@
 
 namespace flexar {
 
-enum class AlgoKind { AUTO, RING, TREE, ONESHOT };
+enum class AlgoKind { AUTO, RING, TREE, ONESHOT, LL };
 enum class AgMode { AUTO, PUSH, PULL };
 
 struct AlgoSpec {
@@ -38,6 +38,7 @@ struct AlgoSpec {
     switch (kind) {
       case AlgoKind::AUTO: ss << "auto"; break;
       case AlgoKind::ONESHOT: ss << "oneshot"; break;
+      case AlgoKind::LL: ss << "ll"; break;
       case AlgoKind::RING: ss << "ring"; if (channels > 1) ss << ":" << channels; break;
       case AlgoKind::TREE:
         ss << "tree:";
@@ -175,6 +176,7 @@ inline bool parse_algo(const std::string& raw, int nranks, AlgoSpec* spec, std::
   if (c != std::string::npos) head = s.substr(0, c), arg = s.substr(c + 1);
   if (head.empty() || head == "auto") { spec->kind = AlgoKind::AUTO; return true; }
   if (head == "oneshot") { spec->kind = AlgoKind::ONESHOT; return true; }
+  if (head == "ll" || head == "oneshot_ll") { spec->kind = AlgoKind::LL; return true; }
   if (head == "ring") {
     spec->kind = AlgoKind::RING;
     if (!arg.empty()) {
@@ -245,6 +247,7 @@ inline std::vector<int> ring_order(int nranks, int channel) {
 inline std::vector<AlgoSpec> enumerate_plans(int nranks) {
   std::vector<AlgoSpec> out;
   if (nranks <= 1) return out;
+  AlgoSpec ll; ll.kind = AlgoKind::LL; out.push_back(ll);
   AlgoSpec os; os.kind = AlgoKind::ONESHOT; out.push_back(os);
   int maxc = max_ring_channels(nranks);
   for (int c = 1; c <= maxc; c *= 2) {

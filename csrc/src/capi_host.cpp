@@ -117,10 +117,12 @@ struct HostReduce {
   }
 };
 
-static bool spec_for(const char* spec, int nranks, double bytes, AlgoSpec* s, std::string* err) {
+static bool spec_for(const char* spec, int nranks, double bytes, AlgoSpec* s, std::string* err,
+                     bool host_only = false) {
   if (!parse_algo(spec ? spec : "auto", nranks, s, err)) return false;
   if (s->kind == AlgoKind::AUTO) *s = select_plan(XgmiModel::from_env(), nranks, bytes);
   if (s->kind == AlgoKind::TREE && s->ag == AgMode::AUTO) s->ag = AgMode::PULL;
+  if (s->kind == AlgoKind::LL && host_only) s->kind = AlgoKind::ONESHOT;  // LL is a device-only protocol
   return true;
 }
 
@@ -194,7 +196,7 @@ int flexar_simulate(const char* spec, int nranks, size_t count, int dtype, int o
   if (!op_supported(dtype, op)) { set_error("unsupported dtype/op"); return FLEXAR_ERR_UNSUPPORTED; }
   AlgoSpec s;
   std::string err;
-  if (!spec_for(spec, nranks, (double)count * es, &s, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  if (!spec_for(spec, nranks, (double)count * es, &s, &err, true)) { set_error(err); return FLEXAR_ERR_INVALID; }
   float fs = scale * (op == FLEXAR_AVG ? 1.0f / (float)nranks : 1.0f);
   std::vector<Program> progs(nranks);
   for (int r = 0; r < nranks; ++r) {

@@ -105,6 +105,8 @@ using namespace flexar;
 struct flexar_comm {
   int rank = 0, nranks = 1, device = 0;
   size_t ws_bytes = 0, half_bytes = 0;
+  size_t ll_bytes = 0;    // LL granule region at the end of each parity half (0 = LL disabled)
+  size_t exec_half = 0;   // part of each half available to op programs
   char* stg = nullptr;
   uint64_t* flags = nullptr;
   uint64_t* epochs = nullptr;
@@ -154,6 +156,17 @@ static int resolve_spec(flexar_comm* c, const char* algo, double bytes, AlgoSpec
   if (s.kind == AlgoKind::TREE && s.ag == AgMode::AUTO) s.ag = AgMode::PULL;
   *out = s;
   return 0;
+}
+
+// LL is valid for 1/2/4-byte elements up to kLLMaxBytes when the communicator reserved its region.
+static bool ll_usable(flexar_comm* c, uint64_t count, uint32_t es) {
+  return c->ll_bytes && es <= 4 && (double)count * es <= kLLMaxBytes && c->nranks > 1;
+}
+static int ll_grid(flexar_comm* c, uint64_t count, uint32_t es) {
+  uint64_t words = (count * es + 3) / 4;
+  uint64_t g = (words + 2 * kExecThreads - 1) / (2 * kExecThreads);  // ~2 words per lane
+  g = std::max<uint64_t>(1, std::min<uint64_t>(g, (uint64_t)std::min(c->max_grid, 64)));
+  return (int)g;
 }
 
 // Decide the bit-level barrier-after flags: an XFER needs a workgroup barrier before the next
@@ -220,9 +233,13 @@ static int choose_grid(flexar_comm* c, uint64_t bytes, uint32_t nchan) {
 
 static void fill_ctx(flexar_comm* c, DevProgram* dp, const void* in, void* out, DevCtx* x) {
   memset(x, 0, sizeof(*x));
-  x->ops = dp->d_ops;
-  x->chan_start = dp->d_chan;
-  x->nchan = dp->prog.nchan;
+  if (dp) {
+    x->ops = dp->d_ops;
+    x->chan_start = dp->d_chan;
+    x->nchan = dp->prog.nchan;
+  }
+  x->ll_off = c->exec_half;
+  x->nranks = c->nranks;
   x->rank = c->rank;
   x->local[BUF_IN] = (char*)in;
   x->local[BUF_OUT] = (char*)out;
@@ -248,16 +265,16 @@ static int plan_pieces(flexar_comm* c, const AlgoSpec& s, uint64_t count, uint32
   int rc = get_program(c, s, count, esize, fs, &dp);
   if (rc) return rc;
   uint64_t need = dp->prog.stg_elems * esize;
-  if (need <= c->half_bytes) { *piece = count; return 0; }
+  if (need <= c->exec_half) { *piece = count; return 0; }
   uint64_t align = std::max<uint64_t>(1, kStageAlignBytes / esize) * c->nranks;
-  uint64_t pieces = (need + c->half_bytes - 1) / c->half_bytes;
+  uint64_t pieces = (need + c->exec_half - 1) / c->exec_half;
   for (int tries = 0; tries < 64; ++tries, ++pieces) {
     uint64_t p = (count + pieces - 1) / pieces;
     p = (p + align - 1) / align * align;
     if (p == 0) p = align;
     rc = get_program(c, s, p, esize, fs, &dp);
     if (rc) return rc;
-    if (dp->prog.stg_elems * esize <= c->half_bytes) { *piece = p; return 0; }
+    if (dp->prog.stg_elems * esize <= c->exec_half) { *piece = p; return 0; }
   }
   set_error("workspace too small for this algorithm");
   return FLEXAR_ERR_NOMEM;
@@ -294,6 +311,10 @@ static int alloc_workspace(flexar_comm* c, size_t ws) {
   c->ws_bytes = (ws + 511) / 512 * 512;
   c->half_bytes = c->ws_bytes / 2 / kStageAlignBytes * kStageAlignBytes;
   FX_HIP(hipMalloc(&c->stg, c->ws_bytes));
+  FX_HIP(hipMemset(c->stg, 0, c->ws_bytes));  // LL granules: zero = epoch 0, never matches a live call
+  c->ll_bytes = (size_t)(2 * kLLMaxBytes) * c->nranks;
+  if (c->ll_bytes * 2 > c->half_bytes) c->ll_bytes = 0;
+  c->exec_half = c->half_bytes - c->ll_bytes;
   FX_HIP(hipExtMallocWithFlags((void**)&c->flags, kFlagWords * sizeof(uint64_t), hipDeviceMallocUncached));
   FX_HIP(hipMemset(c->flags, 0, kFlagWords * sizeof(uint64_t)));
   FX_HIP(hipMalloc(&c->epochs, kMaxGridBlocks * sizeof(uint64_t)));
@@ -490,6 +511,24 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
   std::lock_guard<std::mutex> lk(c->mu);
   AlgoSpec s;
   if ((rc = resolve_spec(c, algo, (double)count * es, &s))) return rc;
+  if (s.kind == AlgoKind::LL && !ll_usable(c, count, es)) s.kind = AlgoKind::ONESHOT;
+  if (s.kind == AlgoKind::LL) {
+    DevCtx x;
+    fill_ctx(c, nullptr, in, out, &x);
+    x.count = count;
+    x.scale = fs;
+    LaunchArgs la;
+    la.kind = LAUNCH_LL;
+    la.ctx = x;
+    la.grid = ll_grid(c, count, es);
+    la.stream = st;
+    if (roctx().push) roctx().push(("flexar allreduce ll " + std::to_string(count * es) + "B").c_str());
+    c->calls++;
+    c->bytes += count * es;
+    rc = launch_dtype(dtype, op, la);
+    if (roctx().pop) roctx().pop();
+    return rc;
+  }
   uint64_t piece = count;
   if (c->nranks > 1 && (rc = plan_pieces(c, s, count, es, fs, &piece))) return rc;
   const std::string sdesc = s.str();
@@ -599,13 +638,36 @@ int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
     int rc = resolve_spec(comms[r], algo, (double)count * es, &specs[r]);
     if (rc) return rc;
   }
+  static thread_local DevCtx* d_ctx = nullptr;
+  if (!d_ctx) FX_HIP(hipMalloc(&d_ctx, sizeof(DevCtx) * kMaxRanks));
+  if (specs[0].kind == AlgoKind::LL && !ll_usable(comms[0], count, es))
+    for (auto& sp : specs) sp.kind = AlgoKind::ONESHOT;
+  if (specs[0].kind == AlgoKind::LL) {
+    std::vector<DevCtx> h(nranks);
+    for (int r = 0; r < nranks; ++r) {
+      const void* in = ins && ins[r] ? ins[r] : outs[r];
+      fill_ctx(comms[r], nullptr, in, outs[r], &h[r]);
+      h[r].count = count;
+      h[r].scale = fs;
+    }
+    int grid = std::max(1, std::min(ll_grid(comms[0], count, es), (int)kGroupMaxBlocks / nranks));
+    FX_HIP(hipMemcpyAsync(d_ctx, h.data(), sizeof(DevCtx) * nranks, hipMemcpyHostToDevice, st));
+    LaunchArgs la;
+    la.kind = LAUNCH_LL_GROUP;
+    la.d_ctxs = d_ctx;
+    la.nranks = nranks;
+    la.grid = grid;
+    la.stream = st;
+    int rc = launch_dtype(dtype, op, la);
+    if (rc) return rc;
+    FX_HIP(hipStreamSynchronize(st));
+    return 0;
+  }
   uint64_t piece = count;
   if (nranks > 1) {
     int rc = plan_pieces(comms[0], specs[0], count, es, fs, &piece);
     if (rc) return rc;
   }
-  static thread_local DevCtx* d_ctx = nullptr;
-  if (!d_ctx) FX_HIP(hipMalloc(&d_ctx, sizeof(DevCtx) * kMaxRanks));
   for (uint64_t off = 0; off < count; off += piece) {
     uint64_t n = std::min<uint64_t>(piece, count - off);
     std::vector<DevCtx> h(nranks);

@@ -43,6 +43,11 @@ struct DevCtx {
   uint32_t fi_kind;
   uint32_t fi_slot;
   uint64_t fi_ticks;
+  // LL protocol (ll_body): no op program
+  uint64_t ll_off;  // byte offset of the LL granule region inside each staging parity half
+  uint32_t nranks;
+  uint64_t count;  // elements
+  float scale;
 };
 
 // 16-byte vector memory ops (global_load/store_dwordx4). Payload bytes are touched once, so loads use
@@ -282,6 +287,105 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
   // implies b2 == b.
   if (tid == 0)
     for (uint32_t j = b; j < kMaxGridBlocks; j += grid) c.epochs[j] = epoch;
+}
+
+// ---------------------------------------------------------------------------------------------
+// LL ("low latency") one-shot for latency-bound sizes: every 4-byte payload word travels as an
+// 8-byte {word, epoch} granule written with ONE system-scope store into every peer's staging and
+// read back with system-scope (cache-bypassing) loads. The data carries its own readiness, so there
+// is no SIGNAL/WAIT, no L2 write-back (release) and no L2 invalidate (acquire) on the critical path
+// (MI355X_MICROARCH.md "handoff-1to1": data-tagged granules are the cheapest hand-off). Every rank
+// reduces the words of all ranks in rank order, so all ranks get bit-identical results.
+// Element types of 1, 2 or 4 bytes (a word holds 4 / sizeof(T) elements).
+__device__ FX_INLINE uint32_t ld_word(const char* base, uint64_t w, uint64_t nbytes) {
+  const uint64_t o = w * 4;
+  if (o + 4 <= nbytes) return *reinterpret_cast<const uint32_t*>(base + o);
+  uint32_t v = 0;
+  for (uint64_t k = o; k < nbytes; ++k) v |= (uint32_t)(uint8_t)base[k] << (8 * (k - o));
+  return v;
+}
+__device__ FX_INLINE void st_word(char* base, uint64_t w, uint64_t nbytes, uint32_t v) {
+  const uint64_t o = w * 4;
+  if (o + 4 <= nbytes) {
+    *reinterpret_cast<uint32_t*>(base + o) = v;
+    return;
+  }
+  for (uint64_t k = o; k < nbytes; ++k) base[k] = (char)((v >> (8 * (k - o))) & 0xff);
+}
+
+template <typename T, typename OP>
+__device__ FX_INLINE void ll_body(const DevCtx& c, const uint32_t b, const uint32_t grid) {
+  using A = typename Elem<T>::acc;
+  constexpr int E = 4 / sizeof(T);
+  __shared__ int s_abort;
+  const uint32_t tid = threadIdx.x;
+  if (tid == 0) s_abort = 0;
+  __syncthreads();
+  const uint64_t epoch = c.epochs[b] + 1;
+  const uint64_t par = ((epoch & 1) ? c.stg_half_bytes : 0) + c.ll_off;  // LL-only region: stale bytes
+  const uint64_t nbytes = c.count * sizeof(T), W = (nbytes + 3) / 4;        // there are older granules
+  const uint32_t N = c.nranks, r = c.rank;
+  uint64_t lo, hi;
+  slice_range(W, b, grid, 1, &lo, &hi);
+  const char* in = c.local[BUF_IN];
+  char* out = c.local[BUF_OUT];
+  // phase 1: publish my words to every peer
+  for (uint64_t w = lo + tid; w < hi; w += blockDim.x) {
+    const uint64_t g = (epoch << 32) | ld_word(in, w, nbytes);
+    for (uint32_t p = 0; p < N; ++p)
+      if (p != r) st_flag(reinterpret_cast<uint64_t*>(c.peer_stg[p] + par) + (uint64_t)r * W + w, g);
+  }
+  // phase 2: gather every rank's word (own from registers' source), reduce in rank order
+  const uint64_t* mine = reinterpret_cast<const uint64_t*>(c.peer_stg[r] + par);
+  const bool sc = Elem<T>::is_float && c.scale != 1.0f;
+  for (uint64_t w = lo + tid; w < hi; w += blockDim.x) {
+    A acc[E];
+    for (uint32_t p = 0; p < N; ++p) {
+      uint32_t v;
+      if (p == r) {
+        v = ld_word(in, w, nbytes);
+      } else {
+        uint64_t g = ld_flag(const_cast<uint64_t*>(mine + (uint64_t)p * W + w));
+        if ((g >> 32) != (epoch & 0xffffffffu)) {
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          do {
+            __builtin_amdgcn_s_sleep(1);
+            g = ld_flag(const_cast<uint64_t*>(mine + (uint64_t)p * W + w));
+            if (__builtin_amdgcn_s_memrealtime() - t0 > c.timeout_ticks) {
+              __hip_atomic_store(c.err, (uint32_t)(0x80000000u | (0xffu << 8) | p), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
+              s_abort = 1;
+              break;
+            }
+          } while ((g >> 32) != (epoch & 0xffffffffu));
+        }
+        v = (uint32_t)g;
+      }
+      T e[E];
+      __builtin_memcpy(e, &v, 4);
+#pragma unroll
+      for (int k = 0; k < E; ++k) acc[k] = p == 0 ? Elem<T>::load(e[k]) : OP::apply(acc[k], Elem<T>::load(e[k]));
+    }
+    T e[E];
+#pragma unroll
+    for (int k = 0; k < E; ++k) e[k] = Elem<T>::store(sc ? (A)(acc[k] * (A)c.scale) : acc[k]);
+    uint32_t v;
+    __builtin_memcpy(&v, e, 4);
+    st_word(out, w, nbytes, v);
+    if (s_abort) break;
+  }
+  __syncthreads();
+  if (tid == 0)
+    for (uint32_t j = b; j < kMaxGridBlocks; j += grid) c.epochs[j] = epoch;
+}
+
+template <typename T, typename OP>
+__global__ void __launch_bounds__(kExecThreads) ll_kernel(DevCtx c) {
+  if constexpr (sizeof(T) <= 4) ll_body<T, OP>(c, blockIdx.x, gridDim.x);
+}
+template <typename T, typename OP>
+__global__ void __launch_bounds__(kExecThreads) ll_group_kernel(const DevCtx* ctxs, uint32_t grid_per_rank) {
+  if constexpr (sizeof(T) <= 4) ll_body<T, OP>(ctxs[blockIdx.x / grid_per_rank], blockIdx.x % grid_per_rank, grid_per_rank);
 }
 
 // Production launch: one rank per process, context by value.

@@ -22,6 +22,15 @@ inline int launch_one(const LaunchArgs& a) {
       hipLaunchKernelGGL((reduce_kernel<T, OP>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.srcs, a.nsrc,
                          a.dst, a.n, a.scale, a.vec);
       break;
+    case LAUNCH_LL:
+      if (sizeof(T) > 4) return FLEXAR_ERR_UNSUPPORTED;
+      hipLaunchKernelGGL((ll_kernel<T, OP>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
+      break;
+    case LAUNCH_LL_GROUP:
+      if (sizeof(T) > 4) return FLEXAR_ERR_UNSUPPORTED;
+      hipLaunchKernelGGL((ll_group_kernel<T, OP>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0, a.stream,
+                         a.d_ctxs, (uint32_t)a.grid);
+      break;
     default:
       return FLEXAR_ERR_INVALID;
   }

@@ -8,7 +8,7 @@
 
 namespace flexar {
 
-enum LaunchKind { LAUNCH_EXEC = 0, LAUNCH_GROUP = 1, LAUNCH_REDUCE = 2 };
+enum LaunchKind { LAUNCH_EXEC = 0, LAUNCH_GROUP = 1, LAUNCH_REDUCE = 2, LAUNCH_LL = 3, LAUNCH_LL_GROUP = 4 };
 
 struct LaunchArgs {
   int kind = LAUNCH_EXEC;

@@ -69,7 +69,7 @@ def test_reduce_kernel_int(cuda, op):
 def _specs(n):
     from allreduce_over_mpi_amd import _native as nv
 
-    base = ["flat", "flat+push", "ring", "oneshot"]
+    base = ["flat", "flat+push", "ring", "oneshot", "ll"]
     base += [p for p in nv.enumerate_plans(n) if p.startswith("tree:") or p.startswith("ring:")]
     base += [p + "+push" for p in nv.enumerate_plans(n) if p.startswith("tree:") and "," in p]
     return sorted(set(base))
@@ -192,3 +192,32 @@ def test_group_varying_grid_between_calls(cuda, groups):
         grp.check()
     finally:
         grp.set_grid(0)
+
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.int8, torch.float8_e4m3fn,
+                                   torch.int32])
+@pytest.mark.parametrize("n", [2, 8])
+def test_group_ll_protocol(cuda, groups, dtype, n):
+    """LL one-shot: 8-B {word, epoch} granules, tails of 1..3 bytes, bit-identical across ranks."""
+    grp = groups[n]
+    g = torch.Generator(device=cuda).manual_seed(31)
+    for size in (1, 3, 1001, 4099, 65537):
+        if dtype in (torch.int8, torch.int32):
+            xs = [torch.randint(-3, 4, (size,), device=cuda, generator=g, dtype=dtype) for _ in range(n)]
+        else:
+            xs = [torch.randn(size, device=cuda, generator=g).to(dtype) for _ in range(n)]
+        for _ in range(3):
+            outs = grp.all_reduce([x.clone() for x in xs], algo="ll")
+            torch.cuda.synchronize()
+            acc = xs[0].float()
+            for x in xs[1:]:
+                acc = acc + x.float()
+            want = acc.to(dtype)
+            for o in outs:
+                assert torch.equal(o.view(torch.uint8), outs[0].view(torch.uint8))  # identical on all ranks
+                if dtype in (torch.float32, torch.int8, torch.int32):
+                    assert torch.equal(o, want), (dtype, size)
+                else:
+                    assert torch.equal(o.view(torch.uint8), want.view(torch.uint8)), (dtype, size)
+    grp.check()
