@@ -79,7 +79,9 @@ def main():
     count = nbytes // esize
     nbytes = count * esize
 
-    comm = Communicator(workspace_bytes=max(512 << 20, 2 * nbytes + (64 << 20)))
+    os.environ.setdefault("FLEXAR_TIMEOUT_MS", "5000")  # a broken candidate costs seconds, not minutes
+    ws_bytes = max(512 << 20, 2 * nbytes + (64 << 20))
+    comm = Communicator(workspace_bytes=ws_bytes)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
     x = torch.randn(count, device=dev, dtype=torch.float32, generator=gen)
@@ -143,6 +145,7 @@ def main():
             cands += ["rhd+pull"]
         best, best_t = None, float("inf")
         for spec in cands:
+            failed = 0.0
             try:
                 ok, err = check(spec)
                 okv = max_over_ranks(0.0 if ok else 1.0) == 0.0
@@ -151,13 +154,22 @@ def main():
                     log(rank, f"tuner: {spec} produced wrong results (err {err:.3g}); excluded")
                     continue
                 t = timed(spec, 3)
-                tune_log[spec] = round(busbw_gbps(nbytes, t, world), 2)
-                log(rank, f"tuner: {spec:12s} {t*1e3:8.3f} ms  busbw {busbw_gbps(nbytes, t, world):8.1f} GB/s")
-                if t < best_t:
-                    best, best_t = spec, t
+                comm.check()
             except nv.FlexarError as e:
+                failed = 1.0
                 tune_log[spec] = f"error: {e}"
-                log(rank, f"tuner: {spec} failed: {e}")
+                log(rank, f"tuner: {spec} failed on this rank: {e}")
+            if max_over_ranks(failed) != 0.0:
+                # a failed candidate may leave the communicator's epochs/flags inconsistent: rebuild it
+                tune_log.setdefault(spec, "failed on a peer")
+                comm.close()
+                torch.cuda.synchronize()
+                comm = Communicator(workspace_bytes=ws_bytes)
+                continue
+            tune_log[spec] = round(busbw_gbps(nbytes, t, world), 2)
+            log(rank, f"tuner: {spec:12s} {t*1e3:8.3f} ms  busbw {busbw_gbps(nbytes, t, world):8.1f} GB/s")
+            if t < best_t:
+                best, best_t = spec, t
         if best is None:
             raise SystemExit("no flexar algorithm produced correct results")
         # grid size for the winner
