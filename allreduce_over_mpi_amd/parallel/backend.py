@@ -68,6 +68,10 @@ class FlexarProcessGroup(dist.ProcessGroup):
         self._gpu_fallback = None
         self.algo = os.environ.get("FLEXAR_ALGO") or None
         self.stats = {"flexar_allreduce": 0, "fallback": 0}
+        # like ProcessGroupNCCL: collectives run on a side stream so they overlap the caller's compute
+        # (DDP backward); the returned Work's CUDA-aware future makes the consumer stream wait on it
+        self.async_stream = os.environ.get("FLEXAR_PG_SYNC_STREAM", "0") != "1"
+        self._streams = {}
 
     # ------------------------------------------------------------------ plumbing
     def getBackendName(self):
@@ -113,17 +117,34 @@ class FlexarProcessGroup(dist.ProcessGroup):
         opname = _redop_name(opts.reduceOp)
         if not self._flexar_ok(tensor_list, opname):
             return self._fallback(tensor_list).allreduce(tensor_list, opts)
-        comm = self.comm(tensor_list[0].device.index)
-        for t in tensor_list:
-            if t.dtype == torch.bool:
-                t8 = t.view(torch.uint8)
-                boolop = {"sum": "max", "max": "max", "bor": "max", "avg": "max", "prod": "min", "min": "min",
-                          "band": "min", "bxor": "bxor"}[opname]
-                comm.all_reduce(t8, op=boolop, algo=self.algo)
-            else:
-                comm.all_reduce(t, op=opname, algo=self.algo)
-            self.stats["flexar_allreduce"] += 1
-        return _done_work(tensor_list)
+        dev = tensor_list[0].device
+        comm = self.comm(dev.index)
+        cur = torch.cuda.current_stream(dev)
+        side = self._side_stream(dev) if self.async_stream else cur
+        if side is not cur:
+            side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            for t in tensor_list:
+                if side is not cur:
+                    t.record_stream(side)
+                if t.dtype == torch.bool:
+                    t8 = t.view(torch.uint8)
+                    boolop = {"sum": "max", "max": "max", "bor": "max", "avg": "max", "prod": "min", "min": "min",
+                              "band": "min", "bxor": "bxor"}[opname]
+                    comm.all_reduce(t8, op=boolop, algo=self.algo)
+                else:
+                    comm.all_reduce(t, op=opname, algo=self.algo)
+                self.stats["flexar_allreduce"] += 1
+            fut = torch.futures.Future(devices=[dev])
+            fut.set_result(tensor_list)  # records an event on the side stream; wait() joins it
+        return _create_work_from_future(fut)
+
+    def _side_stream(self, dev):
+        s = self._streams.get(dev.index)
+        if s is None:
+            s = torch.cuda.Stream(device=dev)
+            self._streams[dev.index] = s
+        return s
 
     def allreduce_coalesced(self, tensor_list, opts=AllreduceCoalescedOptions()):
         o = AllreduceOptions()
@@ -201,6 +222,14 @@ class FlexarHookState:
         self.comm = communicator or Communicator(group=process_group)
         self.algo = algo
         self.calls = 0
+        self._streams = {}
+
+    def stream(self, dev):
+        s = self._streams.get(dev.index)
+        if s is None:
+            s = torch.cuda.Stream(device=dev)
+            self._streams[dev.index] = s
+        return s
 
 
 def flexar_allreduce_hook(state, bucket):
@@ -208,8 +237,13 @@ def flexar_allreduce_hook(state, bucket):
     bucket with the flexar executor kernel (in place, on the current stream). (No annotations: this
     module uses postponed evaluation and DDP compares the annotation objects.)"""
     buf = bucket.buffer()
-    state.comm.all_reduce(buf, op="avg" if buf.is_floating_point() else "sum", algo=state.algo)
+    cur = torch.cuda.current_stream(buf.device)
+    side = state.stream(buf.device)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        buf.record_stream(side)
+        state.comm.all_reduce(buf, op="avg" if buf.is_floating_point() else "sum", algo=state.algo)
+        fut = torch.futures.Future(devices=[buf.device])
+        fut.set_result(buf)  # CUDA-aware: DDP's wait joins the side stream, backward keeps overlapping
     state.calls += 1
-    fut = torch.futures.Future()
-    fut.set_result(buf)
     return fut

@@ -46,6 +46,12 @@
 
 extern "C" int flexar_pointer_is_device(const void* p);  // libflexar: hipPointerGetAttributes
 
+// Feature probe (reference mpi_mod.hpp:8-12 printed "FlexTree enabled").
+static inline int FT_enabled() {
+  fprintf(stdout, "FlexTree enabled (flexar %s, MI355X-native)\n", flexar_version());
+  return 0;
+}
+
 namespace flexar {
 namespace mpi {
 

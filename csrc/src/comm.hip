@@ -28,6 +28,7 @@
 #include "launch.hpp"
 #include "flexar/cost_model.hpp"
 #include "flexar/flexar.h"
+#include "flexar/log.hpp"
 #include "flexar/planner.hpp"
 #include "internal.hpp"
 
@@ -209,6 +210,10 @@ static int get_program(flexar_comm* c, const AlgoSpec& s, uint64_t count, uint32
   Planner pl(c->nranks, c->rank, count, esize, fscale);
   if (!pl.build(s, &dp->prog, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
   mark_barriers(dp->prog, c->rank);
+  logf(LOG_INFO, c->rank, "plan %s: count=%llu esize=%u ops=%zu channels=%u staging=%llu B", s.str().c_str(),
+       (unsigned long long)count, esize, dp->prog.ops.size(), dp->prog.nchan,
+       (unsigned long long)(dp->prog.stg_elems * esize));
+  if (log_level() >= LOG_DEBUG) logf(LOG_DEBUG, c->rank, "%s", dump_program(dp->prog, c->rank).c_str());
   size_t ob = dp->prog.ops.size() * sizeof(Op), cb = dp->prog.chan_start.size() * sizeof(uint32_t);
   FX_HIP(hipMalloc(&dp->d_ops, ob ? ob : sizeof(Op)));
   FX_HIP(hipMalloc(&dp->d_chan, cb));
@@ -350,10 +355,10 @@ static void init_defaults(flexar_comm* c) {
   const char* a = getenv("FLEXAR_ALGO");
   std::string err;
   if (a && *a) {
-    if (!parse_algo(a, c->nranks, &c->spec, &err)) fprintf(stderr, "[flexar] ignoring FLEXAR_ALGO: %s\n", err.c_str());
+    if (!parse_algo(a, c->nranks, &c->spec, &err)) logf(LOG_WARN, c->rank, "ignoring FLEXAR_ALGO: %s", err.c_str());
   } else if (getenv("FT_TOPO")) {  // reference compatibility: FT_TOPO selects the algorithm
     if (!parse_ft_topo(getenv("FT_TOPO"), c->nranks, &c->spec, &err))
-      fprintf(stderr, "[flexar] ignoring FT_TOPO: %s\n", err.c_str());
+      logf(LOG_WARN, c->rank, "ignoring FT_TOPO: %s", err.c_str());
   }
 }
 
