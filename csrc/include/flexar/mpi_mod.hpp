@@ -45,6 +45,7 @@
 #include "flexar/planner.hpp"
 
 extern "C" int flexar_pointer_is_device(const void* p);  // libflexar: hipPointerGetAttributes
+extern "C" int flexar_copy_device_host(void* dst, const void* src, size_t bytes);  // synchronous hipMemcpy
 
 // Feature probe (reference mpi_mod.hpp:8-12 printed "FlexTree enabled").
 static inline int FT_enabled() {
@@ -166,7 +167,7 @@ struct HostComm {
   uint64_t epoch = 0;  // one epoch per call for every host workgroup: uniform staging parity per call
   std::map<std::string, std::unique_ptr<Program>> plans;
   std::map<std::string, std::unique_ptr<P2PPlan>> p2p;
-  std::vector<char> p2p_stg, outbox, inbox;
+  std::vector<char> p2p_stg, outbox, inbox, host_stage;
   std::unique_ptr<Pool> pool;
   XgmiModel model = XgmiModel::from_env();
   int threads = 1;
@@ -447,10 +448,19 @@ inline int allreduce(const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
   const size_t es = dtype_size(dt);
   if (count == 0) return MPI_SUCCESS;
   if (flexar_pointer_is_device(recvbuf)) {
-    flexar_comm_t c = device_comm(comm);
-    int rc = flexar_allreduce(c, in, recvbuf, count, dt, op, nullptr);
-    if (rc) { fprintf(stderr, "[flexar] allreduce: %s\n", flexar_last_error()); return MPI_ERR_OTHER; }
-    return MPI_SUCCESS;  // stream-ordered on the default stream, like a CUDA-aware MPI
+    HostComm* hc = host_comm(comm);
+    if (hc->shared || size <= 1) {  // one node: xGMI/IPC GPU engine
+      flexar_comm_t c = device_comm(comm);
+      int rc = flexar_allreduce(c, in, recvbuf, count, dt, op, nullptr);
+      if (rc) { fprintf(stderr, "[flexar] allreduce: %s\n", flexar_last_error()); return MPI_ERR_OTHER; }
+      return MPI_SUCCESS;  // stream-ordered on the default stream, like a CUDA-aware MPI
+    }
+    // ranks on several nodes: IPC cannot span nodes -> stage through host memory and run the p2p engine
+    hc->host_stage.resize(count * es);
+    if (flexar_copy_device_host(hc->host_stage.data(), in, count * es)) return MPI_ERR_OTHER;
+    int rc = allreduce(MPI_IN_PLACE, hc->host_stage.data(), count, datatype, mop, comm);
+    if (rc == MPI_SUCCESS && flexar_copy_device_host(recvbuf, hc->host_stage.data(), count * es)) rc = MPI_ERR_OTHER;
+    return rc;
   }
   if (size <= 1) {  // reference: memcpy unless in place (mpi_mod.hpp:1181-1188)
     if (!in_place) memcpy(recvbuf, sendbuf, count * es);

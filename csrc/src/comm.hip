@@ -716,6 +716,12 @@ int flexar_pointer_is_device(const void* p) {
   return a.type == hipMemoryTypeDevice ? 1 : 0;
 }
 
+int flexar_copy_device_host(void* dst, const void* src, size_t bytes) {
+  FX_HIP(hipDeviceSynchronize());  // the device buffer may still be written by queued work
+  FX_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
+  return 0;
+}
+
 int flexar_current_device(void) {
   int d = 0;
   if (hipGetDevice(&d) != hipSuccess) return 0;

@@ -1,0 +1,51 @@
+"""MPI_Allreduce_FT on DEVICE buffers (real MI355X): the MPI layer routes hipMalloc'd buffers
+to the flexar GPU engine (handles exchanged with MPI_Allgather, IPC between the ranks' processes),
+or — when ranks do not share a node (forced with FLEXAR_MPI_P2P=1) — stages through host memory
+and the point-to-point engine. Driven through the reference-compatible benchmark CLI with --check.
+Also the RCCL comparator of the benchmark (ncclAllReduce) at one rank."""
+import os
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def tools(cuda):
+    from allreduce_over_mpi_amd import _build
+
+    if not _build.mpi_available():
+        pytest.skip("MPI not available")
+    return _build.build_tools(["flexar_bench"])
+
+
+def _mpirun(n, args, env=None):
+    from allreduce_over_mpi_amd import _build
+
+    e = dict(os.environ)
+    e.update({"FLEXAR_MAX_GRID": "16", "FLEXAR_TIMEOUT_MS": "20000"})
+    e.update(env or {})
+    return subprocess.run([os.path.join(_build.MPI_HOME, "bin", "mpirun"), "-np", str(n)] + args,
+                          stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300, env=e)
+
+
+@pytest.mark.parametrize("algo", ["flat", "ring", "ll", "oneshot"])
+def test_mpi_device_buffers_ipc(tools, algo):
+    r = _mpirun(2, [tools["flexar_bench"], "--mem", "device", "--size", "100003", "--repeat", "5", "--check",
+                    "--algo", algo])
+    assert r.returncode == 0 and "check n=100003: ok" in r.stdout, r.stdout[-3000:]
+
+
+def test_mpi_device_buffers_host_staging(tools):
+    r = _mpirun(2, [tools["flexar_bench"], "--mem", "device", "--size", "65537", "--repeat", "3", "--check"],
+                env={"FLEXAR_MPI_P2P": "1"})
+    assert r.returncode == 0 and "check n=65537: ok" in r.stdout, r.stdout[-3000:]
+
+
+def test_bench_bf16_and_rccl_comparator(tools):
+    r = _mpirun(2, [tools["flexar_bench"], "--mem", "device", "--dtype", "bfloat16", "--size", "4099", "--check"])
+    assert r.returncode == 0 and "check n=4099: ok" in r.stdout, r.stdout[-3000:]
+    r = _mpirun(1, [tools["flexar_bench"], "--mem", "device", "--comm-type", "rccl", "--size", "1M", "--repeat", "5",
+                    "--check"])
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-3000:]
