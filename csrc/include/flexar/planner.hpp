@@ -109,8 +109,9 @@ class Planner {
       for (int k = 0; k < o.ndst; ++k) if (o.dst[k].rank != rank) return true;
       return false;
     };
+    // any rank: a run may not read what another op of the run writes, locally or in a peer's staging
     auto ovl = [&](const Loc& a, uint64_t la, const Loc& b, uint64_t lb) {
-      return a.rank == rank && b.rank == rank && a.buf == b.buf && a.off < b.off + lb && b.off < a.off + la;
+      return a.rank == b.rank && a.buf == b.buf && a.off < b.off + lb && b.off < a.off + la;
     };
     auto indep = [&](const Op& a, const Op& b) {
       for (int i = 0; i < a.ndst; ++i) {
@@ -206,8 +207,17 @@ class Planner {
       srcs = last;
     }
     if (dsts.size() > kMaxDst) {
-      // keep a local destination first so the overflow copies read local memory
+      if (srcs.size() == 1 && sc == 1.0f) {  // pure copy: every chunk of destinations reads the source
+        for (size_t i = 0; i < dsts.size(); i += kMaxDst) {
+          std::vector<Loc> part(dsts.begin() + i, dsts.begin() + std::min(dsts.size(), i + kMaxDst));
+          emit_xfer(len, srcs, part, 1.0f);
+        }
+        return;
+      }
+      // reduction: materialise once in a LOCAL location, then fan out from it (never read back
+      // through a peer's staging)
       std::stable_partition(dsts.begin(), dsts.end(), [&](const Loc& l) { return l.rank == r; });
+      if (dsts[0].rank != r) dsts.insert(dsts.begin(), loc(BUF_STG, r, alloc(len)));
       std::vector<Loc> head(dsts.begin(), dsts.begin() + kMaxDst);
       emit_xfer(len, srcs, head, sc);
       Loc from = head[0];

@@ -173,8 +173,9 @@ static int ll_grid(flexar_comm* c, uint64_t count, uint32_t es) {
 // Decide the bit-level barrier-after flags: an XFER needs a workgroup barrier before the next
 // XFER of the same SIGNAL/WAIT-free run only if they touch overlapping LOCAL memory.
 static void mark_barriers(Program& P, uint32_t rank) {
+  (void)rank;
   auto overlap = [&](const Loc& a, uint64_t la, const Loc& b, uint64_t lb) {
-    if (a.rank != rank || b.rank != rank || a.buf != b.buf) return false;
+    if (a.rank != b.rank || a.buf != b.buf) return false;
     return a.off < b.off + lb && b.off < a.off + la;
   };
   for (uint32_t ch = 0; ch < P.nchan; ++ch) {

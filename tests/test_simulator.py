@@ -41,7 +41,8 @@ def test_all_topologies_f32(nv, n):
 
 
 @pytest.mark.parametrize("n,spec", [(21, "flat"), (21, "tree:3,7"), (21, "ring"), (16, "tree:2,2,2,2"),
-                                    (16, "tree:4,4+push"), (12, "tree:2,3,2"), (9, "tree:3,3")])
+                                    (16, "tree:4,4+push"), (12, "tree:2,3,2"), (9, "tree:3,3"),
+                                    (12, "oneshot"), (16, "oneshot"), (16, "flat+push"), (11, "flat+push")])
 def test_wide_and_prime(nv, n, spec):
     rng = np.random.default_rng(7)
     ins = [rng.integers(-1000, 1000, 4099).astype(np.int64) for _ in range(n)]
