@@ -138,7 +138,7 @@ def main():
     if world > 1 and algo == "auto" and not args.no_tune:
         from allreduce_over_mpi_amd import _native as nv
 
-        cands = ["flat+pull", "flat+push"]
+        cands = ["flat+pull", "flat+push", "flat+pull+nts", "flat+push+nts"]
         maxc = len([d for d in range(1, world) if math.gcd(d, world) == 1])
         cands += ["ring"] + [f"ring:{c}" for c in (2, 4, 8) if c <= maxc]
         if world > 2 and (world & (world - 1)) == 0:

@@ -32,6 +32,7 @@ struct AlgoSpec {
   int channels = 1;         // RING: number of arc-disjoint rings
   AgMode ag = AgMode::AUTO; // TREE: all-gather direction
   bool fuse = true;         // fuse reduce->forward (tree RS / AG multicast)
+  bool nts = false;         // executor stores with the streaming (nontemporal) policy
 
   std::string str() const {
     std::ostringstream ss;
@@ -48,6 +49,7 @@ struct AlgoSpec {
     if (kind == AlgoKind::TREE && ag == AgMode::PULL) ss << "+pull";
     if (kind == AlgoKind::TREE && ag == AgMode::PUSH) ss << "+push";
     if (!fuse) ss << "+nofuse";
+    if (nts) ss << "+nts";
     return ss.str();
   }
 };
@@ -169,6 +171,7 @@ inline bool parse_algo(const std::string& raw, int nranks, AlgoSpec* spec, std::
     else if (mod == "push") spec->ag = AgMode::PUSH;
     else if (mod == "nofuse") spec->fuse = false;
     else if (mod == "fuse") spec->fuse = true;
+    else if (mod == "nts") spec->nts = true;
     else { if (err) *err = "unknown algorithm modifier '+" + mod + "'"; return false; }
   }
   std::string head = s, arg;
@@ -212,9 +215,9 @@ inline bool parse_algo(const std::string& raw, int nranks, AlgoSpec* spec, std::
   }
   if (head == "ft") {
     const char* env = getenv("FT_TOPO");
-    AgMode ag = spec->ag; bool fuse = spec->fuse;
-    if (!parse_ft_topo(env ? env : arg.c_str(), nranks, spec, err)) return false;
-    spec->ag = ag; spec->fuse = fuse;
+    AgMode ag = spec->ag; bool fuse = spec->fuse, nts = spec->nts;
+    if (!parse_ft_topo(!arg.empty() ? arg.c_str() : env, nranks, spec, err)) return false;
+    spec->ag = ag; spec->fuse = fuse; spec->nts = nts;
     return true;
   }
   if (err) *err = "unknown algorithm '" + raw + "'";

@@ -559,6 +559,7 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     la.ctx = x;
     la.grid = grid;
     la.stream = st;
+    la.nts = s.nts;
     rc = launch_dtype(dtype, op, la);
     if (rc) break;
   }
@@ -699,6 +700,7 @@ int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
     la.nranks = nranks;
     la.grid = grid;
     la.stream = st;
+    la.nts = specs[0].nts;
     int rc = launch_dtype(dtype, op, la);
     if (rc) return rc;
     FX_HIP(hipStreamSynchronize(st));  // d_ctx is reused by the next piece

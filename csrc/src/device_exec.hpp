@@ -66,12 +66,14 @@ __device__ FX_INLINE uint4 ld16(const char* p) {
 #endif
   return uint4{v.x, v.y, v.z, v.w};
 }
+template <bool NTS = false>
 __device__ FX_INLINE void st16(char* p, uint4 x) {
   u32x4 v = {x.x, x.y, x.z, x.w};
 #if defined(FLEXAR_NT_STORES)
   __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
 #else
-  *reinterpret_cast<u32x4*>(p) = v;
+  if constexpr (NTS) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));  // "+nts": streaming stores
+  else *reinterpret_cast<u32x4*>(p) = v;
 #endif
 }
 
@@ -103,7 +105,7 @@ __device__ FX_INLINE uint4 combine16(const uint4 (&x)[K], float scale, bool sc) 
 }
 
 // dst[0..nd) = OP(src[0..K)) over n elements; this workgroup's threads only.
-template <typename T, typename OP, int K>
+template <typename T, typename OP, int K, bool NTS = false>
 __device__ FX_INLINE void xfer_k(const char* const (&s)[kMaxSrc], char* const (&d)[kMaxDst], int nd, uint64_t n,
                                  float scale, bool vec) {
   using A = typename Elem<T>::acc;
@@ -124,7 +126,7 @@ __device__ FX_INLINE void xfer_k(const char* const (&s)[kMaxSrc], char* const (&
       uint4 y = combine16<T, OP, K>(x[u], scale, sc);
 #pragma unroll
       for (int dd = 0; dd < kMaxDst; ++dd)
-        if (dd < nd) st16(d[dd] + (v + u * nt) * 16, y);
+        if (dd < nd) st16<NTS>(d[dd] + (v + u * nt) * 16, y);
     }
   }
   for (; v < nv; v += nt) {
@@ -134,7 +136,7 @@ __device__ FX_INLINE void xfer_k(const char* const (&s)[kMaxSrc], char* const (&
     uint4 y = combine16<T, OP, K>(x, scale, sc);
 #pragma unroll
     for (int dd = 0; dd < kMaxDst; ++dd)
-      if (dd < nd) st16(d[dd] + v * 16, y);
+      if (dd < nd) st16<NTS>(d[dd] + v * 16, y);
   }
   // scalar tail (or whole span when a base address is not 16-B aligned)
   for (uint64_t i = nv * E + threadIdx.x; i < n; i += nt) {
@@ -156,18 +158,18 @@ __device__ FX_INLINE void xfer_k(const char* const (&s)[kMaxSrc], char* const (&
   }
 }
 
-template <typename T, typename OP>
+template <typename T, typename OP, bool NTS = false>
 __device__ FX_INLINE void xfer_dispatch(int K, const char* const (&s)[kMaxSrc], char* const (&d)[kMaxDst], int nd,
                                         uint64_t n, float scale, bool vec) {
   switch (K) {
-    case 1: xfer_k<T, OP, 1>(s, d, nd, n, scale, vec); break;
-    case 2: xfer_k<T, OP, 2>(s, d, nd, n, scale, vec); break;
-    case 3: xfer_k<T, OP, 3>(s, d, nd, n, scale, vec); break;
-    case 4: xfer_k<T, OP, 4>(s, d, nd, n, scale, vec); break;
-    case 5: xfer_k<T, OP, 5>(s, d, nd, n, scale, vec); break;
-    case 6: xfer_k<T, OP, 6>(s, d, nd, n, scale, vec); break;
-    case 7: xfer_k<T, OP, 7>(s, d, nd, n, scale, vec); break;
-    default: xfer_k<T, OP, 8>(s, d, nd, n, scale, vec); break;
+    case 1: xfer_k<T, OP, 1, NTS>(s, d, nd, n, scale, vec); break;
+    case 2: xfer_k<T, OP, 2, NTS>(s, d, nd, n, scale, vec); break;
+    case 3: xfer_k<T, OP, 3, NTS>(s, d, nd, n, scale, vec); break;
+    case 4: xfer_k<T, OP, 4, NTS>(s, d, nd, n, scale, vec); break;
+    case 5: xfer_k<T, OP, 5, NTS>(s, d, nd, n, scale, vec); break;
+    case 6: xfer_k<T, OP, 6, NTS>(s, d, nd, n, scale, vec); break;
+    case 7: xfer_k<T, OP, 7, NTS>(s, d, nd, n, scale, vec); break;
+    default: xfer_k<T, OP, 8, NTS>(s, d, nd, n, scale, vec); break;
   }
 }
 
@@ -178,7 +180,7 @@ __device__ FX_INLINE void st_flag(uint64_t* f, uint64_t v) {
   __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-template <typename T, typename OP>
+template <typename T, typename OP, bool NTS>
 __device__ FX_INLINE void xfer_op(const DevCtx& c, const Op* o, uint32_t lb, uint32_t nb, uint32_t quantum,
                                   uint64_t par) {
   uint64_t lo, hi;
@@ -208,10 +210,10 @@ __device__ FX_INLINE void xfer_op(const DevCtx& c, const Op* o, uint32_t lb, uin
       vec &= (l.buf == BUF_STG) || c.vec_ok;
     }
   }
-  xfer_dispatch<T, OP>(ns, s, d, nd, hi - lo, o->scale, vec);
+  xfer_dispatch<T, OP, NTS>(ns, s, d, nd, hi - lo, o->scale, vec);
 }
 
-template <typename T, typename OP>
+template <typename T, typename OP, bool NTS>
 __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uint32_t grid) {
   __shared__ int s_abort;
   const uint32_t tid = threadIdx.x;
@@ -235,7 +237,7 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
       bool bar = false;
       for (uint32_t k = 0; k < n; ++k) {
         const Op* q = c.ops + i + (n > 1 ? (k + lb) % n : 0);
-        xfer_op<T, OP>(c, q, lb, nb, quantum, par);
+        xfer_op<T, OP, NTS>(c, q, lb, nb, quantum, par);
         bar |= (q->flags & kXferBarrierAfter) != 0;
       }
       if (bar) __syncthreads();
@@ -389,18 +391,18 @@ __global__ void __launch_bounds__(kExecThreads) ll_group_kernel(const DevCtx* ct
 }
 
 // Production launch: one rank per process, context by value.
-template <typename T, typename OP>
+template <typename T, typename OP, bool NTS>
 __global__ void __launch_bounds__(kExecThreads) exec_kernel(DevCtx c) {
-  exec_body<T, OP>(c, blockIdx.x, gridDim.x);
+  exec_body<T, OP, NTS>(c, blockIdx.x, gridDim.x);
 }
 
 // In-process group launch: nranks ranks share one grid (rank = blockIdx / grid_per_rank) —
 // every rank's workgroups are co-resident by construction, so the full multi-rank protocol
 // runs on a single GPU in a single process (tests, calibration).
-template <typename T, typename OP>
+template <typename T, typename OP, bool NTS>
 __global__ void __launch_bounds__(kExecThreads) exec_group_kernel(const DevCtx* ctxs, uint32_t grid_per_rank) {
   const uint32_t r = blockIdx.x / grid_per_rank;
-  exec_body<T, OP>(ctxs[r], blockIdx.x % grid_per_rank, grid_per_rank);
+  exec_body<T, OP, NTS>(ctxs[r], blockIdx.x % grid_per_rank, grid_per_rank);
 }
 
 // Standalone reduction: dst[0] = scale * OP(src[0..K)), grid-sliced.

@@ -12,11 +12,18 @@ template <typename T, typename OP>
 inline int launch_one(const LaunchArgs& a) {
   switch (a.kind) {
     case LAUNCH_EXEC:
-      hipLaunchKernelGGL((exec_kernel<T, OP>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
+      if (a.nts)
+        hipLaunchKernelGGL((exec_kernel<T, OP, true>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
+      else
+        hipLaunchKernelGGL((exec_kernel<T, OP, false>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
       break;
     case LAUNCH_GROUP:
-      hipLaunchKernelGGL((exec_group_kernel<T, OP>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0, a.stream,
-                         a.d_ctxs, (uint32_t)a.grid);
+      if (a.nts)
+        hipLaunchKernelGGL((exec_group_kernel<T, OP, true>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
+                           a.stream, a.d_ctxs, (uint32_t)a.grid);
+      else
+        hipLaunchKernelGGL((exec_group_kernel<T, OP, false>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
+                           a.stream, a.d_ctxs, (uint32_t)a.grid);
       break;
     case LAUNCH_REDUCE:
       hipLaunchKernelGGL((reduce_kernel<T, OP>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.srcs, a.nsrc,

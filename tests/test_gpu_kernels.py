@@ -69,7 +69,7 @@ def test_reduce_kernel_int(cuda, op):
 def _specs(n):
     from allreduce_over_mpi_amd import _native as nv
 
-    base = ["flat", "flat+push", "ring", "oneshot", "ll"]
+    base = ["flat", "flat+push", "ring", "oneshot", "ll", "flat+nts", "ring:2+nts"]
     base += [p for p in nv.enumerate_plans(n) if p.startswith("tree:") or p.startswith("ring:")]
     base += [p + "+push" for p in nv.enumerate_plans(n) if p.startswith("tree:") and "," in p]
     return sorted(set(base))
