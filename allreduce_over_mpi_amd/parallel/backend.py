@@ -147,9 +147,21 @@ class FlexarProcessGroup(dist.ProcessGroup):
         return s
 
     def allreduce_coalesced(self, tensor_list, opts=AllreduceCoalescedOptions()):
+        """Many tensors -> one flat bucket -> ONE executor launch (instead of one per tensor)."""
         o = AllreduceOptions()
         o.reduceOp = opts.reduceOp
-        return self.allreduce(tensor_list, o)
+        same = len({(t.dtype, t.device) for t in tensor_list}) == 1
+        if len(tensor_list) < 2 or not same or not self._flexar_ok(tensor_list, _redop_name(opts.reduceOp)):
+            return self.allreduce(tensor_list, o)
+        flat = torch.cat([t.reshape(-1) for t in tensor_list])
+        work = self.allreduce([flat], o)
+        work.wait()
+        off = 0
+        for t in tensor_list:
+            n = t.numel()
+            t.copy_(flat[off:off + n].view_as(t))
+            off += n
+        return _done_work(tensor_list)
 
     # ------------------------------------------------------------------ delegated collectives
     def barrier(self, opts=BarrierOptions()):

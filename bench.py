@@ -51,6 +51,7 @@ def main():
                     help="avg = sum with the 1/N post-scale fused into the reduction (fp8 gradients)")
     ap.add_argument("--sweep", default="", help="MIN:MAX bytes (e.g. 4K:4G): busbw table vs RCCL, x4 steps")
     ap.add_argument("--sweep-out", default="", help="write sweep rows as JSON lines here (rank 0)")
+    ap.add_argument("--tune-out", default="", help="append the tuner's choice as a FLEXAR_TUNE_FILE line")
     ap.add_argument("--algo", default="auto", help="flexar algorithm spec or 'auto' (tuned at start-up)")
     ap.add_argument("--no-rccl", action="store_true", help="skip the RCCL comparison run")
     ap.add_argument("--no-tune", action="store_true", help="use the cost model instead of the start-up tuner")
@@ -183,6 +184,9 @@ def main():
         comm.set_grid(best_grid)
         algo = best
         log(rank, f"tuner: selected {algo} grid={best_grid or 'auto'}")
+        if rank == 0 and args.tune_out:
+            with open(args.tune_out, "a") as f:  # "nranks bytes spec" (cost_model.hpp TuneTable)
+                f.write(f"{world} {nbytes} {algo}\n")
 
     ok, err = check(algo)
     if max_over_ranks(0.0 if ok else 1.0) != 0.0:
