@@ -66,6 +66,10 @@ def _sig(lib):
         "flexar_legacy_cost": (d, [cp, i, d]),
         "flexar_plan_dump": (i, [cp, i, i, sz, i, cp, sz]),
         "flexar_simulate": (i, [cp, i, sz, i, i, c.POINTER(vp), c.POINTER(vp), i, i, i, f]),
+        "flexar_simulate_coll": (i, [i, cp, i, sz, i, i, c.POINTER(vp), c.POINTER(vp), i, i, f]),
+        "flexar_reduce_scatter": (i, [vp, vp, vp, sz, i, i, vp, cp]),
+        "flexar_all_gather": (i, [vp, vp, vp, sz, i, vp, cp]),
+        "flexar_group_collective": (i, [c.POINTER(vp), i, i, c.POINTER(vp), c.POINTER(vp), sz, i, i, vp, cp]),
     }
     for name, (res, args) in table.items():
         fn = getattr(lib, name)
@@ -228,3 +232,22 @@ def reduce_host(srcs, op="sum", scale=1.0, dtype: str | None = None):
     check(lib().flexar_reduce_host(out.ctypes.data, _ptr_array([s.ctypes.data for s in srcs]), len(srcs),
                                    srcs[0].size, code, op_code(op), float(scale)), "reduce_host")
     return out
+
+
+COLLS = {"allreduce": 0, "reduce_scatter": 1, "all_gather": 2}
+
+
+def simulate_coll(coll: str, spec: str, inputs, count: int, dtype: str = "float32", op="sum", grid=2, ncalls=2,
+                  scale=1.0):
+    """Simulate reduce_scatter (inputs N*count, outputs count) or all_gather (inputs count, outputs N*count)."""
+    import numpy as np
+
+    n = len(inputs)
+    ins = [np.ascontiguousarray(x) for x in inputs]
+    out_n = count if coll == "reduce_scatter" else (n * count if coll == "all_gather" else count)
+    outs = [np.zeros(out_n, dtype=ins[0].dtype) for _ in range(n)]
+    rc = lib().flexar_simulate_coll(COLLS[coll], spec.encode(), n, count, DTYPES[dtype], op_code(op),
+                                    _ptr_array([x.ctypes.data for x in ins]), _ptr_array([o.ctypes.data for o in outs]),
+                                    grid, ncalls, float(scale))
+    check(rc, "simulate_coll")
+    return outs

@@ -174,6 +174,10 @@ class FlexarProcessGroup(dist.ProcessGroup):
         return self._fallback(input_tensor).allgather(output_tensors, input_tensor, opts)
 
     def _allgather_base(self, output_tensor, input_tensor, opts=AllgatherOptions()):
+        if self._flexar_ok([input_tensor, output_tensor], "sum") and input_tensor.dtype != torch.bool and \
+                output_tensor.numel() == input_tensor.numel() * self._world:
+            return self._on_side([input_tensor, output_tensor], lambda c: c.all_gather(input_tensor, output_tensor),
+                                 [output_tensor])
         return self._fallback([input_tensor])._allgather_base(output_tensor, input_tensor, opts)
 
     def allgather_into_tensor_coalesced(self, output_tensors, input_tensors, opts=AllgatherOptions()):
@@ -183,7 +187,30 @@ class FlexarProcessGroup(dist.ProcessGroup):
         return self._fallback(output_tensors).reduce_scatter(output_tensors, input_tensors, opts)
 
     def _reduce_scatter_base(self, output_tensor, input_tensor, opts=ReduceScatterOptions()):
+        opname = _redop_name(opts.reduceOp)
+        if self._flexar_ok([input_tensor, output_tensor], opname) and input_tensor.dtype != torch.bool and \
+                input_tensor.numel() == output_tensor.numel() * self._world:
+            return self._on_side([input_tensor, output_tensor],
+                                 lambda c: c.reduce_scatter(input_tensor, output_tensor, op=opname), [output_tensor])
         return self._fallback([input_tensor])._reduce_scatter_base(output_tensor, input_tensor, opts)
+
+    def _on_side(self, tensors, fn, result):
+        """Run fn(comm) on the side stream (ordered after the caller's stream); CUDA-aware completion."""
+        dev = tensors[0].device
+        comm = self.comm(dev.index)
+        cur = torch.cuda.current_stream(dev)
+        side = self._side_stream(dev) if self.async_stream else cur
+        if side is not cur:
+            side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            for t in tensors:
+                if side is not cur:
+                    t.record_stream(side)
+            fn(comm)
+            self.stats["flexar_allreduce"] += 1
+            fut = torch.futures.Future(devices=[dev])
+            fut.set_result(result)
+        return _create_work_from_future(fut)
 
     def reduce_scatter_tensor_coalesced(self, output_tensors, input_tensors, opts=ReduceScatterOptions()):
         return self._fallback(input_tensors).reduce_scatter_tensor_coalesced(output_tensors, input_tensors, opts)

@@ -115,6 +115,28 @@ class Communicator:
         nv.check(rc, "allreduce")
         return dst
 
+    def reduce_scatter(self, input, output, op="sum", algo: Optional[str] = None, stream=None):
+        """``output`` (m elements) = this rank's reduced block of ``input`` (world_size * m elements)."""
+        _require_cuda(input)
+        _require_cuda(output, "output")
+        if input.numel() != output.numel() * self.world_size or input.dtype != output.dtype:
+            raise nv.FlexarError(1, "input must hold world_size * output.numel() elements of output's dtype")
+        nv.check(self._lib.flexar_reduce_scatter(self._h, input.data_ptr(), output.data_ptr(), output.numel(),
+                                                 nv.dtype_code(output.dtype), nv.op_code(op), _stream_handle(stream),
+                                                 algo.encode() if algo else None), "reduce_scatter")
+        return output
+
+    def all_gather(self, input, output, algo: Optional[str] = None, stream=None):
+        """``output`` (world_size * m elements) = concatenation of every rank's ``input`` (m elements)."""
+        _require_cuda(input)
+        _require_cuda(output, "output")
+        if output.numel() != input.numel() * self.world_size or input.dtype != output.dtype:
+            raise nv.FlexarError(1, "output must hold world_size * input.numel() elements of input's dtype")
+        nv.check(self._lib.flexar_all_gather(self._h, input.data_ptr(), output.data_ptr(), input.numel(),
+                                             nv.dtype_code(input.dtype), _stream_handle(stream),
+                                             algo.encode() if algo else None), "all_gather")
+        return output
+
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
             self._lib.flexar_comm_destroy(self._h)
@@ -177,6 +199,17 @@ class LocalGroup:
                                               nv.dtype_code(tensors[0].dtype), nv.op_code(op), _stream_handle(stream),
                                               algo.encode() if algo else None, float(scale))
         nv.check(rc, "group_allreduce")
+        return outs
+
+    def collective(self, coll: str, ins: Sequence, outs: Sequence, op="sum", algo: Optional[str] = None, stream=None):
+        """``coll`` = "reduce_scatter" or "all_gather" for every rank of the group in one launch."""
+        code = nv.COLLS[coll]
+        count = outs[0].numel() if coll == "reduce_scatter" else ins[0].numel()
+        a = (ctypes.c_void_p * self.nranks)(*[t.data_ptr() for t in ins])
+        b = (ctypes.c_void_p * self.nranks)(*[t.data_ptr() for t in outs])
+        nv.check(self._lib.flexar_group_collective(self._comms, self.nranks, code, a, b, count,
+                                                   nv.dtype_code(ins[0].dtype), nv.op_code(op), _stream_handle(stream),
+                                                   algo.encode() if algo else None), coll)
         return outs
 
     def check(self):

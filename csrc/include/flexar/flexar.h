@@ -110,6 +110,14 @@ int flexar_allreduce(flexar_comm_t comm, const void* sendbuf, void* recvbuf, siz
  * post-scale applied to the reduced value (1.0f = none; AVG multiplies 1/N on top). */
 int flexar_allreduce_ex(flexar_comm_t comm, const void* sendbuf, void* recvbuf, size_t count, int dtype,
                         int op, void* hip_stream, const char* algo, float scale);
+/* Reduce-scatter: sendbuf holds nranks blocks of `count` elements, recvbuf receives this rank's
+ * reduced block (count elements). All-gather: sendbuf has `count` elements, recvbuf nranks*count.
+ * algo: "ring" or the direct exchange ("flat", default). Used by FSDP/ZeRO-style sharded DP and by
+ * the hierarchical multi-node allreduce of the MPI layer. */
+int flexar_reduce_scatter(flexar_comm_t comm, const void* sendbuf, void* recvbuf, size_t count, int dtype, int op,
+                          void* hip_stream, const char* algo);
+int flexar_all_gather(flexar_comm_t comm, const void* sendbuf, void* recvbuf, size_t count, int dtype,
+                      void* hip_stream, const char* algo);
 /* Non-blocking health check: returns FLEXAR_ERR_TIMEOUT (and fills flexar_last_error)
  * if a device-side wait timed out in any previous call. */
 int flexar_comm_check(flexar_comm_t comm);
@@ -125,6 +133,9 @@ int flexar_comm_describe(flexar_comm_t comm, size_t count, int dtype, char* buf,
 int flexar_group_create(int nranks, int device, size_t workspace_bytes, flexar_comm_t* comms_out);
 int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* ins, void* const* outs, size_t count,
                            int dtype, int op, void* hip_stream, const char* algo, float scale);
+/* coll: 1 = reduce-scatter, 2 = all-gather (count = elements per rank block). */
+int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const void* const* ins, void* const* outs,
+                            size_t count, int dtype, int op, void* hip_stream, const char* algo);
 
 /* ---- standalone device reduction kernel ----------------------------------- */
 /* dst[i] = scale * OP_k srcs[k][i], k < nsrc (1..64), fp32 accumulation for 16/8-bit floats. */
@@ -159,6 +170,10 @@ int flexar_plan_dump(const char* spec, int rank, int nranks, size_t count, int d
 /* Execute the exact op programs the GPU runs, on host memory with one thread per (rank, grid block).
  * inputs/outputs: nranks host pointers each. in_place: outputs[r] already holds the input.
  * Returns 0 on success. Used to validate every algorithm/topology without a GPU. */
+/* Same for coll = 0 allreduce, 1 reduce-scatter (inputs nranks*count, outputs count), 2 all-gather
+ * (inputs count, outputs nranks*count). */
+int flexar_simulate_coll(int coll, const char* spec, int nranks, size_t count, int dtype, int op,
+                         const void* const* inputs, void* const* outputs, int grid, int ncalls, float scale);
 int flexar_simulate(const char* spec, int nranks, size_t count, int dtype, int op, const void* const* inputs,
                     void* const* outputs, int grid, int ncalls, int in_place, float scale);
 

@@ -44,6 +44,8 @@ struct Program {
   std::string desc;
 };
 
+enum class Coll { ALLREDUCE = 0, REDUCE_SCATTER = 1, ALL_GATHER = 2 };
+
 class Planner {
  public:
   Planner(uint32_t nranks, uint32_t rank, uint64_t count, uint32_t esize, float final_scale)
@@ -93,6 +95,35 @@ class Planner {
     } else {
       if (err) *err = "planner needs a concrete algorithm (not auto)";
       return false;
+    }
+    P->stg_elems = stg;
+    P->nchan = (uint32_t)P->chan_start.size() - 1;
+    mark_runs(*P, r);
+    return true;
+  }
+
+  // Reduce-scatter / all-gather programs. `count` = elements per rank-block (m); `stride` = elements
+  // between consecutive rank-blocks of the N*m side (IN for reduce-scatter, OUT for all-gather), so a
+  // call can be split into pieces along m. Ring for "ring*", otherwise the direct (flat) exchange.
+  bool build_coll(Coll coll, const AlgoSpec& spec, uint64_t stride, Program* P, std::string* err) {
+    if (coll == Coll::ALLREDUCE) return build(spec, P, err);
+    prog = P;
+    *P = Program();
+    P->count = count;
+    P->esize = esize;
+    P->chan_start.push_back(0);
+    stg = 0;
+    const bool ring = spec.kind == AlgoKind::RING && N > 2;
+    if (N == 1) {
+      if (count) xfer(count, {loc(BUF_IN, r, 0)}, {loc(BUF_OUT, r, 0)}, coll == Coll::REDUCE_SCATTER ? scale : 1.0f);
+      finish_channel();
+      P->desc = "copy";
+    } else if (coll == Coll::REDUCE_SCATTER) {
+      ring ? build_ring_rs(stride) : build_flat_rs(stride);
+      P->desc = ring ? "ring-rs" : "flat-rs";
+    } else {
+      ring ? build_ring_ag(stride) : build_flat_ag(stride);
+      P->desc = ring ? "ring-ag" : "flat-ag";
     }
     P->stg_elems = stg;
     P->nchan = (uint32_t)P->chan_start.size() - 1;
@@ -469,6 +500,85 @@ class Planner {
         }
       }
     }
+  }
+
+  // ------------------------------------------------------------------ reduce-scatter / all-gather
+  std::vector<uint32_t> rotated_peers() const {
+    std::vector<uint32_t> v;
+    for (uint32_t jj = 1; jj < N; ++jj) v.push_back((r + jj) % N);
+    return v;
+  }
+  void build_flat_rs(uint64_t stride) {
+    const uint64_t m = count, m_al = round_up(m);
+    uint64_t base = alloc((uint64_t)N * m_al);
+    auto peers = rotated_peers();
+    for (uint32_t p : peers) xfer(m, {loc(BUF_IN, r, (uint64_t)p * stride)}, {loc(BUF_STG, p, base + r * m_al)}, 1.0f);
+    signal(peers, 0);
+    wait(peers, 0);
+    std::vector<Loc> srcs;  // rank order: identical summation order for every block owner
+    for (uint32_t p = 0; p < N; ++p)
+      srcs.push_back(p == r ? loc(BUF_IN, r, (uint64_t)r * stride) : loc(BUF_STG, r, base + p * m_al));
+    xfer(m, srcs, {loc(BUF_OUT, r, 0)}, scale);
+    finish_channel();
+  }
+  void build_flat_ag(uint64_t stride) {
+    const uint64_t m = count, m_al = round_up(m);
+    uint64_t base = alloc((uint64_t)N * m_al);
+    auto peers = rotated_peers();
+    std::vector<Loc> dsts{loc(BUF_OUT, r, (uint64_t)r * stride)};
+    for (uint32_t p : peers) dsts.push_back(loc(BUF_STG, p, base + r * m_al));
+    xfer(m, {loc(BUF_IN, r, 0)}, dsts, 1.0f);
+    signal(peers, 0);
+    wait(peers, 0);
+    for (uint32_t p : peers) xfer(m, {loc(BUF_STG, r, base + p * m_al)}, {loc(BUF_OUT, r, (uint64_t)p * stride)}, 1.0f);
+    finish_channel();
+  }
+  // Ring reduce-scatter: the rank at ring position v ends up owning ITS block (data of rank ord[v]).
+  void build_ring_rs(uint64_t stride) {
+    const uint64_t m = count, m_al = round_up(m);
+    std::vector<int> ord = ring_order(N, 0);
+    uint32_t v = 0;
+    for (uint32_t q = 0; q < N; ++q)
+      if ((uint32_t)ord[q] == r) v = q;
+    const uint32_t right = ord[(v + 1) % N], left = ord[(v + N - 1) % N];
+    auto mod = [&](long x) { return (uint32_t)(((x % (long)N) + N) % N); };
+    auto boff = [&](uint32_t j) { return (uint64_t)ord[mod((long)j - 1)] * stride; };  // block j <-> rank ord[j-1]
+    uint64_t base = alloc((uint64_t)(N - 1) * m_al);
+    xfer(m, {loc(BUF_IN, r, boff(v))}, {loc(BUF_STG, right, base)}, 1.0f);
+    signal({right}, 0);
+    for (uint32_t i = 0; i + 1 < N; ++i) {
+      wait({left}, i);
+      uint32_t b = mod((long)v - 1 - (long)i);
+      std::vector<Loc> srcs{loc(BUF_IN, r, boff(b)), loc(BUF_STG, r, base + i * m_al)};
+      if (i + 2 < N) {
+        xfer(m, srcs, {loc(BUF_STG, right, base + (i + 1) * m_al)}, 1.0f);
+        signal({right}, i + 1);
+      } else {
+        xfer(m, srcs, {loc(BUF_OUT, r, 0)}, scale);  // b == v + 1  <->  rank ord[v] == r
+      }
+    }
+    finish_channel();
+  }
+  void build_ring_ag(uint64_t stride) {
+    const uint64_t m = count, m_al = round_up(m);
+    std::vector<int> ord = ring_order(N, 0);
+    uint32_t v = 0;
+    for (uint32_t q = 0; q < N; ++q)
+      if ((uint32_t)ord[q] == r) v = q;
+    const uint32_t right = ord[(v + 1) % N], left = ord[(v + N - 1) % N];
+    auto mod = [&](long x) { return (uint32_t)(((x % (long)N) + N) % N); };
+    uint64_t base = alloc((uint64_t)(N - 1) * m_al);
+    xfer(m, {loc(BUF_IN, r, 0)}, {loc(BUF_OUT, r, (uint64_t)r * stride), loc(BUF_STG, right, base)}, 1.0f);
+    signal({right}, 0);
+    for (uint32_t i = 0; i + 1 < N; ++i) {
+      wait({left}, i);
+      uint32_t owner = (uint32_t)ord[mod((long)v - 1 - (long)i)];  // the block that reached us at step i
+      std::vector<Loc> dsts{loc(BUF_OUT, r, (uint64_t)owner * stride)};
+      if (i + 2 < N) dsts.push_back(loc(BUF_STG, right, base + (i + 1) * m_al));
+      xfer(m, {loc(BUF_STG, r, base + i * m_al)}, dsts, 1.0f);
+      if (i + 2 < N) signal({right}, i + 1);
+    }
+    finish_channel();
   }
 
   // ------------------------------------------------------------------ oneshot

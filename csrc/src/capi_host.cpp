@@ -208,6 +208,29 @@ int flexar_simulate(const char* spec, int nranks, size_t count, int dtype, int o
   return dispatch_dtype_op<SimRun>(dtype, op, progs, nranks, grid, ncalls, in_place, inputs, outputs, count);
 }
 
+int flexar_simulate_coll(int coll, const char* spec, int nranks, size_t count, int dtype, int op,
+                         const void* const* inputs, void* const* outputs, int grid, int ncalls, float scale) {
+  size_t es = dtype_size(dtype);
+  if (!es || nranks < 1 || nranks > 64 || grid < 1 || grid > 64 || ncalls < 1 || !inputs || !outputs || coll < 0 ||
+      coll > 2) {
+    set_error("bad simulate arguments");
+    return FLEXAR_ERR_INVALID;
+  }
+  if (!op_supported(dtype, op)) { set_error("unsupported dtype/op"); return FLEXAR_ERR_UNSUPPORTED; }
+  AlgoSpec s;
+  std::string err;
+  if (!spec_for(spec, nranks, (double)count * es, &s, &err, true)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  float fs = coll == 1 ? scale * (op == FLEXAR_AVG ? 1.0f / (float)nranks : 1.0f) : 1.0f;
+  std::vector<Program> progs(nranks);
+  for (int r = 0; r < nranks; ++r) {
+    Planner pl(nranks, r, count, (uint32_t)es, fs);
+    if (!pl.build_coll((Coll)coll, s, count, &progs[r], &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  }
+  if (grid % progs[0].nchan) { set_error("grid must be a multiple of the channel count"); return FLEXAR_ERR_INVALID; }
+  return dispatch_dtype_op<SimRun>(dtype, coll == 2 ? FLEXAR_SUM : op, progs, nranks, grid, ncalls, 0, inputs,
+                                   outputs, count);
+}
+
 int flexar_reduce_host(void* dst, const void* const* srcs, int nsrc, size_t count, int dtype, int op, float scale) {
   if (!dst || !srcs || nsrc < 1) { set_error("bad reduce arguments"); return FLEXAR_ERR_INVALID; }
   float fs = scale * (op == FLEXAR_AVG ? 1.0f / (float)nsrc : 1.0f);

@@ -199,17 +199,18 @@ static void mark_barriers(Program& P, uint32_t rank) {
 }
 
 static int get_program(flexar_comm* c, const AlgoSpec& s, uint64_t count, uint32_t esize, float fscale,
-                       DevProgram** out) {
-  char key[256];
+                       DevProgram** out, Coll coll = Coll::ALLREDUCE, uint64_t stride = 0) {
+  char key[320];
   uint32_t sb;
   memcpy(&sb, &fscale, 4);
-  snprintf(key, sizeof(key), "%s|%llu|%u|%08x", s.str().c_str(), (unsigned long long)count, esize, sb);
+  snprintf(key, sizeof(key), "%d|%s|%llu|%u|%08x|%llu", (int)coll, s.str().c_str(), (unsigned long long)count, esize,
+           sb, (unsigned long long)stride);
   auto it = c->cache.find(key);
   if (it != c->cache.end()) { *out = it->second.get(); return 0; }
   std::unique_ptr<DevProgram> dp(new DevProgram);
   std::string err;
   Planner pl(c->nranks, c->rank, count, esize, fscale);
-  if (!pl.build(s, &dp->prog, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  if (!pl.build_coll(coll, s, stride, &dp->prog, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
   mark_barriers(dp->prog, c->rank);
   logf(LOG_INFO, c->rank, "plan %s: count=%llu esize=%u ops=%zu channels=%u staging=%llu B", s.str().c_str(),
        (unsigned long long)count, esize, dp->prog.ops.size(), dp->prog.nchan,
@@ -266,24 +267,57 @@ static void fill_ctx(flexar_comm* c, DevProgram* dp, const void* in, void* out, 
 
 // Split a call into pieces whose staging fits one parity half of the workspace.
 static int plan_pieces(flexar_comm* c, const AlgoSpec& s, uint64_t count, uint32_t esize, float fs,
-                       uint64_t* piece) {
+                       uint64_t* piece, Coll coll = Coll::ALLREDUCE, uint64_t stride = 0) {
   DevProgram* dp = nullptr;
-  int rc = get_program(c, s, count, esize, fs, &dp);
+  int rc = get_program(c, s, count, esize, fs, &dp, coll, stride);
   if (rc) return rc;
   uint64_t need = dp->prog.stg_elems * esize;
   if (need <= c->exec_half) { *piece = count; return 0; }
-  uint64_t align = std::max<uint64_t>(1, kStageAlignBytes / esize) * c->nranks;
+  uint64_t align = std::max<uint64_t>(1, kStageAlignBytes / esize) * (coll == Coll::ALLREDUCE ? c->nranks : 1);
   uint64_t pieces = (need + c->exec_half - 1) / c->exec_half;
   for (int tries = 0; tries < 64; ++tries, ++pieces) {
     uint64_t p = (count + pieces - 1) / pieces;
     p = (p + align - 1) / align * align;
     if (p == 0) p = align;
-    rc = get_program(c, s, p, esize, fs, &dp);
+    rc = get_program(c, s, p, esize, fs, &dp, coll, stride);
     if (rc) return rc;
     if (dp->prog.stg_elems * esize <= c->exec_half) { *piece = p; return 0; }
   }
   set_error("workspace too small for this algorithm");
   return FLEXAR_ERR_NOMEM;
+}
+
+// Reduce-scatter / all-gather (count = elements per rank block): split along the block so each
+// piece's program sees blocks `stride` = count elements apart in the N*count-sized buffer.
+static int run_rs_ag(flexar_comm* c, Coll coll, const void* in, void* out, size_t count, int dtype, int op,
+                     hipStream_t st, const char* algo, float scale) {
+  const uint32_t es = (uint32_t)dtype_size(dtype);
+  float fs = coll == Coll::REDUCE_SCATTER ? scale * (op == FLEXAR_AVG ? 1.0f / (float)c->nranks : 1.0f) : 1.0f;
+  AlgoSpec s;
+  int rc = resolve_spec(c, algo, (double)count * es * c->nranks, &s);
+  if (rc) return rc;
+  if (s.kind != AlgoKind::RING) s.kind = AlgoKind::TREE, s.widths = {c->nranks}, s.ag = AgMode::PUSH;
+  std::lock_guard<std::mutex> lk(c->mu);
+  uint64_t piece = count;
+  if (c->nranks > 1 && (rc = plan_pieces(c, s, count, es, fs, &piece, coll, count))) return rc;
+  for (uint64_t off = 0; off < count; off += piece) {
+    uint64_t n = std::min<uint64_t>(piece, count - off);
+    DevProgram* dp = nullptr;
+    if ((rc = get_program(c, s, n, es, fs, &dp, coll, count))) return rc;
+    DevCtx x;
+    fill_ctx(c, dp, (const char*)in + off * es, (char*)out + off * es, &x);
+    LaunchArgs la;
+    la.kind = LAUNCH_EXEC;
+    la.ctx = x;
+    la.grid = choose_grid(c, n * es * c->nranks, dp->prog.nchan);
+    la.stream = st;
+    la.nts = s.nts;
+    // all-gather moves bytes only: run the SUM instantiation (the op is never applied, K == 1)
+    if ((rc = launch_dtype(dtype, coll == Coll::ALL_GATHER ? FLEXAR_SUM : op, la))) return rc;
+  }
+  c->calls++;
+  c->bytes += count * es * c->nranks;
+  return 0;
 }
 
 static int check_err(flexar_comm* c) {
@@ -606,6 +640,26 @@ int flexar_allreduce(flexar_comm_t c, const void* in, void* out, size_t count, i
   return flexar_allreduce_ex(c, in, out, count, dtype, op, stream, nullptr, 1.0f);
 }
 
+int flexar_reduce_scatter(flexar_comm_t c, const void* in, void* out, size_t count, int dtype, int op, void* stream,
+                          const char* algo) {
+  int rc = validate_call(c, dtype, op, 1.0f);
+  if (rc) return rc;
+  if (!in || !out) { set_error("reduce_scatter needs distinct send/recv buffers"); return FLEXAR_ERR_INVALID; }
+  if ((rc = check_err(c))) return rc;
+  if (count == 0) return 0;
+  return run_rs_ag(c, Coll::REDUCE_SCATTER, in, out, count, dtype, op, (hipStream_t)stream, algo, 1.0f);
+}
+
+int flexar_all_gather(flexar_comm_t c, const void* in, void* out, size_t count, int dtype, void* stream,
+                      const char* algo) {
+  int rc = validate_call(c, dtype, FLEXAR_SUM, 1.0f);
+  if (rc) return rc;
+  if (!in || !out) { set_error("all_gather needs send/recv buffers"); return FLEXAR_ERR_INVALID; }
+  if ((rc = check_err(c))) return rc;
+  if (count == 0) return 0;
+  return run_rs_ag(c, Coll::ALL_GATHER, in, out, count, dtype, FLEXAR_SUM, (hipStream_t)stream, algo, 1.0f);
+}
+
 // ---- in-process group: N ranks on ONE device in one process (tests / calibration) -------------
 int flexar_group_create(int nranks, int device, size_t workspace_bytes, flexar_comm_t* comms) {
   if (!comms || nranks < 1 || nranks > (int)kMaxRanks) { set_error("invalid nranks"); return FLEXAR_ERR_INVALID; }
@@ -705,6 +759,51 @@ int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
     if (rc) return rc;
     FX_HIP(hipStreamSynchronize(st));  // d_ctx is reused by the next piece
   }
+  return 0;
+}
+
+// Reduce-scatter / all-gather for an in-process group (tests): one launch, every rank of the group.
+int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const void* const* ins, void* const* outs,
+                            size_t count, int dtype, int op, void* stream, const char* algo) {
+  if (!comms || nranks < 1 || (coll != 1 && coll != 2)) return FLEXAR_ERR_INVALID;
+  if (coll == 2) op = FLEXAR_SUM;
+  for (int r = 0; r < nranks; ++r) {
+    int rc = validate_call(comms[r], dtype, op, 1.0f);
+    if (rc) return rc;
+  }
+  if (count == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const uint32_t es = (uint32_t)dtype_size(dtype);
+  float fs = coll == 1 && op == FLEXAR_AVG ? 1.0f / (float)nranks : 1.0f;
+  static thread_local DevCtx* d_ctx = nullptr;
+  if (!d_ctx) FX_HIP(hipMalloc(&d_ctx, sizeof(DevCtx) * kMaxRanks));
+  std::vector<DevCtx> h(nranks);
+  int grid = 0;
+  bool nts = false;
+  for (int r = 0; r < nranks; ++r) {
+    AlgoSpec s;
+    int rc = resolve_spec(comms[r], algo, (double)count * es * nranks, &s);
+    if (rc) return rc;
+    if (s.kind != AlgoKind::RING) s.kind = AlgoKind::TREE, s.widths = {nranks}, s.ag = AgMode::PUSH;
+    nts = s.nts;
+    DevProgram* dp = nullptr;
+    if ((rc = get_program(comms[r], s, count, es, fs, &dp, (Coll)coll, count))) return rc;
+    if (dp->prog.stg_elems * es > comms[r]->exec_half) { set_error("group collective exceeds workspace"); return FLEXAR_ERR_NOMEM; }
+    fill_ctx(comms[r], dp, ins[r], outs[r], &h[r]);
+    int g = choose_grid(comms[r], count * es * nranks, dp->prog.nchan);
+    grid = r == 0 ? g : grid;
+  }
+  FX_HIP(hipMemcpyAsync(d_ctx, h.data(), sizeof(DevCtx) * nranks, hipMemcpyHostToDevice, st));
+  LaunchArgs la;
+  la.kind = LAUNCH_GROUP;
+  la.d_ctxs = d_ctx;
+  la.nranks = nranks;
+  la.grid = grid;
+  la.stream = st;
+  la.nts = nts;
+  int rc = launch_dtype(dtype, op, la);
+  if (rc) return rc;
+  FX_HIP(hipStreamSynchronize(st));
   return 0;
 }
 

@@ -98,3 +98,54 @@ def test_ddp_over_flexar(cuda, mode, model_kind):
         assert tb is None, tb
         assert used and used > 0, "flexar path was not used"
         assert err < (1e-5 if model_kind == "mlp" else 2e-4), (mode, model_kind, rank, err)
+
+
+def _colls(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
+                          FLEXAR_PG_FALLBACK="gloo", FLEXAR_TIMEOUT_MS="20000")
+        import torch.distributed as dist
+
+        from allreduce_over_mpi_amd.parallel import backend as fb  # noqa: F401
+
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        dist.init_process_group("flexar", rank=rank, world_size=world)
+        m = 1001
+        full = torch.arange(world * m, dtype=torch.float32, device=dev) * (rank + 1)
+        out = torch.empty(m, device=dev)
+        dist.reduce_scatter_tensor(out, full)
+        want = torch.arange(world * m, dtype=torch.float32, device=dev)[rank * m:(rank + 1) * m] * sum(
+            r + 1 for r in range(world))
+        e1 = (out - want).abs().max().item()
+        part = torch.full((m,), float(rank), device=dev)
+        gat = torch.empty(world * m, device=dev)
+        dist.all_gather_into_tensor(gat, part)
+        e2 = (gat - torch.arange(world, device=dev).float().repeat_interleave(m)).abs().max().item()
+        x = torch.ones(5, device=dev)
+        dist.all_reduce(x, op=dist.ReduceOp.AVG)
+        e3 = (x - 1).abs().max().item()
+        used = dist.group.WORLD.stats["flexar_allreduce"]
+        dist.destroy_process_group()
+        q.put((rank, max(e1, e2, e3), used, None))
+    except Exception:
+        import traceback
+
+        q.put((rank, None, None, traceback.format_exc()))
+
+
+def test_backend_reduce_scatter_all_gather(cuda):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_colls, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(2)]
+    for p in ps:
+        p.join(60)
+    for rank, err, used, tb in res:
+        assert tb is None, tb
+        assert err == 0.0 and used >= 3, (rank, err, used)

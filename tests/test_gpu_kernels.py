@@ -221,3 +221,24 @@ def test_group_ll_protocol(cuda, groups, dtype, n):
                 else:
                     assert torch.equal(o.view(torch.uint8), want.view(torch.uint8)), (dtype, size)
     grp.check()
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+@pytest.mark.parametrize("spec", ["flat", "ring", "flat+nts"])
+def test_group_reduce_scatter_all_gather(cuda, groups, n, spec):
+    grp = groups[n]
+    g = torch.Generator(device=cuda).manual_seed(41)
+    for m in (1, 37, 100003):
+        xs = [torch.randn(n * m, device=cuda, generator=g) for _ in range(n)]
+        outs = [torch.empty(m, device=cuda) for _ in range(n)]
+        grp.collective("reduce_scatter", xs, outs, algo=spec)
+        total = torch.stack([x.double() for x in xs]).sum(0)
+        for r, o in enumerate(outs):
+            assert (o.double() - total[r * m:(r + 1) * m]).abs().max().item() < 1e-4, (spec, n, m, r)
+        ys = [torch.randn(m, device=cuda, generator=g).to(torch.bfloat16) for _ in range(n)]
+        gath = [torch.empty(n * m, device=cuda, dtype=torch.bfloat16) for _ in range(n)]
+        grp.collective("all_gather", ys, gath, algo=spec)
+        cat = torch.cat(ys)
+        for o in gath:
+            assert torch.equal(o, cat)
+    grp.check()

@@ -151,3 +151,19 @@ def test_lonely_ranks(nv, n, spec):
             ref = ref_sum(ins)
             for o in outs:
                 np.testing.assert_allclose(o, ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 7, 8])
+@pytest.mark.parametrize("spec", ["flat", "ring"])
+def test_reduce_scatter_all_gather(nv, n, spec):
+    rng = np.random.default_rng(n)
+    for m in (1, 5, 1000, 4099):
+        ins = [rng.integers(-100, 100, n * m).astype(np.int32) for _ in range(n)]
+        outs = nv.simulate_coll("reduce_scatter", spec, ins, m, dtype="int32", grid=3)
+        total = np.sum(np.stack(ins), 0)
+        for r, o in enumerate(outs):
+            np.testing.assert_array_equal(o, total[r * m:(r + 1) * m], err_msg=f"rs {spec} n={n} m={m} r={r}")
+        ins = [rng.standard_normal(m).astype(np.float32) for _ in range(n)]
+        outs = nv.simulate_coll("all_gather", spec, ins, m, grid=3)
+        for o in outs:
+            np.testing.assert_array_equal(o, np.concatenate(ins), err_msg=f"ag {spec} n={n} m={m}")
