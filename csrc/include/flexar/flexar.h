@@ -149,6 +149,8 @@ int flexar_reduce_host(void* dst, const void* const* srcs, int nsrc, size_t coun
 int flexar_pointer_is_device(const void* p); /* 1 if p is device memory */
 int flexar_current_device(void);
 int flexar_copy_device_host(void* dst, const void* src, size_t bytes); /* synchronous, any direction */
+void* flexar_device_alloc(size_t bytes);
+void flexar_device_free(void* p);
 
 /* ---- host-only planning utilities (no GPU needed) ------------------------ */
 /* Parse an FT_TOPO string for nranks with the reference's rules (any 1 -> ring, unset -> flat,

@@ -46,6 +46,8 @@
 
 extern "C" int flexar_pointer_is_device(const void* p);  // libflexar: hipPointerGetAttributes
 extern "C" int flexar_copy_device_host(void* dst, const void* src, size_t bytes);  // synchronous hipMemcpy
+extern "C" void* flexar_device_alloc(size_t bytes);
+extern "C" void flexar_device_free(void* p);
 
 // Feature probe (reference mpi_mod.hpp:8-12 printed "FlexTree enabled").
 static inline int FT_enabled() {
@@ -168,11 +170,19 @@ struct HostComm {
   std::map<std::string, std::unique_ptr<Program>> plans;
   std::map<std::string, std::unique_ptr<P2PPlan>> p2p;
   std::vector<char> p2p_stg, outbox, inbox, host_stage;
+  // node structure for device buffers across nodes (FLEXAR_NODE_SIZE=k forces virtual nodes of k ranks)
+  MPI_Comm local = MPI_COMM_NULL, cross = MPI_COMM_NULL;
+  int nodes = 1;
+  void* shard_dev = nullptr;
+  size_t shard_cap = 0;
   std::unique_ptr<Pool> pool;
   XgmiModel model = XgmiModel::from_env();
   int threads = 1;
 
   ~HostComm() {
+    if (shard_dev) flexar_device_free(shard_dev);
+    if (local != MPI_COMM_NULL) MPI_Comm_free(&local);
+    if (cross != MPI_COMM_NULL) MPI_Comm_free(&cross);
     if (win != MPI_WIN_NULL) MPI_Win_free(&win);
     if (comm != MPI_COMM_NULL) MPI_Comm_free(&comm);
   }
@@ -187,6 +197,19 @@ struct HostComm {
     MPI_Comm_size(node, &nsz);
     MPI_Comm_free(&node);
     shared = (nsz == size) && getenv("FLEXAR_MPI_P2P") == nullptr;
+    // node split: physical shared-memory domains, or virtual nodes of FLEXAR_NODE_SIZE ranks
+    const char* ns = getenv("FLEXAR_NODE_SIZE");
+    int k = ns ? atoi(ns) : 0;
+    if (k > 0 && size % k == 0) {
+      MPI_Comm_split(comm, rank / k, rank, &local);
+    } else {
+      MPI_Comm_split_type(comm, MPI_COMM_TYPE_SHARED, rank, MPI_INFO_NULL, &local);
+    }
+    int lr = 0, ls = 1;
+    MPI_Comm_rank(local, &lr);
+    MPI_Comm_size(local, &ls);
+    MPI_Comm_split(comm, lr, rank, &cross);
+    MPI_Comm_size(cross, &nodes);
     const char* t = getenv("FLEXAR_HOST_THREADS");
     threads = t ? atoi(t) : 1;
     if (threads < 1) threads = 1;
@@ -435,6 +458,51 @@ inline flexar_comm_t device_comm(MPI_Comm comm) {
 }
 
 inline int allreduce(const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype datatype, MPI_Op mop,
+                     MPI_Comm comm);
+
+// Device buffers spanning nodes: intra-node reduce-scatter over xGMI (flexar), inter-node allreduce
+// of each rank's 1/L shard through host memory (p2p engine over the cross-node communicator of the
+// ranks with the same node-local index), intra-node all-gather over xGMI. Each rank ships only 1/L of
+// the buffer across nodes — the hierarchical form of the reference's multi-host FlexTree.
+inline int hierarchical_device_allreduce(HostComm& hc, const void* in, void* out, size_t count, MPI_Datatype datatype,
+                                         MPI_Op mop, int dt, int op) {
+  int L = 1;
+  MPI_Comm_size(hc.local, &L);
+  const size_t es = dtype_size(dt);
+  const size_t m = count / L, main = m * L, rem = count - main;
+  flexar_comm_t dc = device_comm(hc.local);
+  int rc = MPI_SUCCESS;
+  if (m > 0) {
+    if (hc.shard_cap < m * es) {
+      if (hc.shard_dev) flexar_device_free(hc.shard_dev);
+      hc.shard_dev = flexar_device_alloc(m * es);
+      hc.shard_cap = hc.shard_dev ? m * es : 0;
+      if (!hc.shard_dev) return MPI_ERR_NO_MEM;
+    }
+    if (flexar_reduce_scatter(dc, in, hc.shard_dev, m, dt, op, nullptr, nullptr)) {
+      fprintf(stderr, "[flexar] reduce_scatter: %s\n", flexar_last_error());
+      return MPI_ERR_OTHER;
+    }
+    hc.host_stage.resize(m * es);
+    if (flexar_copy_device_host(hc.host_stage.data(), hc.shard_dev, m * es)) return MPI_ERR_OTHER;
+    rc = allreduce(MPI_IN_PLACE, hc.host_stage.data(), m, datatype, mop, hc.cross);
+    if (rc != MPI_SUCCESS) return rc;
+    if (flexar_copy_device_host(hc.shard_dev, hc.host_stage.data(), m * es)) return MPI_ERR_OTHER;
+    if (flexar_all_gather(dc, hc.shard_dev, out, m, dt, nullptr, nullptr)) {
+      fprintf(stderr, "[flexar] all_gather: %s\n", flexar_last_error());
+      return MPI_ERR_OTHER;
+    }
+  }
+  if (rem > 0) {  // fewer than L trailing elements: whole-communicator host allreduce
+    std::vector<char> tail(rem * es);
+    if (flexar_copy_device_host(tail.data(), (const char*)in + main * es, rem * es)) return MPI_ERR_OTHER;
+    rc = allreduce(MPI_IN_PLACE, tail.data(), rem, datatype, mop, hc.comm);
+    if (rc == MPI_SUCCESS && flexar_copy_device_host((char*)out + main * es, tail.data(), rem * es)) rc = MPI_ERR_OTHER;
+  }
+  return rc;
+}
+
+inline int allreduce(const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype datatype, MPI_Op mop,
                      MPI_Comm comm) {
   const int dt = dtype_of(datatype), op = op_of(mop);
   if (dt < 0 || op < 0 || !op_supported(dt, op)) {
@@ -449,7 +517,9 @@ inline int allreduce(const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
   if (count == 0) return MPI_SUCCESS;
   if (flexar_pointer_is_device(recvbuf)) {
     HostComm* hc = host_comm(comm);
-    if (hc->shared || size <= 1) {  // one node: xGMI/IPC GPU engine
+    if (hc->nodes > 1 && getenv("FLEXAR_MPI_FLAT_STAGING") == nullptr)
+      return hierarchical_device_allreduce(*hc, in, recvbuf, count, datatype, mop, dt, op);
+    if (hc->nodes == 1 || size <= 1) {  // one node: xGMI/IPC GPU engine
       flexar_comm_t c = device_comm(comm);
       int rc = flexar_allreduce(c, in, recvbuf, count, dt, op, nullptr);
       if (rc) { fprintf(stderr, "[flexar] allreduce: %s\n", flexar_last_error()); return MPI_ERR_OTHER; }

@@ -824,6 +824,13 @@ int flexar_copy_device_host(void* dst, const void* src, size_t bytes) {
   return 0;
 }
 
+void* flexar_device_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) return nullptr;
+  return p;
+}
+void flexar_device_free(void* p) { (void)hipFree(p); }
+
 int flexar_current_device(void) {
   int d = 0;
   if (hipGetDevice(&d) != hipSuccess) return 0;

@@ -38,9 +38,19 @@ def test_mpi_device_buffers_ipc(tools, algo):
 
 
 def test_mpi_device_buffers_host_staging(tools):
+    """Ranks on 'different nodes' (virtual nodes of 1 rank): whole buffer staged through host p2p."""
     r = _mpirun(2, [tools["flexar_bench"], "--mem", "device", "--size", "65537", "--repeat", "3", "--check"],
-                env={"FLEXAR_MPI_P2P": "1"})
+                env={"FLEXAR_NODE_SIZE": "1", "FLEXAR_MPI_FLAT_STAGING": "1", "FLEXAR_MPI_P2P": "1"})
     assert r.returncode == 0 and "check n=65537: ok" in r.stdout, r.stdout[-3000:]
+
+
+@pytest.mark.parametrize("size", ["1", "7", "100003"])
+def test_mpi_device_hierarchical(tools, size):
+    """4 ranks as 2 virtual nodes x 2: intra-node reduce-scatter (flexar/IPC) -> inter-node host p2p
+    allreduce of the shard -> intra-node all-gather; plus the < L-element tail."""
+    r = _mpirun(4, [tools["flexar_bench"], "--mem", "device", "--size", size, "--repeat", "3", "--check"],
+                env={"FLEXAR_NODE_SIZE": "2", "FLEXAR_MPI_P2P": "1"})
+    assert r.returncode == 0 and f"check n={size}: ok" in r.stdout, r.stdout[-3000:]
 
 
 def test_bench_bf16_and_rccl_comparator(tools):
