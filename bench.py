@@ -139,9 +139,9 @@ def main():
     if world > 1 and algo == "auto" and not args.no_tune:
         from allreduce_over_mpi_amd import _native as nv
 
-        cands = ["flat+pull", "flat+push", "flat+pull+nts", "flat+push+nts"]
+        cands = ["flat+pull", "flat+push", "flat+pull+nts", "flat+push+nts", "flat+pull+wt", "flat+push+wt"]
         maxc = len([d for d in range(1, world) if math.gcd(d, world) == 1])
-        cands += ["ring"] + [f"ring:{c}" for c in (2, 4, 8) if c <= maxc]
+        cands += ["ring", "ring+wt"] + [f"ring:{c}{m}" for c in (2, 4, 8) if c <= maxc for m in ("", "+wt")]
         if world > 2 and (world & (world - 1)) == 0:
             cands += ["rhd+pull"]
         best, best_t = None, float("inf")

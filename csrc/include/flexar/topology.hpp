@@ -33,6 +33,7 @@ struct AlgoSpec {
   AgMode ag = AgMode::AUTO; // TREE: all-gather direction
   bool fuse = true;         // fuse reduce->forward (tree RS / AG multicast)
   bool nts = false;         // executor stores with the streaming (nontemporal) policy
+  bool wt = false;          // write-through protocol: sc0 sc1 payload, fence-free SIGNAL/WAIT
 
   std::string str() const {
     std::ostringstream ss;
@@ -50,6 +51,7 @@ struct AlgoSpec {
     if (kind == AlgoKind::TREE && ag == AgMode::PUSH) ss << "+push";
     if (!fuse) ss << "+nofuse";
     if (nts) ss << "+nts";
+    if (wt) ss << "+wt";
     return ss.str();
   }
 };
@@ -172,6 +174,7 @@ inline bool parse_algo(const std::string& raw, int nranks, AlgoSpec* spec, std::
     else if (mod == "nofuse") spec->fuse = false;
     else if (mod == "fuse") spec->fuse = true;
     else if (mod == "nts") spec->nts = true;
+    else if (mod == "wt") spec->wt = true;
     else { if (err) *err = "unknown algorithm modifier '+" + mod + "'"; return false; }
   }
   std::string head = s, arg;
@@ -215,9 +218,9 @@ inline bool parse_algo(const std::string& raw, int nranks, AlgoSpec* spec, std::
   }
   if (head == "ft") {
     const char* env = getenv("FT_TOPO");
-    AgMode ag = spec->ag; bool fuse = spec->fuse, nts = spec->nts;
+    AgMode ag = spec->ag; bool fuse = spec->fuse, nts = spec->nts, wt = spec->wt;
     if (!parse_ft_topo(!arg.empty() ? arg.c_str() : env, nranks, spec, err)) return false;
-    spec->ag = ag; spec->fuse = fuse; spec->nts = nts;
+    spec->ag = ag; spec->fuse = fuse; spec->nts = nts; spec->wt = wt;
     return true;
   }
   if (err) *err = "unknown algorithm '" + raw + "'";

@@ -121,7 +121,7 @@ struct flexar_comm {
   AlgoSpec spec;              // communicator default
   int grid_override = 0;
   int max_grid = 256;
-  uint64_t min_block_bytes = 256 * 1024;
+  uint64_t min_block_bytes = 32 * 1024;
   uint64_t timeout_ticks = 0;
   uint32_t fi_kind = 0, fi_slot = 0;
   uint64_t fi_ticks = 0;
@@ -226,6 +226,8 @@ static int get_program(flexar_comm* c, const AlgoSpec& s, uint64_t count, uint32
   return 0;
 }
 
+static int proto_of(const AlgoSpec& s) { return s.wt ? PM_WT : s.nts ? PM_FENCE_NTS : PM_FENCE; }
+
 static int choose_grid(flexar_comm* c, uint64_t bytes, uint32_t nchan) {
   int g = c->grid_override;
   if (g <= 0) {
@@ -311,7 +313,7 @@ static int run_rs_ag(flexar_comm* c, Coll coll, const void* in, void* out, size_
     la.ctx = x;
     la.grid = choose_grid(c, n * es * c->nranks, dp->prog.nchan);
     la.stream = st;
-    la.nts = s.nts;
+    la.proto = proto_of(s);
     // all-gather moves bytes only: run the SUM instantiation (the op is never applied, K == 1)
     if ((rc = launch_dtype(dtype, coll == Coll::ALL_GATHER ? FLEXAR_SUM : op, la))) return rc;
   }
@@ -373,7 +375,7 @@ static void init_defaults(flexar_comm* c) {
   c->max_grid = (int)env_u64("FLEXAR_MAX_GRID", 256);
   if (c->max_grid < 1) c->max_grid = 1;
   if (c->max_grid > (int)kMaxGridBlocks) c->max_grid = kMaxGridBlocks;
-  c->min_block_bytes = env_u64("FLEXAR_MIN_BLOCK_BYTES", 256 * 1024);
+  c->min_block_bytes = env_u64("FLEXAR_MIN_BLOCK_BYTES", 32 * 1024);
   c->profile = env_u64("FLEXAR_PROFILE", 0) != 0;
   if (!c->min_block_bytes) c->min_block_bytes = 1;
   // FLEXAR_FAULT_INJECT=delay:RANK:SLOT:MICROSECONDS | drop:RANK:SLOT  (tests / race hunting)
@@ -593,7 +595,7 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     la.ctx = x;
     la.grid = grid;
     la.stream = st;
-    la.nts = s.nts;
+    la.proto = proto_of(s);
     rc = launch_dtype(dtype, op, la);
     if (rc) break;
   }
@@ -754,7 +756,7 @@ int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
     la.nranks = nranks;
     la.grid = grid;
     la.stream = st;
-    la.nts = specs[0].nts;
+    la.proto = proto_of(specs[0]);
     int rc = launch_dtype(dtype, op, la);
     if (rc) return rc;
     FX_HIP(hipStreamSynchronize(st));  // d_ctx is reused by the next piece
@@ -779,13 +781,13 @@ int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const vo
   if (!d_ctx) FX_HIP(hipMalloc(&d_ctx, sizeof(DevCtx) * kMaxRanks));
   std::vector<DevCtx> h(nranks);
   int grid = 0;
-  bool nts = false;
+  int proto = PM_FENCE;
   for (int r = 0; r < nranks; ++r) {
     AlgoSpec s;
     int rc = resolve_spec(comms[r], algo, (double)count * es * nranks, &s);
     if (rc) return rc;
     if (s.kind != AlgoKind::RING) s.kind = AlgoKind::TREE, s.widths = {nranks}, s.ag = AgMode::PUSH;
-    nts = s.nts;
+    proto = proto_of(s);
     DevProgram* dp = nullptr;
     if ((rc = get_program(comms[r], s, count, es, fs, &dp, (Coll)coll, count))) return rc;
     if (dp->prog.stg_elems * es > comms[r]->exec_half) { set_error("group collective exceeds workspace"); return FLEXAR_ERR_NOMEM; }
@@ -800,7 +802,7 @@ int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const vo
   la.nranks = nranks;
   la.grid = grid;
   la.stream = st;
-  la.nts = nts;
+  la.proto = proto;
   int rc = launch_dtype(dtype, op, la);
   if (rc) return rc;
   FX_HIP(hipStreamSynchronize(st));

@@ -58,11 +58,14 @@ struct DevCtx {
 #define FLEXAR_NT_LOADS 1
 #endif
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// Payload pointers are always global memory (HBM, local or IPC-mapped): address-space-1 accesses
+// compile to global_load/store (one counter, no flat aperture check) instead of flat_*.
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
 __device__ FX_INLINE uint4 ld16(const char* p) {
 #if defined(FLEXAR_NT_LOADS)
-  u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  u32x4 v = __builtin_nontemporal_load((const g_u32x4*)(p));
 #else
-  u32x4 v = *reinterpret_cast<const u32x4*>(p);
+  u32x4 v = *(const g_u32x4*)(p);
 #endif
   return uint4{v.x, v.y, v.z, v.w};
 }
@@ -70,11 +73,74 @@ template <bool NTS = false>
 __device__ FX_INLINE void st16(char* p, uint4 x) {
   u32x4 v = {x.x, x.y, x.z, x.w};
 #if defined(FLEXAR_NT_STORES)
-  __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+  __builtin_nontemporal_store(v, (g_u32x4*)(p));
 #else
-  if constexpr (NTS) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));  // "+nts": streaming stores
-  else *reinterpret_cast<u32x4*>(p) = v;
+  if constexpr (NTS) __builtin_nontemporal_store(v, (g_u32x4*)(p));  // "+nts": streaming stores
+  else *(g_u32x4*)(p) = v;
 #endif
+}
+
+// Executor protocol modes (template parameter PM of the executor):
+//   PM_FENCE      plain stores; SIGNAL = system release (buffer_wbl2 sc0 sc1), WAIT = system acquire
+//                 (buffer_inv sc0 sc1)
+//   PM_FENCE_NTS  the same with streaming (nontemporal) stores ("+nts")
+//   PM_WT         write-through ("+wt"): every payload load/store is system-coherent (sc0 sc1), so a
+//                 drained store (vmcnt(0)) is already visible to every agent and the hand-off needs no
+//                 L2 write-back or invalidate — SIGNAL is vmcnt(0) + barrier + flag store, WAIT is poll +
+//                 barrier. This is the LL protocol's visibility rule (sc0 sc1 granules) applied to bulk
+//                 data, and MI355X_MICROARCH.md's "sc1 stores + drained flag + sc1 loads" hand-off at
+//                 system scope.
+enum : int { PM_FENCE = 0, PM_FENCE_NTS = 1, PM_WT = 2 };
+constexpr int kAuxSys = 1 | 16;  // buffer cache-policy bits: sc0 | sc1 (system coherence)
+constexpr uint32_t kRsrcWord3 = 0x00020000u;  // gfx9 raw buffer descriptor word 3 (dword data format)
+constexpr uint64_t kWtChunkBytes = 1ull << 30;  // buffer offsets are 32-bit: spans go in <= 1 GiB pieces
+
+// Operands are workgroup-uniform; readfirstlane states it so the descriptor lives in SGPRs (otherwise
+// the compiler wraps every buffer access in a waterfall loop).
+__device__ FX_INLINE __amdgpu_buffer_rsrc_t rsrc_of(const char* p, uint64_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint64_t u = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a) |
+                     ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32);
+  const int nrec = __builtin_amdgcn_readfirstlane((int)(uint32_t)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(u), (short)0, nrec, (int)kRsrcWord3);
+}
+__device__ FX_INLINE uint4 ld16_sys(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kAuxSys);
+  return uint4{v.x, v.y, v.z, v.w};
+}
+__device__ FX_INLINE void st16_sys(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 x) {
+  u32x4 v = {x.x, x.y, x.z, x.w};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxSys);
+}
+template <int B> struct UintOf;
+template <> struct UintOf<1> { using type = uint8_t; };
+template <> struct UintOf<2> { using type = uint16_t; };
+template <> struct UintOf<4> { using type = uint32_t; };
+template <> struct UintOf<8> { using type = uint64_t; };
+// scalar element access; PM_WT: system-coherent (global_load/store_* sc0 sc1)
+template <int PM, typename T>
+__device__ FX_INLINE T ld_elem(const char* base, uint64_t i) {
+  if constexpr (PM == PM_WT) {
+    using U = typename UintOf<sizeof(T)>::type;
+    U u = __hip_atomic_load(reinterpret_cast<U*>(const_cast<char*>(base)) + i, __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_SYSTEM);
+    T t;
+    __builtin_memcpy(&t, &u, sizeof(T));
+    return t;
+  } else {
+    return reinterpret_cast<const T*>(base)[i];
+  }
+}
+template <int PM, typename T>
+__device__ FX_INLINE void st_elem(char* base, uint64_t i, T t) {
+  if constexpr (PM == PM_WT) {
+    using U = typename UintOf<sizeof(T)>::type;
+    U u;
+    __builtin_memcpy(&u, &t, sizeof(T));
+    __hip_atomic_store(reinterpret_cast<U*>(base) + i, u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  } else {
+    reinterpret_cast<T*>(base)[i] = t;
+  }
 }
 
 template <typename T, typename OP, int K>
@@ -105,71 +171,90 @@ __device__ FX_INLINE uint4 combine16(const uint4 (&x)[K], float scale, bool sc) 
 }
 
 // dst[0..nd) = OP(src[0..K)) over n elements; this workgroup's threads only.
-template <typename T, typename OP, int K, bool NTS = false>
+template <typename T, typename OP, int K, int PM>
 __device__ FX_INLINE void xfer_k(const char* const (&s)[kMaxSrc], char* const (&d)[kMaxDst], int nd, uint64_t n,
                                  float scale, bool vec) {
   using A = typename Elem<T>::acc;
   constexpr int E = 16 / sizeof(T);
   constexpr int U = (K <= 2) ? 4 : ((K <= 4) ? 2 : 1);  // 16-B loads in flight per lane ~ 4..8
+  constexpr bool WT = PM == PM_WT;
+  constexpr bool NTS = PM == PM_FENCE_NTS;
   const bool sc = Elem<T>::is_float && scale != 1.0f;
   const uint64_t nt = blockDim.x;
   const uint64_t nv = vec ? n / E : 0;
+  // PM_WT: one raw buffer descriptor per operand (bounded by the span: n * sizeof(T) < 4 GiB)
+  __amdgpu_buffer_rsrc_t rs[K], rd[kMaxDst];
+  if constexpr (WT) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) rs[k] = rsrc_of(s[k], n * sizeof(T));
+#pragma unroll
+    for (int dd = 0; dd < kMaxDst; ++dd)
+      if (dd < nd) rd[dd] = rsrc_of(d[dd], n * sizeof(T));
+  }
+  auto ld = [&](int k, uint64_t v) -> uint4 {
+    if constexpr (WT) return ld16_sys(rs[k], (uint32_t)(v * 16));
+    else return ld16(s[k] + v * 16);
+  };
+  auto st = [&](int dd, uint64_t v, uint4 y) {
+    if constexpr (WT) st16_sys(rd[dd], (uint32_t)(v * 16), y);
+    else st16<NTS>(d[dd] + v * 16, y);
+  };
   uint64_t v = threadIdx.x;
   for (; v + (U - 1) * nt < nv; v += U * nt) {
     uint4 x[U][K];
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int k = 0; k < K; ++k) x[u][k] = ld16(s[k] + (v + u * nt) * 16);
+      for (int k = 0; k < K; ++k) x[u][k] = ld(k, v + u * nt);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       uint4 y = combine16<T, OP, K>(x[u], scale, sc);
 #pragma unroll
       for (int dd = 0; dd < kMaxDst; ++dd)
-        if (dd < nd) st16<NTS>(d[dd] + (v + u * nt) * 16, y);
+        if (dd < nd) st(dd, v + u * nt, y);
     }
   }
   for (; v < nv; v += nt) {
     uint4 x[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) x[k] = ld16(s[k] + v * 16);
+    for (int k = 0; k < K; ++k) x[k] = ld(k, v);
     uint4 y = combine16<T, OP, K>(x, scale, sc);
 #pragma unroll
     for (int dd = 0; dd < kMaxDst; ++dd)
-      if (dd < nd) st16<NTS>(d[dd] + v * 16, y);
+      if (dd < nd) st(dd, v, y);
   }
   // scalar tail (or whole span when a base address is not 16-B aligned)
   for (uint64_t i = nv * E + threadIdx.x; i < n; i += nt) {
     if (K == 1 && !sc) {
-      const T y = reinterpret_cast<const T*>(s[0])[i];
+      const T y = ld_elem<PM, T>(s[0], i);
 #pragma unroll
       for (int dd = 0; dd < kMaxDst; ++dd)
-        if (dd < nd) reinterpret_cast<T*>(d[dd])[i] = y;
+        if (dd < nd) st_elem<PM, T>(d[dd], i, y);
       continue;
     }
-    A acc = Elem<T>::load(reinterpret_cast<const T*>(s[0])[i]);
+    A acc = Elem<T>::load(ld_elem<PM, T>(s[0], i));
 #pragma unroll
-    for (int k = 1; k < K; ++k) acc = OP::apply(acc, Elem<T>::load(reinterpret_cast<const T*>(s[k])[i]));
+    for (int k = 1; k < K; ++k) acc = OP::apply(acc, Elem<T>::load(ld_elem<PM, T>(s[k], i)));
     if (sc) acc = (A)(acc * (A)scale);
     T y = Elem<T>::store(acc);
 #pragma unroll
     for (int dd = 0; dd < kMaxDst; ++dd)
-      if (dd < nd) reinterpret_cast<T*>(d[dd])[i] = y;
+      if (dd < nd) st_elem<PM, T>(d[dd], i, y);
   }
 }
 
-template <typename T, typename OP, bool NTS = false>
+template <typename T, typename OP, int PM>
 __device__ FX_INLINE void xfer_dispatch(int K, const char* const (&s)[kMaxSrc], char* const (&d)[kMaxDst], int nd,
                                         uint64_t n, float scale, bool vec) {
   switch (K) {
-    case 1: xfer_k<T, OP, 1, NTS>(s, d, nd, n, scale, vec); break;
-    case 2: xfer_k<T, OP, 2, NTS>(s, d, nd, n, scale, vec); break;
-    case 3: xfer_k<T, OP, 3, NTS>(s, d, nd, n, scale, vec); break;
-    case 4: xfer_k<T, OP, 4, NTS>(s, d, nd, n, scale, vec); break;
-    case 5: xfer_k<T, OP, 5, NTS>(s, d, nd, n, scale, vec); break;
-    case 6: xfer_k<T, OP, 6, NTS>(s, d, nd, n, scale, vec); break;
-    case 7: xfer_k<T, OP, 7, NTS>(s, d, nd, n, scale, vec); break;
-    default: xfer_k<T, OP, 8, NTS>(s, d, nd, n, scale, vec); break;
+    case 1: xfer_k<T, OP, 1, PM>(s, d, nd, n, scale, vec); break;
+    case 2: xfer_k<T, OP, 2, PM>(s, d, nd, n, scale, vec); break;
+    case 3: xfer_k<T, OP, 3, PM>(s, d, nd, n, scale, vec); break;
+    case 4: xfer_k<T, OP, 4, PM>(s, d, nd, n, scale, vec); break;
+    case 5: xfer_k<T, OP, 5, PM>(s, d, nd, n, scale, vec); break;
+    case 6: xfer_k<T, OP, 6, PM>(s, d, nd, n, scale, vec); break;
+    case 7: xfer_k<T, OP, 7, PM>(s, d, nd, n, scale, vec); break;
+    default: xfer_k<T, OP, 8, PM>(s, d, nd, n, scale, vec); break;
   }
 }
 
@@ -180,7 +265,7 @@ __device__ FX_INLINE void st_flag(uint64_t* f, uint64_t v) {
   __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-template <typename T, typename OP, bool NTS>
+template <typename T, typename OP, int PM>
 __device__ FX_INLINE void xfer_op(const DevCtx& c, const Op* o, uint32_t lb, uint32_t nb, uint32_t quantum,
                                   uint64_t par) {
   uint64_t lo, hi;
@@ -210,10 +295,23 @@ __device__ FX_INLINE void xfer_op(const DevCtx& c, const Op* o, uint32_t lb, uin
       vec &= (l.buf == BUF_STG) || c.vec_ok;
     }
   }
-  xfer_dispatch<T, OP, NTS>(ns, s, d, nd, hi - lo, o->scale, vec);
+  if constexpr (PM == PM_WT) {
+    const uint64_t step = kWtChunkBytes / sizeof(T);  // 32-bit buffer offsets
+    for (uint64_t p = 0; p < hi - lo; p += step) {
+      const char* s2[kMaxSrc];
+      char* d2[kMaxDst];
+#pragma unroll
+      for (int k = 0; k < kMaxSrc; ++k) s2[k] = k < ns ? s[k] + p * sizeof(T) : nullptr;
+#pragma unroll
+      for (int k = 0; k < kMaxDst; ++k) d2[k] = k < nd ? d[k] + p * sizeof(T) : nullptr;
+      xfer_dispatch<T, OP, PM>(ns, s2, d2, nd, (hi - lo - p) < step ? (hi - lo - p) : step, o->scale, vec);
+    }
+  } else {
+    xfer_dispatch<T, OP, PM>(ns, s, d, nd, hi - lo, o->scale, vec);
+  }
 }
 
-template <typename T, typename OP, bool NTS>
+template <typename T, typename OP, int PM>
 __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uint32_t grid) {
   __shared__ int s_abort;
   const uint32_t tid = threadIdx.x;
@@ -237,7 +335,7 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
       bool bar = false;
       for (uint32_t k = 0; k < n; ++k) {
         const Op* q = c.ops + i + (n > 1 ? (k + lb) % n : 0);
-        xfer_op<T, OP, NTS>(c, q, lb, nb, quantum, par);
+        xfer_op<T, OP, PM>(c, q, lb, nb, quantum, par);
         bar |= (q->flags & kXferBarrierAfter) != 0;
       }
       if (bar) __syncthreads();
@@ -253,7 +351,7 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
         while (__builtin_amdgcn_s_memrealtime() - t0 < c.fi_ticks) __builtin_amdgcn_s_sleep(8);
       }
       if (tid < 64) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        if constexpr (PM != PM_WT) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // WT: stores already drained
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the flag must not overtake the write-back
         if (tid < o->npeers) st_flag(c.peer_flags[o->peers[tid]] + flag_index(o->slot, c.rank, b), epoch);
       }
@@ -272,7 +370,7 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
             }
           }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        if constexpr (PM != PM_WT) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // WT: loads are sc0 sc1
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __syncthreads();
@@ -287,8 +385,8 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
   // call k reads parity(k) while an eager rank in call k+1 writes parity(k+1)). No slot is read in
   // this call by another workgroup: workgroup b2 reads only slot b2 < grid, and b2 == b (mod grid)
   // implies b2 == b.
-  if (tid == 0)
-    for (uint32_t j = b; j < kMaxGridBlocks; j += grid) c.epochs[j] = epoch;
+  // All lanes share the stores: one lane alone serialises up to 1024 stores at small grids.
+  for (uint32_t j = b + tid * grid; j < kMaxGridBlocks; j += blockDim.x * grid) c.epochs[j] = epoch;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -377,8 +475,8 @@ __device__ FX_INLINE void ll_body(const DevCtx& c, const uint32_t b, const uint3
     if (s_abort) break;
   }
   __syncthreads();
-  if (tid == 0)
-    for (uint32_t j = b; j < kMaxGridBlocks; j += grid) c.epochs[j] = epoch;
+  // All lanes share the stores: one lane alone serialises up to 1024 stores at small grids.
+  for (uint32_t j = b + tid * grid; j < kMaxGridBlocks; j += blockDim.x * grid) c.epochs[j] = epoch;
 }
 
 template <typename T, typename OP>
@@ -391,18 +489,18 @@ __global__ void __launch_bounds__(kExecThreads) ll_group_kernel(const DevCtx* ct
 }
 
 // Production launch: one rank per process, context by value.
-template <typename T, typename OP, bool NTS>
+template <typename T, typename OP, int PM>
 __global__ void __launch_bounds__(kExecThreads) exec_kernel(DevCtx c) {
-  exec_body<T, OP, NTS>(c, blockIdx.x, gridDim.x);
+  exec_body<T, OP, PM>(c, blockIdx.x, gridDim.x);
 }
 
 // In-process group launch: nranks ranks share one grid (rank = blockIdx / grid_per_rank) —
 // every rank's workgroups are co-resident by construction, so the full multi-rank protocol
 // runs on a single GPU in a single process (tests, calibration).
-template <typename T, typename OP, bool NTS>
+template <typename T, typename OP, int PM>
 __global__ void __launch_bounds__(kExecThreads) exec_group_kernel(const DevCtx* ctxs, uint32_t grid_per_rank) {
   const uint32_t r = blockIdx.x / grid_per_rank;
-  exec_body<T, OP, NTS>(ctxs[r], blockIdx.x % grid_per_rank, grid_per_rank);
+  exec_body<T, OP, PM>(ctxs[r], blockIdx.x % grid_per_rank, grid_per_rank);
 }
 
 // Standalone reduction: dst[0] = scale * OP(src[0..K)), grid-sliced.
@@ -424,7 +522,7 @@ __global__ void __launch_bounds__(kExecThreads) reduce_kernel(SrcTable srcs, int
 #pragma unroll
   for (int k = 0; k < kMaxDst; ++k) d[k] = nullptr;
   d[0] = dst + lo * sizeof(T);
-  xfer_dispatch<T, OP>(nsrc, s, d, 1, hi - lo, scale, vec != 0);
+  xfer_dispatch<T, OP, PM_FENCE>(nsrc, s, d, 1, hi - lo, scale, vec != 0);
 }
 
 }  // namespace flexar

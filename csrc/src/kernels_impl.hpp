@@ -12,17 +12,22 @@ template <typename T, typename OP>
 inline int launch_one(const LaunchArgs& a) {
   switch (a.kind) {
     case LAUNCH_EXEC:
-      if (a.nts)
-        hipLaunchKernelGGL((exec_kernel<T, OP, true>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
+      if (a.proto == PM_WT)
+        hipLaunchKernelGGL((exec_kernel<T, OP, PM_WT>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
+      else if (a.proto == PM_FENCE_NTS)
+        hipLaunchKernelGGL((exec_kernel<T, OP, PM_FENCE_NTS>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
       else
-        hipLaunchKernelGGL((exec_kernel<T, OP, false>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
+        hipLaunchKernelGGL((exec_kernel<T, OP, PM_FENCE>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
       break;
     case LAUNCH_GROUP:
-      if (a.nts)
-        hipLaunchKernelGGL((exec_group_kernel<T, OP, true>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
+      if (a.proto == PM_WT)
+        hipLaunchKernelGGL((exec_group_kernel<T, OP, PM_WT>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
+                           a.stream, a.d_ctxs, (uint32_t)a.grid);
+      else if (a.proto == PM_FENCE_NTS)
+        hipLaunchKernelGGL((exec_group_kernel<T, OP, PM_FENCE_NTS>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
                            a.stream, a.d_ctxs, (uint32_t)a.grid);
       else
-        hipLaunchKernelGGL((exec_group_kernel<T, OP, false>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
+        hipLaunchKernelGGL((exec_group_kernel<T, OP, PM_FENCE>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
                            a.stream, a.d_ctxs, (uint32_t)a.grid);
       break;
     case LAUNCH_REDUCE:

@@ -23,7 +23,7 @@ struct LaunchArgs {
   uint64_t n = 0;
   float scale = 1.0f;
   int vec = 1;
-  bool nts = false;  // streaming (nontemporal) stores in the executor ("+nts")
+  int proto = PM_FENCE;  // executor protocol mode (PM_*: "+nts", "+wt")
 };
 
 // Defined in k_<dtype>.hip; returns 0 or a FLEXAR_ERR_* code.

@@ -70,6 +70,7 @@ def _specs(n):
     from allreduce_over_mpi_amd import _native as nv
 
     base = ["flat", "flat+push", "ring", "oneshot", "ll", "flat+nts", "ring:2+nts"]
+    base += ["flat+wt", "flat+push+wt", "ring+wt", "ring:2+wt", "oneshot+wt"]
     base += [p for p in nv.enumerate_plans(n) if p.startswith("tree:") or p.startswith("ring:")]
     base += [p + "+push" for p in nv.enumerate_plans(n) if p.startswith("tree:") and "," in p]
     return sorted(set(base))
@@ -224,7 +225,7 @@ def test_group_ll_protocol(cuda, groups, dtype, n):
 
 
 @pytest.mark.parametrize("n", [2, 4, 8])
-@pytest.mark.parametrize("spec", ["flat", "ring", "flat+nts"])
+@pytest.mark.parametrize("spec", ["flat", "ring", "flat+nts", "flat+wt", "ring+wt"])
 def test_group_reduce_scatter_all_gather(cuda, groups, n, spec):
     grp = groups[n]
     g = torch.Generator(device=cuda).manual_seed(41)

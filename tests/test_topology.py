@@ -92,3 +92,14 @@ def test_algo_spec_errors(nv):
     assert nv.model_cost_us("tree:2,2", 8, 1e6) > 0  # 4 lonely ranks folded into 4 partners
     with pytest.raises(nv.FlexarError):
         nv.model_cost_us("bogus", 8, 1e6)
+
+
+def test_protocol_modifiers(nv):
+    # "+nts" / "+wt" change only the executor's memory protocol, never the schedule
+    for spec in ("flat+wt", "flat+push+wt", "ring:2+wt", "oneshot+wt", "flat+nts+wt"):
+        assert nv.model_cost_us(spec, 8, 1e6) > 0
+        base = spec.replace("+wt", "").replace("+nts", "")
+        body = lambda sp: nv.plan_dump(sp, 1, 8, 4096).split("\n", 1)[1]  # noqa: E731 (header names the spec)
+        assert body(spec) == body(base)
+    with pytest.raises(nv.FlexarError):
+        nv.model_cost_us("flat+wtx", 8, 1e6)
