@@ -144,6 +144,7 @@ def main():
         cands += ["ring", "ring+wt"] + [f"ring:{c}{m}" for c in (2, 4, 8) if c <= maxc for m in ("", "+wt")]
         if world > 2 and (world & (world - 1)) == 0:
             cands += ["rhd+pull"]
+        cands += ["dma"]  # copy engines (CU-free)
         best, best_t = None, float("inf")
         for spec in cands:
             failed = 0.0

@@ -43,6 +43,8 @@ struct XgmiModel {
   double link_gbps = 64.0;       // usable per-direction bandwidth of one xGMI link (GB/s)
   double hbm_gbps = 4000.0;      // effective local HBM bandwidth of the fused reduce
   int links = 7;                 // point-to-point links per GPU (fully connected 8-GPU node)
+  double alpha_dma_us = 15.0;    // copy-engine path: stream fork/join + stream-memory wait/write per phase
+  double dma_link_gbps = 50.0;   // one SDMA engine's peer-copy rate
 
   static XgmiModel from_env() {
     XgmiModel m;
@@ -59,10 +61,11 @@ struct XgmiModel {
   }
 
   // time (us) to move `bytes` to each of `fan` peers concurrently
-  double fanout_us(double bytes, int fan) const {
+  double fanout_us(double bytes, int fan) const { return fanout_us_at(bytes, fan, link_gbps); }
+  double fanout_us_at(double bytes, int fan, double gbps) const {
     if (fan <= 0 || bytes <= 0) return 0.0;
     double par = fan <= links ? 1.0 : (double)links / fan;  // more peers than links share them
-    return bytes / (link_gbps * 1e3 * par);
+    return bytes / (gbps * 1e3 * par);
   }
   double reduce_us(double bytes_read) const { return bytes_read / (hbm_gbps * 1e3); }
 
@@ -92,6 +95,9 @@ struct XgmiModel {
         if (s.ag == AgMode::PUSH || s.ag == AgMode::AUTO) t += reduce_us(S);  // local copy-out of pushed blocks
         return t;
       }
+      case AlgoKind::DMA:  // copy engines: CU-free, but a host-enqueued fork/join and 2 stream-memory hand-offs
+        return alpha_launch_us + 2.0 * alpha_dma_us + 2.0 * fanout_us_at(S / N, N - 1, dma_link_gbps) +
+               reduce_us(S);
       default:
         return 1e30;
     }

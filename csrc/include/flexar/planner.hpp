@@ -67,7 +67,7 @@ class Planner {
       P->desc = "copy";
     } else if (spec.kind == AlgoKind::RING) {
       int C = std::max(1, std::min(spec.channels, max_ring_channels(N)));
-      if (2ull * (N - 1) * C > kMaxSlots) { if (err) *err = "too many ring channels"; return false; }
+      if (2ull * (N - 1) * C > kProgSlots) { if (err) *err = "too many ring channels"; return false; }
       build_ring(C);
       P->desc = spec.str();
     } else if (spec.kind == AlgoKind::TREE) {
@@ -79,13 +79,18 @@ class Planner {
         if (err) *err = "tree widths must multiply to N (or to at least N/2 with lonely ranks)";
         return false;
       }
-      if (2 * spec.widths.size() + 2 > kMaxSlots) { if (err) *err = "too many stages"; return false; }
+      if (2 * spec.widths.size() + 2 > kProgSlots) { if (err) *err = "too many stages"; return false; }
       for (int w : spec.widths)
         if (w < 2) { if (err) *err = "tree width < 2"; return false; }
       build_tree_lonely(spec.widths, (uint32_t)prod, spec.ag == AgMode::PULL, spec.fuse);
       P->desc = spec.str();
     } else if (spec.kind == AlgoKind::ONESHOT) {
       build_oneshot();
+      P->desc = spec.str();
+    } else if (spec.kind == AlgoKind::DMA) {
+      // the copy-engine engine runs the flat two-shot exchange (RS push, AG pull) with SDMA copies and
+      // stream-ordered flag writes (comm.hip run_dma); this program is its host-executable equivalent
+      build_tree_lonely({(int)N}, N, true, true);
       P->desc = spec.str();
     } else if (spec.kind == AlgoKind::LL) {
       // executed by the dedicated LL kernel (no op program): only the staging size is planned

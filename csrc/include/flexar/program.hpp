@@ -29,7 +29,8 @@ enum : uint32_t {
   kMaxSrc = 8,           // fan-in per XFER; the planner chains wider reductions
   kMaxDst = 8,           // multicast fan-out per XFER (one-shot pushes to 7 peers)
   kMaxPeersPerOp = 8,    // peers per SIGNAL/WAIT
-  kMaxSlots = 128,       // flag slots (stages/steps) per program
+  kMaxSlots = 128,       // flag slots per rank: op programs use [0, kProgSlots), the copy-engine
+                         // (dma) allreduce the last two
   kMaxGridBlocks = 1024, // grid blocks per launch (per-block flags/epochs)
   kStageAlignBytes = 256 // staging regions / block boundaries alignment
 };
@@ -80,6 +81,9 @@ FX_HD FX_INLINE void slice_range(uint64_t len, uint32_t lb, uint32_t nb, uint32_
   *lo = l;
   *hi = h;
 }
+
+constexpr uint32_t kProgSlots = kMaxSlots - 2;
+constexpr uint32_t kDmaSlotRS = kMaxSlots - 2, kDmaSlotAG = kMaxSlots - 1;
 
 // Flag word index: flags[slot][src_rank][grid_block]
 FX_HD FX_INLINE uint64_t flag_index(uint32_t slot, uint32_t src_rank, uint32_t gblock) {

@@ -23,7 +23,7 @@
 
 namespace flexar {
 
-enum class AlgoKind { AUTO, RING, TREE, ONESHOT, LL };
+enum class AlgoKind { AUTO, RING, TREE, ONESHOT, LL, DMA };
 enum class AgMode { AUTO, PUSH, PULL };
 
 struct AlgoSpec {
@@ -41,6 +41,7 @@ struct AlgoSpec {
       case AlgoKind::AUTO: ss << "auto"; break;
       case AlgoKind::ONESHOT: ss << "oneshot"; break;
       case AlgoKind::LL: ss << "ll"; break;
+      case AlgoKind::DMA: ss << "dma"; break;
       case AlgoKind::RING: ss << "ring"; if (channels > 1) ss << ":" << channels; break;
       case AlgoKind::TREE:
         ss << "tree:";
@@ -183,6 +184,7 @@ inline bool parse_algo(const std::string& raw, int nranks, AlgoSpec* spec, std::
   if (head.empty() || head == "auto") { spec->kind = AlgoKind::AUTO; return true; }
   if (head == "oneshot") { spec->kind = AlgoKind::ONESHOT; return true; }
   if (head == "ll" || head == "oneshot_ll") { spec->kind = AlgoKind::LL; return true; }
+  if (head == "dma" || head == "sdma") { spec->kind = AlgoKind::DMA; return true; }
   if (head == "ring") {
     spec->kind = AlgoKind::RING;
     if (!arg.empty()) {

@@ -123,6 +123,8 @@ static bool spec_for(const char* spec, int nranks, double bytes, AlgoSpec* s, st
   if (s->kind == AlgoKind::AUTO) *s = select_plan(XgmiModel::from_env(), nranks, bytes);
   if (s->kind == AlgoKind::TREE && s->ag == AgMode::AUTO) s->ag = AgMode::PULL;
   if (s->kind == AlgoKind::LL && host_only) s->kind = AlgoKind::ONESHOT;  // LL is a device-only protocol
+  if (s->kind == AlgoKind::DMA && host_only) *s = AlgoSpec(), s->kind = AlgoKind::TREE, s->widths = {nranks},
+                                             s->ag = AgMode::PULL;  // same exchange, host-executable
   return true;
 }
 

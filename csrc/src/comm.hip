@@ -135,6 +135,12 @@ struct flexar_comm {
   struct Agg { uint64_t calls = 0, bytes = 0; double ms = 0; };
   std::map<std::string, Agg> prof;
   uint64_t calls = 0, bytes = 0;
+  // host mirror of the device epoch: every executor/LL launch and every dma call advances it by one
+  uint64_t launches = 0;
+  // copy-engine (dma) engine: one stream per peer (created on first use) and fork/join events
+  bool dma_ready = false;
+  hipStream_t dma_st[kMaxRanks] = {};
+  hipEvent_t dma_fork = nullptr, dma_join[kMaxRanks] = {};
 };
 
 namespace flexar {
@@ -235,8 +241,9 @@ static int choose_grid(flexar_comm* c, uint64_t bytes, uint32_t nchan) {
     g = (int)std::min<uint64_t>(want, (uint64_t)c->max_grid);
   }
   if (g < (int)nchan) g = (int)nchan;
-  g = (g + nchan - 1) / nchan * nchan;
-  if (g > (int)kMaxGridBlocks) g = (int)(kMaxGridBlocks / nchan * nchan);
+  g = (g + nchan - 1) / nchan * nchan;  // whole channels
+  const int cap = std::max((int)nchan, std::min(std::max(c->max_grid, c->grid_override), (int)kMaxGridBlocks));
+  if (g > cap) g = cap / (int)nchan * (int)nchan;  // round down rather than exceed the cap
   return g;
 }
 
@@ -316,9 +323,173 @@ static int run_rs_ag(flexar_comm* c, Coll coll, const void* in, void* out, size_
     la.proto = proto_of(s);
     // all-gather moves bytes only: run the SUM instantiation (the op is never applied, K == 1)
     if ((rc = launch_dtype(dtype, coll == Coll::ALL_GATHER ? FLEXAR_SUM : op, la))) return rc;
+    c->launches++;
   }
   c->calls++;
   c->bytes += count * es * c->nranks;
+  return 0;
+}
+
+// dst (and dst2, if given) = scale * OP(srcs[0..nsrc)) over `count` elements: groups of kMaxSrc
+// sources chain through dst (fan-in > 8: dst joins the next group; only the last group scales and
+// writes dst2).
+static int reduce_chain(char* dst, char* dst2, const char* const* srcs, int nsrc, uint64_t count, int dtype,
+                        int op, float fs, hipStream_t st, int proto) {
+  const size_t es = dtype_size(dtype);
+  int grid = (int)std::min<uint64_t>(1024, std::max<uint64_t>(1, count * es / (64 * 1024)));
+  int done = 0;
+  while (done < nsrc) {
+    SrcTable t;
+    memset(&t, 0, sizeof(t));
+    int k = 0;
+    if (done > 0) t.p[k++] = dst;
+    while (k < (int)kMaxSrc && done < nsrc) t.p[k++] = srcs[done++];
+    const bool last = done >= nsrc;
+    uintptr_t al = (uintptr_t)dst | (last && dst2 ? (uintptr_t)dst2 : 0);
+    for (int i = 0; i < k; ++i) al |= (uintptr_t)t.p[i];
+    LaunchArgs la;
+    la.kind = LAUNCH_REDUCE;
+    la.srcs = t;
+    la.nsrc = k;
+    la.dst = dst;
+    la.dst2 = last ? dst2 : nullptr;
+    la.n = count;
+    la.scale = last ? fs : 1.0f;
+    la.vec = (al & 15) == 0 ? 1 : 0;
+    la.grid = grid;
+    la.stream = st;
+    la.proto = proto;
+    int rc = launch_dtype(dtype, op, la);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+// ---- copy-engine ("dma") allreduce ------------------------------------------------------------
+// The flat two-shot exchange with the bytes moved by copy engines instead of CUs, so an allreduce
+// overlapped with compute (DDP backward) takes no CUs beyond a short reduce (SURVEY.md §5.8 (a),
+// the reference's MPI_Isend/Irecv per block, mpi_mod.hpp:662-765, as one peer copy per peer):
+//   phase 0  fork: on peer p's stream, copy my block p into p's landing slot r, then write flag
+//            (kDmaSlotRS, r) = e into p's flags (stream-ordered after the copy);
+//   phase 1  on the caller's stream: wait for every peer's RS flag, reduce my block (write-through)
+//            into OUT and my staging result slot, then write flag (kDmaSlotAG, r) = e to every peer;
+//   phase 2  on peer q's stream: wait for q's AG flag, copy q's result slot into my OUT block q;
+//            join the streams and advance the device epoch (staging parity) to e.
+// Staging per parity half: N landing slots + 1 result slot of one block each. The parity/epoch
+// argument of the executor applies unchanged because a dma call is one epoch.
+static int dma_init(flexar_comm* c) {
+  if (c->dma_ready) return 0;
+  FX_HIP(hipSetDevice(c->device));
+  for (int p = 0; p < c->nranks; ++p) {
+    if (p == c->rank) continue;
+    FX_HIP(hipStreamCreateWithFlags(&c->dma_st[p], hipStreamNonBlocking));
+    FX_HIP(hipEventCreateWithFlags(&c->dma_join[p], hipEventDisableTiming));
+  }
+  FX_HIP(hipEventCreateWithFlags(&c->dma_fork, hipEventDisableTiming));
+  c->dma_ready = true;
+  return 0;
+}
+
+// elements per dma piece: N + 1 block slots must fit one parity half
+static uint64_t dma_piece(flexar_comm* c, uint64_t count, uint32_t es) {
+  const uint64_t slot = c->exec_half / (uint64_t)(c->nranks + 1) / kStageAlignBytes * kStageAlignBytes;
+  const uint64_t per_block = std::max<uint64_t>(1, slot / es);
+  return std::min<uint64_t>(count, per_block * (uint64_t)c->nranks);
+}
+
+static int dma_wait(flexar_comm* c, uint32_t slot, const int* srcs, int n, uint64_t e, hipStream_t st) {
+  DmaWait w;
+  memset(&w, 0, sizeof(w));
+  w.flags = c->flags;
+  for (int i = 0; i < n; ++i) {
+    w.idx[i] = (uint32_t)flag_index(slot, (uint32_t)srcs[i], 0);
+    w.src[i] = (uint32_t)srcs[i];
+  }
+  w.n = (uint32_t)n;
+  w.slot = slot;
+  w.value = e;
+  w.timeout_ticks = c->timeout_ticks;
+  w.err = c->err_dev;
+  hipLaunchKernelGGL(dma_wait_kernel, dim3(1), dim3(64), 0, st, w);
+  FX_HIP(hipGetLastError());
+  return 0;
+}
+
+static int dma_phase(flexar_comm* c, int phase, const char* in, char* out, uint64_t count, int dtype, int op,
+                     float fs, hipStream_t st) {
+  const int N = c->nranks, r = c->rank;
+  const uint64_t es = dtype_size(dtype);
+  const uint64_t B = (count + N - 1) / N;
+  const uint64_t Bb = (B * es + kStageAlignBytes - 1) / kStageAlignBytes * kStageAlignBytes;
+  const uint64_t e = c->launches + 1;
+  const uint64_t par = (e & 1) ? c->half_bytes : 0;
+  auto len = [&](int i) -> uint64_t {
+    const uint64_t s0 = (uint64_t)i * B;
+    return s0 >= count ? 0 : std::min<uint64_t>(B, count - s0);
+  };
+  if (phase == 0) {
+    FX_HIP(hipEventRecord(c->dma_fork, st));
+    for (int j = 1; j < N; ++j) {
+      const int p = (r + j) % N;
+      hipStream_t s = c->dma_st[p];
+      FX_HIP(hipStreamWaitEvent(s, c->dma_fork, 0));
+      if (len(p))
+        FX_HIP(hipMemcpyAsync(c->peer_stg[p] + par + (uint64_t)r * Bb, in + (uint64_t)p * B * es, len(p) * es,
+                              hipMemcpyDeviceToDevice, s));
+      FX_HIP(hipStreamWriteValue64(s, c->peer_flags[p] + flag_index(kDmaSlotRS, (uint32_t)r, 0), e, 0));
+    }
+  } else if (phase == 1) {
+    int peers[kMaxRanks], np = 0;
+    for (int j = 1; j < N; ++j) peers[np++] = (r + j) % N;
+    int rc = dma_wait(c, kDmaSlotRS, peers, np, e, st);
+    if (rc) return rc;
+    if (len(r)) {
+      const char* srcs[kMaxRanks];
+      int ns = 0;
+      srcs[ns++] = in + (uint64_t)r * B * es;
+      for (int j = 0; j < np; ++j) srcs[ns++] = c->stg + par + (uint64_t)peers[j] * Bb;
+      rc = reduce_chain(out + (uint64_t)r * B * es, c->stg + par + (uint64_t)N * Bb, srcs, ns, len(r), dtype, op, fs,
+                        st, PM_WT);
+      if (rc) return rc;
+    }
+    for (int j = 0; j < np; ++j)
+      FX_HIP(hipStreamWriteValue64(st, c->peer_flags[peers[j]] + flag_index(kDmaSlotAG, (uint32_t)r, 0), e, 0));
+  } else {
+    for (int j = 1; j < N; ++j) {
+      const int q = (r + j) % N;
+      hipStream_t s = c->dma_st[q];  // same stream as the send to q: an in-place OUT block q is read first
+      int rc = dma_wait(c, kDmaSlotAG, &q, 1, e, s);
+      if (rc) return rc;
+      if (len(q))
+        FX_HIP(hipMemcpyAsync(out + (uint64_t)q * B * es, c->peer_stg[q] + par + (uint64_t)N * Bb, len(q) * es,
+                              hipMemcpyDeviceToDevice, s));
+      FX_HIP(hipEventRecord(c->dma_join[q], s));
+      FX_HIP(hipStreamWaitEvent(st, c->dma_join[q], 0));
+    }
+    hipLaunchKernelGGL(epoch_set_kernel, dim3(1), dim3(256), 0, st, c->epochs, e);
+    FX_HIP(hipGetLastError());
+    c->launches = e;
+  }
+  return 0;
+}
+
+static int run_dma(flexar_comm* const* cs, int ncomm, const char* const* ins, char* const* outs, uint64_t count,
+                   int dtype, int op, float fs, hipStream_t st) {
+  const uint32_t es = (uint32_t)dtype_size(dtype);
+  for (int i = 0; i < ncomm; ++i) {
+    int rc = dma_init(cs[i]);
+    if (rc) return rc;
+  }
+  const uint64_t piece = dma_piece(cs[0], count, es);
+  for (uint64_t off = 0; off < count; off += piece) {
+    const uint64_t n = std::min<uint64_t>(piece, count - off);
+    // phase by phase across the group: a rank's waits are enqueued after every rank's signals
+    for (int phase = 0; phase < 3; ++phase)
+      for (int i = 0; i < ncomm; ++i) {
+        int rc = dma_phase(cs[i], phase, ins[i] + off * es, outs[i] + off * es, n, dtype, op, fs, st);
+        if (rc) return rc;
+      }
+  }
   return 0;
 }
 
@@ -484,6 +655,11 @@ int flexar_comm_destroy(flexar_comm_t c) {
       (void)hipIpcCloseMemHandle(c->peer_stg[r]);
       (void)hipIpcCloseMemHandle(c->peer_flags[r]);
     }
+  for (int r = 0; r < kMaxRanks; ++r) {
+    if (c->dma_st[r]) (void)hipStreamDestroy(c->dma_st[r]);
+    if (c->dma_join[r]) (void)hipEventDestroy(c->dma_join[r]);
+  }
+  if (c->dma_fork) (void)hipEventDestroy(c->dma_fork);
   (void)hipFree(c->stg);
   (void)hipFree(c->flags);
   (void)hipFree(c->epochs);
@@ -554,6 +730,17 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
   AlgoSpec s;
   if ((rc = resolve_spec(c, algo, (double)count * es, &s))) return rc;
   if (s.kind == AlgoKind::LL && !ll_usable(c, count, es)) s.kind = AlgoKind::ONESHOT;
+  if (s.kind == AlgoKind::DMA && c->nranks > 1) {
+    if (roctx().push) roctx().push(("flexar allreduce dma " + std::to_string(count * es) + "B").c_str());
+    c->calls++;
+    c->bytes += count * es;
+    const char* ip = (const char*)in;
+    char* op_ = (char*)out;
+    rc = run_dma(&c, 1, &ip, &op_, count, dtype, op, fs, st);
+    if (roctx().pop) roctx().pop();
+    return rc;
+  }
+  if (s.kind == AlgoKind::DMA) s.kind = AlgoKind::ONESHOT;  // one rank: the executor's copy
   if (s.kind == AlgoKind::LL) {
     DevCtx x;
     fill_ctx(c, nullptr, in, out, &x);
@@ -568,6 +755,7 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     c->calls++;
     c->bytes += count * es;
     rc = launch_dtype(dtype, op, la);
+    if (!rc) c->launches++;
     if (roctx().pop) roctx().pop();
     return rc;
   }
@@ -598,6 +786,7 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     la.proto = proto_of(s);
     rc = launch_dtype(dtype, op, la);
     if (rc) break;
+    c->launches++;
   }
   if (c->profile) {
     (void)hipEventRecord(ev1, st);
@@ -705,6 +894,19 @@ int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
   if (!d_ctx) FX_HIP(hipMalloc(&d_ctx, sizeof(DevCtx) * kMaxRanks));
   if (specs[0].kind == AlgoKind::LL && !ll_usable(comms[0], count, es))
     for (auto& sp : specs) sp.kind = AlgoKind::ONESHOT;
+  if (specs[0].kind == AlgoKind::DMA && nranks > 1) {
+    std::vector<const char*> ip(nranks);
+    std::vector<char*> op_(nranks);
+    for (int r = 0; r < nranks; ++r) {
+      ip[r] = ins && ins[r] ? (const char*)ins[r] : (const char*)outs[r];
+      op_[r] = (char*)outs[r];
+    }
+    int rc = run_dma(comms, nranks, ip.data(), op_.data(), count, dtype, op, fs, st);
+    if (rc) return rc;
+    FX_HIP(hipStreamSynchronize(st));
+    return 0;
+  }
+  if (specs[0].kind == AlgoKind::DMA) specs[0].kind = AlgoKind::ONESHOT;
   if (specs[0].kind == AlgoKind::LL) {
     std::vector<DevCtx> h(nranks);
     for (int r = 0; r < nranks; ++r) {
@@ -723,6 +925,7 @@ int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
     la.stream = st;
     int rc = launch_dtype(dtype, op, la);
     if (rc) return rc;
+    for (int r = 0; r < nranks; ++r) comms[r]->launches++;
     FX_HIP(hipStreamSynchronize(st));
     return 0;
   }
@@ -759,6 +962,7 @@ int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
     la.proto = proto_of(specs[0]);
     int rc = launch_dtype(dtype, op, la);
     if (rc) return rc;
+    for (int r = 0; r < nranks; ++r) comms[r]->launches++;
     FX_HIP(hipStreamSynchronize(st));  // d_ctx is reused by the next piece
   }
   return 0;
@@ -805,6 +1009,7 @@ int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const vo
   la.proto = proto;
   int rc = launch_dtype(dtype, op, la);
   if (rc) return rc;
+  for (int r = 0; r < nranks; ++r) comms[r]->launches++;
   FX_HIP(hipStreamSynchronize(st));
   return 0;
 }
@@ -845,35 +1050,9 @@ int flexar_reduce(void* dst, const void* const* srcs, int nsrc, size_t count, in
   if (!dst || !srcs || nsrc < 1 || nsrc > 64) { set_error("bad reduce arguments"); return FLEXAR_ERR_INVALID; }
   if (!op_supported(dtype, op)) { set_error("unsupported dtype/op"); return FLEXAR_ERR_UNSUPPORTED; }
   if (count == 0) return 0;
-  const size_t es = dtype_size(dtype);
   float fs = scale * (op == FLEXAR_AVG ? 1.0f / (float)nsrc : 1.0f);
-  hipStream_t st = (hipStream_t)stream;
-  int grid = (int)std::min<uint64_t>(1024, std::max<uint64_t>(1, count * es / (64 * 1024)));
-  // chain groups of kMaxSrc sources through dst (fan-in > 8: dst joins the next group)
-  int done = 0;
-  while (done < nsrc) {
-    SrcTable t;
-    memset(&t, 0, sizeof(t));
-    int k = 0;
-    if (done > 0) t.p[k++] = (const char*)dst;
-    while (k < (int)kMaxSrc && done < nsrc) t.p[k++] = (const char*)srcs[done++];
-    uintptr_t al = (uintptr_t)dst;
-    for (int i = 0; i < k; ++i) al |= (uintptr_t)t.p[i];
-    float sc = done >= nsrc ? fs : 1.0f;
-    LaunchArgs la;
-    la.kind = LAUNCH_REDUCE;
-    la.srcs = t;
-    la.nsrc = k;
-    la.dst = (char*)dst;
-    la.n = (uint64_t)count;
-    la.scale = sc;
-    la.vec = (al & 15) == 0 ? 1 : 0;
-    la.grid = grid;
-    la.stream = st;
-    int rc = launch_dtype(dtype, op, la);
-    if (rc) return rc;
-  }
-  return 0;
+  return reduce_chain((char*)dst, nullptr, (const char* const*)srcs, nsrc, count, dtype, op, fs, (hipStream_t)stream,
+                      PM_FENCE);
 }
 
 }  // extern "C"

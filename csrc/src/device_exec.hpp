@@ -508,21 +508,60 @@ struct SrcTable {
   const char* p[kMaxSrc];
 };
 
-template <typename T, typename OP>
-__global__ void __launch_bounds__(kExecThreads) reduce_kernel(SrcTable srcs, int nsrc, char* dst, uint64_t n,
-                                                              float scale, int vec) {
+// PM_WT (copy-engine allreduce): sources written by peers' DMA are read system-coherently and the
+// result is written through, so a stream-ordered flag write after this kernel publishes it.
+template <typename T, typename OP, int PM>
+__global__ void __launch_bounds__(kExecThreads) reduce_kernel(SrcTable srcs, int nsrc, char* dst, char* dst2,
+                                                              uint64_t n, float scale, int vec) {
   const uint32_t quantum = sizeof(T) >= 16 ? 1u : (uint32_t)(16 / sizeof(T));
   uint64_t lo, hi;
   slice_range(n, blockIdx.x, gridDim.x, quantum, &lo, &hi);
-  if (hi <= lo) return;
-  const char* s[kMaxSrc];
-  char* d[kMaxDst];
+  const uint64_t step = PM == PM_WT ? kWtChunkBytes / sizeof(T) : ~0ull;  // 32-bit buffer offsets
+  for (uint64_t m; lo < hi; lo += m) {
+    m = (hi - lo) < step ? (hi - lo) : step;
+    const char* s[kMaxSrc];
+    char* d[kMaxDst];
 #pragma unroll
-  for (int k = 0; k < kMaxSrc; ++k) s[k] = k < nsrc ? srcs.p[k] + lo * sizeof(T) : nullptr;
+    for (int k = 0; k < kMaxSrc; ++k) s[k] = k < nsrc ? srcs.p[k] + lo * sizeof(T) : nullptr;
 #pragma unroll
-  for (int k = 0; k < kMaxDst; ++k) d[k] = nullptr;
-  d[0] = dst + lo * sizeof(T);
-  xfer_dispatch<T, OP, PM_FENCE>(nsrc, s, d, 1, hi - lo, scale, vec != 0);
+    for (int k = 0; k < kMaxDst; ++k) d[k] = nullptr;
+    d[0] = dst + lo * sizeof(T);
+    if (dst2) d[1] = dst2 + lo * sizeof(T);
+    xfer_dispatch<T, OP, PM>(nsrc, s, d, dst2 ? 2 : 1, m, scale, vec != 0);
+  }
+}
+
+// Copy-engine allreduce: one wave polls up to kMaxRanks flags (system scope) until they reach `value`
+// and then lets the stream proceed (the next copy / reduce is stream-ordered behind this kernel).
+// Same watchdog as the executor's WAIT.
+struct DmaWait {
+  const uint64_t* flags;
+  uint32_t idx[kMaxRanks];
+  uint32_t src[kMaxRanks];
+  uint32_t n;
+  uint32_t slot;
+  uint64_t value;
+  uint64_t timeout_ticks;
+  uint32_t* err;
+};
+static __global__ void dma_wait_kernel(DmaWait w) {
+  const uint32_t t = threadIdx.x;
+  if (t >= w.n) return;
+  uint64_t* f = const_cast<uint64_t*>(w.flags) + w.idx[t];
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (ld_flag(f) < w.value) {
+    __builtin_amdgcn_s_sleep(2);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > w.timeout_ticks) {
+      __hip_atomic_store(w.err, (uint32_t)(0x80000000u | (w.slot << 8) | w.src[t]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+  }
+}
+
+// Copy-engine allreduce bookkeeping: the call consumed one epoch of the staging protocol.
+static __global__ void epoch_set_kernel(uint64_t* epochs, uint64_t e) {
+  for (uint32_t j = threadIdx.x; j < kMaxGridBlocks; j += blockDim.x) epochs[j] = e;
 }
 
 }  // namespace flexar

@@ -31,8 +31,12 @@ inline int launch_one(const LaunchArgs& a) {
                            a.stream, a.d_ctxs, (uint32_t)a.grid);
       break;
     case LAUNCH_REDUCE:
-      hipLaunchKernelGGL((reduce_kernel<T, OP>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.srcs, a.nsrc,
-                         a.dst, a.n, a.scale, a.vec);
+      if (a.proto == PM_WT)
+        hipLaunchKernelGGL((reduce_kernel<T, OP, PM_WT>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.srcs,
+                           a.nsrc, a.dst, a.dst2, a.n, a.scale, a.vec);
+      else
+        hipLaunchKernelGGL((reduce_kernel<T, OP, PM_FENCE>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.srcs,
+                           a.nsrc, a.dst, a.dst2, a.n, a.scale, a.vec);
       break;
     case LAUNCH_LL:
       if (sizeof(T) > 4) return FLEXAR_ERR_UNSUPPORTED;

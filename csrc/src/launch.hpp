@@ -20,6 +20,7 @@ struct LaunchArgs {
   SrcTable srcs;                   // REDUCE
   int nsrc = 0;
   char* dst = nullptr;
+  char* dst2 = nullptr;            // REDUCE: optional second destination
   uint64_t n = 0;
   float scale = 1.0f;
   int vec = 1;

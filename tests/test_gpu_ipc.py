@@ -58,7 +58,7 @@ def _worker(rank, world, port, specs, q):
 def test_ipc_allreduce_processes(cuda, world):
     import torch.multiprocessing as mp
 
-    specs = ["flat", "flat+push", "ring", "ring:2", "oneshot", "flat+wt", "flat+push+wt", "ring+wt"]
+    specs = ["flat", "flat+push", "ring", "ring:2", "oneshot", "flat+wt", "flat+push+wt", "ring+wt", "dma"]
     specs += ["rhd", "tree:2,2+push", "tree:2,2+wt"] if world == 4 else []
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -103,3 +103,11 @@ def test_protocol_modifiers(nv):
         assert body(spec) == body(base)
     with pytest.raises(nv.FlexarError):
         nv.model_cost_us("flat+wtx", 8, 1e6)
+
+
+def test_dma_spec(nv):
+    # copy-engine allreduce: device-only engine, host programs run the same flat exchange
+    assert nv.model_cost_us("dma", 8, 256e6) > 0
+    assert nv.model_cost_us("dma", 8, 4096) > nv.model_cost_us("ll", 8, 4096)
+    body = lambda sp: nv.plan_dump(sp, 2, 8, 1000).split("\n", 1)[1]  # noqa: E731
+    assert body("dma") == body("flat+pull")
