@@ -26,7 +26,8 @@ def run(args):
     dev = torch.device("cuda", 0)
     manifest = []
     for nr in [int(v) for v in args.ranks.split(",")]:
-        g = LocalGroup(nr, workspace_bytes=128 << 20)
+        kibs = [int(v) for v in args.kib.split(",")]
+        g = LocalGroup(nr, workspace_bytes=max(128 << 20, 4 * nr * max(kibs) << 10))  # one piece per call
         for kib in [int(v) for v in args.kib.split(",")]:
             n = kib * 256
             xs = [torch.randn(n, device=dev) for _ in range(nr)]
