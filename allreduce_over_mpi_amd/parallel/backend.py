@@ -115,7 +115,7 @@ class FlexarProcessGroup(dist.ProcessGroup):
 
     def allreduce(self, tensor_list, opts=AllreduceOptions()):
         opname = _redop_name(opts.reduceOp)
-        if not self._flexar_ok(tensor_list, opname):
+        if not self._flexar_ok(tensor_list, opname) or self.algo == "rccl":  # FLEXAR_ALGO=rccl: vendor path
             return self._fallback(tensor_list).allreduce(tensor_list, opts)
         dev = tensor_list[0].device
         comm = self.comm(dev.index)

@@ -74,12 +74,39 @@ class Communicator:
                 allb = b"".join(exchange(bytes(buf.raw)))
                 nv.check(self._lib.flexar_comm_connect(self._h, allb), "comm_connect")
                 exchange(b"connected")
-        if algo:
-            self.set_algo(algo)
+        self._rccl_default = False
+        self._rccl_group = None
+        env_algo = os.environ.get("FLEXAR_ALGO", "")
+        if algo or env_algo == "rccl":
+            self.set_algo(algo or env_algo)
 
     # ------------------------------------------------------------------ config
     def set_algo(self, spec: str):
-        nv.check(self._lib.flexar_comm_set_algo(self._h, spec.encode()), "set_algo")
+        """Default algorithm spec (see README); ``"rccl"`` routes allreduces to RCCL (comparator / fallback)."""
+        self._rccl_default = spec == "rccl"
+        if not self._rccl_default:
+            nv.check(self._lib.flexar_comm_set_algo(self._h, spec.encode()), "set_algo")
+
+    def _rccl_all_reduce(self, tensor, op, out, scale):
+        """FLEXAR_ALGO=rccl: the vendor collective on an RCCL group of the same ranks."""
+        import torch.distributed as dist
+
+        if self._rccl_group is None:
+            if self.group is None and dist.get_backend() == "nccl":
+                self._rccl_group = dist.group.WORLD
+            elif self.group is not None and dist.get_backend(self.group) == "nccl":
+                self._rccl_group = self.group
+            else:
+                self._rccl_group = dist.new_group(ranks=dist.get_process_group_ranks(self.group or dist.group.WORLD),
+                                                  backend="nccl")
+        dst = tensor if out is None else out.copy_(tensor)
+        ops = {"sum": dist.ReduceOp.SUM, "avg": dist.ReduceOp.AVG, "max": dist.ReduceOp.MAX,
+               "min": dist.ReduceOp.MIN, "prod": dist.ReduceOp.PRODUCT, "band": dist.ReduceOp.BAND,
+               "bor": dist.ReduceOp.BOR, "bxor": dist.ReduceOp.BXOR}
+        dist.all_reduce(dst, op=ops[op], group=self._rccl_group)
+        if scale != 1.0:
+            dst.mul_(scale)
+        return dst
 
     def set_grid(self, grid: int):
         nv.check(self._lib.flexar_comm_set_grid(self._h, int(grid), 0), "set_grid")
@@ -104,6 +131,8 @@ class Communicator:
     def all_reduce(self, tensor, op="sum", out=None, algo: Optional[str] = None, scale: float = 1.0, stream=None):
         """Allreduce ``tensor`` (in place unless ``out`` is given). Returns the result tensor."""
         _require_cuda(tensor)
+        if algo == "rccl" or (algo is None and self._rccl_default):
+            return self._rccl_all_reduce(tensor, op, out, scale)
         dst = tensor if out is None else out
         if out is not None:
             _require_cuda(out, "out")

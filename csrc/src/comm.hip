@@ -122,6 +122,8 @@ struct flexar_comm {
   int grid_override = 0;
   int max_grid = 256;
   uint64_t min_block_bytes = 32 * 1024;
+  uint64_t chunk_bytes = 0;  // FLEXAR_CHUNK_BYTES: cap on the bytes of one launch (0 = workspace-bound only)
+  int nchannels = 0;         // FLEXAR_NCHANNELS: channels of a plain "ring" spec (0 = 1)
   uint64_t timeout_ticks = 0;
   uint32_t fi_kind = 0, fi_slot = 0;
   uint64_t fi_ticks = 0;
@@ -150,6 +152,7 @@ static int resolve_spec(flexar_comm* c, const char* algo, double bytes, AlgoSpec
   if (algo && *algo) {
     std::string err;
     if (!parse_algo(algo, c->nranks, &s, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+    if (s.kind == AlgoKind::RING && c->nchannels > 1 && !strchr(algo, ':')) s.channels = c->nchannels;
   }
   if (s.kind == AlgoKind::AUTO) {
     std::string t;
@@ -281,9 +284,12 @@ static int plan_pieces(flexar_comm* c, const AlgoSpec& s, uint64_t count, uint32
   int rc = get_program(c, s, count, esize, fs, &dp, coll, stride);
   if (rc) return rc;
   uint64_t need = dp->prog.stg_elems * esize;
-  if (need <= c->exec_half) { *piece = count; return 0; }
+  const uint64_t bytes = count * esize;
+  const bool chunked = c->chunk_bytes && bytes > c->chunk_bytes;
+  if (need <= c->exec_half && !chunked) { *piece = count; return 0; }
   uint64_t align = std::max<uint64_t>(1, kStageAlignBytes / esize) * (coll == Coll::ALLREDUCE ? c->nranks : 1);
-  uint64_t pieces = (need + c->exec_half - 1) / c->exec_half;
+  uint64_t pieces = std::max<uint64_t>((need + c->exec_half - 1) / c->exec_half,
+                                       chunked ? (bytes + c->chunk_bytes - 1) / c->chunk_bytes : 1);
   for (int tries = 0; tries < 64; ++tries, ++pieces) {
     uint64_t p = (count + pieces - 1) / pieces;
     p = (p + align - 1) / align * align;
@@ -547,6 +553,8 @@ static void init_defaults(flexar_comm* c) {
   if (c->max_grid < 1) c->max_grid = 1;
   if (c->max_grid > (int)kMaxGridBlocks) c->max_grid = kMaxGridBlocks;
   c->min_block_bytes = env_u64("FLEXAR_MIN_BLOCK_BYTES", 32 * 1024);
+  c->chunk_bytes = env_u64("FLEXAR_CHUNK_BYTES", 0);
+  c->nchannels = (int)env_u64("FLEXAR_NCHANNELS", 0);
   c->profile = env_u64("FLEXAR_PROFILE", 0) != 0;
   if (!c->min_block_bytes) c->min_block_bytes = 1;
   // FLEXAR_FAULT_INJECT=delay:RANK:SLOT:MICROSECONDS | drop:RANK:SLOT  (tests / race hunting)
@@ -562,8 +570,9 @@ static void init_defaults(flexar_comm* c) {
   }
   const char* a = getenv("FLEXAR_ALGO");
   std::string err;
-  if (a && *a) {
+  if (a && *a && strcmp(a, "rccl") != 0) {  // "rccl" is routed by the Python layer / c10d backend
     if (!parse_algo(a, c->nranks, &c->spec, &err)) logf(LOG_WARN, c->rank, "ignoring FLEXAR_ALGO: %s", err.c_str());
+    if (c->spec.kind == AlgoKind::RING && c->nchannels > 1 && !strchr(a, ':')) c->spec.channels = c->nchannels;
   } else if (getenv("FT_TOPO")) {  // reference compatibility: FT_TOPO selects the algorithm
     if (!parse_ft_topo(getenv("FT_TOPO"), c->nranks, &c->spec, &err))
       logf(LOG_WARN, c->rank, "ignoring FT_TOPO: %s", err.c_str());

@@ -149,3 +149,36 @@ def test_backend_reduce_scatter_all_gather(cuda):
     for rank, err, used, tb in res:
         assert tb is None, tb
         assert err == 0.0 and used >= 3, (rank, err, used)
+
+
+def test_rccl_algo_routing_single_rank():
+    """algo="rccl" / FLEXAR_ALGO=rccl routes Communicator.all_reduce to RCCL (one rank: RCCL refuses two
+    ranks on one GPU)."""
+    import subprocess
+    import sys
+
+    code = r'''
+import os, torch, torch.distributed as dist
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ["PORT"])
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", rank=0, world_size=1)
+from allreduce_over_mpi_amd.parallel import Communicator
+c = Communicator()
+x = torch.arange(1000, device="cuda", dtype=torch.float32)
+y = torch.empty_like(x)
+c.all_reduce(x, out=y, algo="rccl", scale=0.5)
+assert torch.equal(y, x * 0.5)
+c.set_algo("rccl")
+z = x.clone()
+c.all_reduce(z, op="max")
+assert torch.equal(z, x)
+c.set_algo("flat")
+c.all_reduce(z)
+assert torch.equal(z, x)
+c.close()
+dist.destroy_process_group()
+print("rccl routing ok")
+'''
+    env = dict(os.environ, PORT=str(_port()), PYTHONPATH=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "rccl routing ok" in r.stdout, r.stdout + r.stderr

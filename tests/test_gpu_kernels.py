@@ -243,3 +243,27 @@ def test_group_reduce_scatter_all_gather(cuda, groups, n, spec):
         for o in gath:
             assert torch.equal(o, cat)
     grp.check()
+
+
+def test_chunk_and_channel_knobs(cuda, monkeypatch):
+    """FLEXAR_CHUNK_BYTES splits a call into launches of at most that many bytes; FLEXAR_NCHANNELS sets the
+    channel count of a plain ring spec (both read once, at communicator creation)."""
+    from allreduce_over_mpi_amd.parallel import LocalGroup
+
+    monkeypatch.setenv("FLEXAR_CHUNK_BYTES", str(1 << 20))
+    monkeypatch.setenv("FLEXAR_NCHANNELS", "2")
+    monkeypatch.setenv("FLEXAR_ALGO", "ring")
+    grp = LocalGroup(4, workspace_bytes=32 << 20)
+    try:
+        d = grp.describe(1 << 20, torch.float32)
+        assert d.startswith("ring:2") and "pieces=4" in d, d
+        xs = [torch.randn((1 << 20) + 3, device=cuda) for _ in range(4)]
+        ref = torch.stack([x.double() for x in xs]).sum(0)
+        for spec in (None, "flat", "ring"):
+            outs = grp.all_reduce([x.clone() for x in xs], algo=spec)
+            torch.cuda.synchronize()
+            for o in outs:
+                assert (o.double() - ref).abs().max().item() < 1e-4, spec
+        grp.check()
+    finally:
+        grp.close()
