@@ -64,10 +64,22 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # FLEXAR_BENCH_SHARED_GPU=1: rehearsal of the multi-rank flow with every rank on device 0 (a 1-GPU
+    # box). RCCL refuses two ranks on one GPU, so the reference result and barriers use gloo and the RCCL
+    # comparison is skipped; the numbers measure one shared HBM, not xGMI.
+    shared = os.environ.get("FLEXAR_BENCH_SHARED_GPU", "0") == "1"
+    if shared:
+        local = 0
+        args.no_rccl = True
+        # every rank's workgroups must be co-resident on the one GPU (they spin on each other)
+        os.environ.setdefault("FLEXAR_MAX_GRID", str(max(8, 256 // (2 * world))))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     if args.gpus != world:
         log(rank, f"note: --gpus {args.gpus} but WORLD_SIZE={world}; benchmarking {world} rank(s)")
 
@@ -94,17 +106,22 @@ def main():
     def max_over_ranks(v: float) -> float:
         if world == 1:
             return v
-        t = torch.tensor([v], device=dev, dtype=torch.float64)
+        t = torch.tensor([v], device="cpu" if shared else dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
     # ---------------------------------------------------------------- correctness vs RCCL
     op = args.op
-    if dtype == torch.float8_e4m3fn:  # RCCL reference computed in fp32 from the same fp8 inputs
+    if dtype == torch.float8_e4m3fn and not shared:  # RCCL reference computed in fp32 from the same fp8 inputs
         ref = x.float()
         if world > 1:
             dist.all_reduce(ref)
         ref = (ref / world if op == "avg" else ref).to(dtype)
+    elif shared:  # gloo: reference on the host
+        ref = x.float().cpu()
+        if world > 1:
+            dist.all_reduce(ref)
+        ref = (ref / world if op == "avg" else ref).to(dev).to(dtype)
     else:
         ref = x.clone()
         if world > 1:
@@ -150,13 +167,14 @@ def main():
             failed = 0.0
             try:
                 ok, err = check(spec)
-                okv = max_over_ranks(0.0 if ok else 1.0) == 0.0
-                if not okv:
+                comm.check()  # a watchdog timeout belongs to THIS candidate (its wrong result is a symptom)
+                if max_over_ranks(0.0 if ok else 1.0) != 0.0:
+                    failed = 1.0
                     tune_log[spec] = f"WRONG (max err {err:.3g})"
                     log(rank, f"tuner: {spec} produced wrong results (err {err:.3g}); excluded")
-                    continue
-                t = timed(spec, 3)
-                comm.check()
+                else:
+                    t = timed(spec, 3)
+                    comm.check()
             except nv.FlexarError as e:
                 failed = 1.0
                 tune_log[spec] = f"error: {e}"
@@ -173,10 +191,10 @@ def main():
             if t < best_t:
                 best, best_t = spec, t
         if best is None:
-            raise SystemExit("no flexar algorithm produced correct results")
+            raise SystemExit("no flexar algorithm produced correct results: " + json.dumps(tune_log))
         # grid size for the winner
         best_grid, best_gt = 0, best_t
-        for g in (32, 64, 128):
+        for g in [g for g in (32, 64, 128) if not shared or g <= int(os.environ["FLEXAR_MAX_GRID"])]:
             comm.set_grid(g)
             t = timed(best, 3)
             tune_log[f"{best}@grid{g}"] = round(busbw_gbps(nbytes, t, world), 2)
@@ -244,7 +262,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": round(value / BASELINE_BUSBW_256MIB, 2) if (world > 1 and args.size_mb == 256.0) else None,
         "dtype": {"float32": "fp32", "bfloat16": "bf16", "float16": "fp16", "float8_e4m3fn": "fp8_e4m3"}[args.dtype],
-        "data": "synthetic (torch.randn per rank, seeded); result checked against RCCL before timing",
+        "data": "synthetic (torch.randn per rank, seeded); result checked against RCCL before timing"
+                + ("; REHEARSAL: all ranks share one GPU (gloo reference), not an xGMI measurement" if shared else ""),
         "config": {
             "model": f"allreduce {args.dtype} {args.size_mb:g}MiB buffer per rank"
                      + (" (BASELINE config #2)" if args.dtype == "float32" and args.size_mb == 256 else ""),
