@@ -1,1 +1,1 @@
-from .comm import Communicator, LocalGroup, store_exchange  # noqa: F401
+from .comm import Communicator, LocalGroup, file_exchange, store_exchange  # noqa: F401

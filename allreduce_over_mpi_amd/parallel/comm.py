@@ -191,6 +191,36 @@ def store_exchange(store, rank: int, world_size: int, prefix: str = "flexar"):
     return ex
 
 
+def file_exchange(directory: str, rank: int, world_size: int, prefix: str = "flexar", timeout_s: float = 300.0):
+    """An ``exchange`` callable over a shared directory (no torch.distributed, no MPI): rank r writes
+    ``<prefix>.<round>.<r>`` atomically (write + rename) and polls for every other rank's file.
+    SURVEY.md §7.2 bootstrap option "env + file rendezvous"; the directory must be fresh per job."""
+    import time
+
+    state = {"round": 0}
+    os.makedirs(directory, exist_ok=True)
+
+    def ex(data: bytes):
+        rnd = state["round"]
+        state["round"] += 1
+        path = os.path.join(directory, f"{prefix}.{rnd}.{rank}")
+        with open(path + ".tmp", "wb") as f:
+            f.write(data)
+        os.replace(path + ".tmp", path)
+        out, t0 = [], time.monotonic()
+        for r in range(world_size):
+            p = os.path.join(directory, f"{prefix}.{rnd}.{r}")
+            while not os.path.exists(p):
+                if time.monotonic() - t0 > timeout_s:
+                    raise TimeoutError(f"file rendezvous: rank {r} never wrote {p}")
+                time.sleep(0.005)
+            with open(p, "rb") as f:
+                out.append(f.read())
+        return out
+
+    return ex
+
+
 class LocalGroup:
     """``nranks`` flexar ranks on one GPU in one process (single-launch group execution)."""
 

@@ -15,11 +15,14 @@
 
 #include <stdint.h>
 
+#include <algorithm>
 #include <cctype>
 #include <cstdlib>
 #include <sstream>
 #include <string>
 #include <vector>
+
+#include "flexar/program.hpp"
 
 namespace flexar {
 
@@ -240,7 +243,12 @@ inline std::vector<int> ring_steps(int nranks) {
     if (gcd_int(d, nranks) == 1) steps.push_back(d);
   return steps;
 }
-inline int max_ring_channels(int nranks) { int n = (int)ring_steps(nranks).size(); return n < 1 ? 1 : n; }
+// arc-disjoint rings available, capped by the flag-slot budget (2 (N-1) slots per channel)
+inline int max_ring_channels(int nranks) {
+  int n = (int)ring_steps(nranks).size();
+  if (nranks > 1) n = std::min(n, (int)kProgSlots / (2 * (nranks - 1)));
+  return n < 1 ? 1 : n;
+}
 // order[c][pos] = rank at position pos of ring c
 inline std::vector<int> ring_order(int nranks, int channel) {
   std::vector<int> st = ring_steps(nranks);

@@ -59,3 +59,30 @@ def test_flexar_backend_cpu_world2():
         assert x == [float(i * 3) for i in range(10)]
         assert y == 2 and b == 7.0
         assert outs == [[0.0, 0.0], [1.0, 1.0]]
+
+
+def _fx_worker(d, rank, world, q):
+    from allreduce_over_mpi_amd.parallel import file_exchange
+
+    ex = file_exchange(d, rank, world)
+    a = ex(f"hello{rank}".encode())
+    b = ex(bytes([rank]) * (rank + 1))
+    q.put((rank, a, b))
+
+
+def test_file_exchange_rendezvous(tmp_path):
+    """File-based bootstrap exchange: two all-gather rounds across 3 processes."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_fx_worker, args=(str(tmp_path), r, 3, q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    res = dict((r, (a, b)) for r, a, b in (q.get(timeout=60) for _ in ps))
+    for p in ps:
+        p.join(30)
+    for r in range(3):
+        a, b = res[r]
+        assert a == [b"hello0", b"hello1", b"hello2"]
+        assert b == [b"\x00", b"\x01\x01", b"\x02\x02\x02"]

@@ -111,3 +111,34 @@ def test_dma_spec(nv):
     assert nv.model_cost_us("dma", 8, 4096) > nv.model_cost_us("ll", 8, 4096)
     body = lambda sp: nv.plan_dump(sp, 2, 8, 1000).split("\n", 1)[1]  # noqa: E731
     assert body("dma") == body("flat+pull")
+
+
+def _remote_elems(dump, rank):
+    """Elements a rank's program moves over links: every XFER operand in another rank's staging."""
+    import re
+
+    total = 0
+    for line in dump.splitlines():
+        m = re.match(r"\s+XFER len=(\d+) \[(.*)\] -> \[(.*)\]", line)
+        if not m:
+            continue
+        locs = m.group(2).split(" + ") + m.group(3).split(", ")
+        remote = sum(1 for loc in locs if loc.startswith("STG@") and int(loc[4:].split(":")[0]) != rank)
+        total += int(m.group(1)) * remote
+    return total
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 6, 8, 12, 16])
+def test_plans_move_bandwidth_optimal_bytes(nv, n):
+    """every tree/ring/flat schedule moves 2(N-1)/N * S per rank (the reference's
+    'key structural fact'); oneshot moves (N-1) * S. Checked on the compiled programs of every rank."""
+    count = 4096 * n
+    specs = [p for p in nv.enumerate_plans(n) if p.startswith(("tree:", "ring"))]
+    specs = [s for s in specs if not s.startswith("tree:") or
+             __import__("math").prod(int(w) for w in s[5:].split(",")) == n]  # lonely trees fold extra data
+    specs += [s + "+push" for s in specs if s.startswith("tree:")] + ["flat", "oneshot"]
+    for spec in specs:
+        want = (n - 1) * count if spec == "oneshot" else 2 * (n - 1) * count / n
+        for r in range(n):
+            got = _remote_elems(nv.plan_dump(spec, r, n, count), r)
+            assert abs(got - want) <= 0.01 * want, (spec, n, r, got, want)
