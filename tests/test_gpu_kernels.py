@@ -119,7 +119,7 @@ def test_group_allreduce_dtypes(cuda, groups, dtype):
     else:
         xs = [torch.randn(300007, device=cuda, generator=g).to(dtype) for _ in range(n)]
     ref = torch.stack([x.double() for x in xs]).sum(0)
-    for spec in ("flat", "ring:4", "rhd", "tree:2,4+push", "oneshot"):
+    for spec in ("flat", "ring:4", "rhd", "tree:2,4+push", "oneshot", "flat+wt", "ring:2+wt", "dma"):
         outs = grp.all_reduce([x.clone() for x in xs], "sum", algo=spec)
         torch.cuda.synchronize()
         for o in outs:
@@ -153,11 +153,34 @@ def test_group_avg_and_fp8(cuda, groups):
         torch.testing.assert_close(o, ref, rtol=1e-5, atol=1e-6)
     # fp8 e4m3 gradient allreduce with fused 1/N post-scale (BASELINE config #5)
     x8 = [(x * 8).to(torch.float8_e4m3fn) for x in xs]
-    outs = grp.all_reduce([x.clone() for x in x8], "avg", algo="flat")
     exact = (torch.stack([x.float() for x in x8]).sum(0) / n)
+    for spec in ("flat", "flat+wt", "dma"):  # one fp32-accumulated reduction stage each
+        outs = grp.all_reduce([x.clone() for x in x8], "avg", algo=spec)
+        for o in outs:
+            assert torch.equal(o.view(torch.uint8), exact.to(torch.float8_e4m3fn).view(torch.uint8)) or \
+                (o.float() - exact).abs().max().item() <= 0.0625 * exact.abs().max().item(), spec
+    outs = grp.all_reduce([x.clone() for x in xs], "avg", algo="dma")
     for o in outs:
-        assert torch.equal(o.view(torch.uint8), exact.to(torch.float8_e4m3fn).view(torch.uint8)) or \
-            (o.float() - exact).abs().max().item() <= 0.0625 * exact.abs().max().item()
+        torch.testing.assert_close(o, ref, rtol=1e-5, atol=1e-6)
+
+
+def test_group_mixed_engines_sequence(cuda, groups):
+    """Executor, LL and copy-engine calls share one staging/epoch protocol: any interleaving (including
+    sizes that split into pieces) must stay correct on both parities."""
+    n = 4
+    grp = groups[n]
+    g = torch.Generator(device=cuda).manual_seed(31)
+    seq = ["dma", "ll", "flat", "dma", "dma", "ring+wt", "oneshot", "dma", "flat+wt", "ll", "ll", "dma",
+           "tree:2,2+push", "dma"]
+    for it, spec in enumerate(seq):
+        size = [1000, 65539, 300007, (1 << 22) + 3][it % 4]
+        xs = [torch.randn(size, device=cuda, generator=g) for _ in range(n)]
+        ref = torch.stack([x.double() for x in xs]).sum(0)
+        outs = grp.all_reduce([x.clone() for x in xs], algo=spec)
+        torch.cuda.synchronize()
+        for o in outs:
+            assert (o.double() - ref).abs().max().item() < 1e-4, (it, spec, size)
+    grp.check()
 
 
 def test_communicator_single_rank(cuda):
