@@ -65,15 +65,19 @@ class Communicator:
             buf = ctypes.create_string_buffer(hs)
             nv.check(self._lib.flexar_comm_export(self._h, buf), "comm_export")
             if exchange is None:
-                gathered = [None] * self.world_size
-                dist.all_gather_object(gathered, bytes(buf.raw), group=group)
-                allb = b"".join(gathered)
-                nv.check(self._lib.flexar_comm_connect(self._h, allb), "comm_connect")
-                dist.barrier(group=group)  # everyone has mapped everyone before the first collective
-            else:
-                allb = b"".join(exchange(bytes(buf.raw)))
-                nv.check(self._lib.flexar_comm_connect(self._h, allb), "comm_connect")
-                exchange(b"connected")
+                def exchange(data: bytes):
+                    gathered = [None] * self.world_size
+                    dist.all_gather_object(gathered, data, group=group)
+                    return gathered
+            allb = b"".join(exchange(bytes(buf.raw)))
+            rc = self._lib.flexar_comm_connect(self._h, allb)
+            # agreement round (also the barrier: everyone has mapped everyone before the first collective);
+            # a rank that failed to map a peer must not leave the others waiting in a later collective
+            msg = b"" if rc == 0 else f"rank {self.rank}: {nv.last_error()}".encode()
+            bad = [m.decode(errors="replace") for m in exchange(msg) if m]
+            if bad:
+                self.close()
+                raise nv.FlexarError(rc or 5, "comm_connect: " + "; ".join(bad))
         self._rccl_default = False
         self._rccl_group = None
         env_algo = os.environ.get("FLEXAR_ALGO", "")

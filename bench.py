@@ -1,22 +1,28 @@
 #!/usr/bin/env python3
 """Flagship benchmark: allreduce bus bandwidth on N MI355X GPUs (one rank per GPU).
 
-Metric and config are BASELINE.json's: "allreduce bus bandwidth (GB/s) vs buffer
-bytes, fp32/bf16, at 1/2/4/8 MI355X", headline buffer = config #2 (fp32,
-256 MiB). The reference's own driver (allreduce_over_mpi/benchmark.cpp:147-215)
-times MPI_Allreduce_FT with MPI_Barrier + MPI_Wtime on rank 0 only; here every
-rank is timed over K steps bracketed by barrier + device synchronize on both
-sides and the MAX over ranks is reported.
+Metric and config are BASELINE.json's: "allreduce bus bandwidth (GB/s) vs buffer bytes, fp32/bf16, at
+1/2/4/8 MI355X", headline buffer = config #2 (fp32, 256 MiB). The reference's own driver
+(allreduce_over_mpi/benchmark.cpp:147-215) times MPI_Allreduce_FT with MPI_Barrier + MPI_Wtime on rank 0
+only; here every rank is timed over K steps bracketed by barrier + device synchronize on both sides and
+the MAX over ranks is reported.
 
     python bench.py --gpus 1 --steps 20 --warmup 5
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
         --master-addr 127.0.0.1 --master-port 29500 bench.py --gpus 8
 
-busbw = (bytes / t) * 2 (N - 1) / N (rccl-tests convention). For N = 1 the
-factor is 0 (no inter-GPU traffic), so the N = 1 line reports algbw of the
-out-of-place allreduce (a device copy through the flexar kernel) and says so.
-Data: synthetic torch.randn buffers seeded per rank. Every run first checks the
-flexar result against RCCL's (torch.distributed "nccl") on the same inputs.
+Numbers (rccl-tests convention): algbw = bytes / t and per-rank busbw = algbw * 2 (N - 1) / N.
+`value` is the whole-job aggregate: the per-rank busbw summed over the N ranks; `busbw_GBps` is the
+per-rank figure rccl-tests prints and `vs_baseline` compares that per-rank figure with the reference's
+per-rank busbw. For N = 1 the busbw factor is 0 (no inter-GPU traffic), so the N = 1 line reports the
+algbw of the out-of-place allreduce (a device copy through the flexar kernel) and says so.
+
+Correctness: every tuner candidate and the final choice are checked against RCCL's result
+(torch.distributed "nccl") on three consecutive calls whose inputs are scaled by 1, 1/2 and 1/4 (exact
+in every dtype). Calls alternate staging halves, so a read of a staging line left over from one of the
+two previous calls changes the result and is caught. The check runs again after the timed region.
+Data: synthetic torch.randn buffers seeded per rank. If no flexar algorithm is correct on this node the
+run falls back to RCCL and says so in `config.algorithm` and `fallback`.
 """
 from __future__ import annotations
 
@@ -30,14 +36,39 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-# the reference (FlexTree ring, FT_TOPO=1) at N=2, 256 MiB fp32 = 3.15 GB/s busbw
+# the reference (FlexTree ring, FT_TOPO=1) at N=2, 256 MiB fp32 = 3.15 GB/s busbw per rank
 # (measured locally on CPU/MPICH — the reference publishes no numbers).
 BASELINE_BUSBW_256MIB = 3.15
+CHECK_SCALES = (1.0, 0.5, 0.25)  # powers of two: exact scaling of inputs and of the reference sum
 
 
 def log(rank, *a):
     if rank == 0:
         print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+class RcclOnly:
+    """Stand-in communicator when flexar cannot run on this node: every call is RCCL's allreduce."""
+
+    def __init__(self, dist):
+        self.dist = dist
+
+    def all_reduce(self, tensor, op="sum", out=None, algo=None, scale=1.0):
+        dst = tensor if out is None else out.copy_(tensor)
+        self.dist.all_reduce(dst, op=self.dist.ReduceOp.AVG if op == "avg" else self.dist.ReduceOp.SUM)
+        return dst
+
+    def check(self):
+        pass
+
+    def set_grid(self, g):
+        pass
+
+    def describe(self, count, dtype):
+        return "rccl"
+
+    def close(self):
+        pass
 
 
 def main():
@@ -83,6 +114,7 @@ def main():
     if args.gpus != world:
         log(rank, f"note: --gpus {args.gpus} but WORLD_SIZE={world}; benchmarking {world} rank(s)")
 
+    from allreduce_over_mpi_amd import _native as nv
     from allreduce_over_mpi_amd.parallel.comm import Communicator
     from allreduce_over_mpi_amd.utils.perf import algbw_gbps, busbw_gbps
 
@@ -93,8 +125,23 @@ def main():
     nbytes = count * esize
 
     os.environ.setdefault("FLEXAR_TIMEOUT_MS", "5000")  # a broken candidate costs seconds, not minutes
-    ws_bytes = max(512 << 20, 2 * nbytes + (64 << 20))
-    comm = Communicator(workspace_bytes=ws_bytes)
+    # staging for one whole call (flat pull: N landing blocks + N published blocks per parity half), so a
+    # 256 MiB allreduce is ONE launch; 288 GB of HBM makes 1 GiB of workspace per rank free
+    ws_bytes = max(512 << 20, 4 * nbytes + (64 << 20))
+    fallback = None
+
+    def make_comm():
+        try:
+            return Communicator(workspace_bytes=ws_bytes)
+        except nv.FlexarError as e:
+            if world == 1 or shared:
+                raise
+            log(rank, f"flexar communicator unavailable on this node ({e}); measuring RCCL instead")
+            return None
+
+    comm = make_comm()
+    if comm is None:
+        comm, fallback = RcclOnly(dist), "flexar communicator could not be created"
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
     x = torch.randn(count, device=dev, dtype=torch.float32, generator=gen)
@@ -102,6 +149,7 @@ def main():
         x = x * 8  # fp8 e4m3 range: |x| <= 448
     x = x.to(dtype)
     y = torch.empty_like(x)
+    xs = torch.empty_like(x)  # scaled copies of x for the stale-staging check
 
     def max_over_ranks(v: float) -> float:
         if world == 1:
@@ -126,16 +174,25 @@ def main():
         ref = x.clone()
         if world > 1:
             dist.all_reduce(ref, op=dist.ReduceOp.AVG if op == "avg" else dist.ReduceOp.SUM)
+    ref_f = ref.float()
+    ref_max = float(ref_f.abs().max().item()) + 1e-6
     tol = {torch.float32: 1e-5, torch.bfloat16: 2e-2, torch.float16: 4e-3, torch.float8_e4m3fn: 0.13}[dtype]
     tol = tol * math.sqrt(world) * 4 if dtype != torch.float8_e4m3fn else tol
 
     def check(spec):
-        comm.all_reduce(x, out=y, op=op, algo=None if spec == "auto" else spec)
-        torch.cuda.synchronize()
-        err = float((y.float() - ref.float()).abs().max().item())
-        scale = float(ref.float().abs().max().item()) + 1e-6
-        ok = err <= tol * scale
-        return ok, err
+        """Three consecutive calls with inputs x, x/2, x/4: every result must match the reference scaled
+        the same way (a stale staging line from either of the two previous calls would be off by 2x/4x)."""
+        worst = 0.0
+        for s in CHECK_SCALES:
+            src = x
+            if s != 1.0:
+                xs.copy_((x.float() * s).to(dtype))
+                src = xs
+            comm.all_reduce(src, out=y, op=op, algo=None if spec == "auto" else spec)
+            torch.cuda.synchronize()
+            err = float((y.float() - ref_f * s).abs().max().item()) / (ref_max * s)
+            worst = max(worst, err)
+        return worst <= tol, worst
 
     def timed(spec, iters, warm=1):
         a = None if spec == "auto" else spec
@@ -153,16 +210,18 @@ def main():
     # ---------------------------------------------------------------- start-up tuner
     algo = args.algo
     tune_log = {}
-    if world > 1 and algo == "auto" and not args.no_tune:
-        from allreduce_over_mpi_amd import _native as nv
-
+    if fallback:
+        algo = "rccl"
+    elif world > 1 and algo == "auto" and not args.no_tune:
         cands = ["flat+pull", "flat+push", "flat+pull+nts", "flat+push+nts", "flat+pull+wt", "flat+push+wt"]
         maxc = len([d for d in range(1, world) if math.gcd(d, world) == 1])
         cands += ["ring", "ring+wt"] + [f"ring:{c}{m}" for c in (2, 4, 8) if c <= maxc for m in ("", "+wt")]
         if world > 2 and (world & (world - 1)) == 0:
             cands += ["rhd+pull"]
+        if world >= 8 and world % 4 == 0:  # two-stage FlexTree factorizations (3 + 1 / 1 + 3 links per stage)
+            cands += [f"tree:4,{world // 4}+pull", f"tree:{world // 4},4+pull"]
         cands += ["dma"]  # copy engines (CU-free)
-        best, best_t = None, float("inf")
+        timings = {}
         for spec in cands:
             failed = 0.0
             try:
@@ -170,8 +229,8 @@ def main():
                 comm.check()  # a watchdog timeout belongs to THIS candidate (its wrong result is a symptom)
                 if max_over_ranks(0.0 if ok else 1.0) != 0.0:
                     failed = 1.0
-                    tune_log[spec] = f"WRONG (max err {err:.3g})"
-                    log(rank, f"tuner: {spec} produced wrong results (err {err:.3g}); excluded")
+                    tune_log[spec] = f"WRONG (max rel err {err:.3g})"
+                    log(rank, f"tuner: {spec} produced wrong results (rel err {err:.3g}); excluded")
                 else:
                     t = timed(spec, 3)
                     comm.check()
@@ -184,34 +243,47 @@ def main():
                 tune_log.setdefault(spec, "failed on a peer")
                 comm.close()
                 torch.cuda.synchronize()
-                comm = Communicator(workspace_bytes=ws_bytes)
+                comm = make_comm() or RcclOnly(dist)
+                if isinstance(comm, RcclOnly):
+                    fallback = "flexar communicator could not be rebuilt"
+                    break
                 continue
+            timings[spec] = t
             tune_log[spec] = round(busbw_gbps(nbytes, t, world), 2)
-            log(rank, f"tuner: {spec:12s} {t*1e3:8.3f} ms  busbw {busbw_gbps(nbytes, t, world):8.1f} GB/s")
-            if t < best_t:
-                best, best_t = spec, t
-        if best is None:
-            raise SystemExit("no flexar algorithm produced correct results: " + json.dumps(tune_log))
-        # grid size for the winner
-        best_grid, best_gt = 0, best_t
-        for g in [g for g in (32, 64, 128) if not shared or g <= int(os.environ["FLEXAR_MAX_GRID"])]:
-            comm.set_grid(g)
-            t = timed(best, 3)
-            tune_log[f"{best}@grid{g}"] = round(busbw_gbps(nbytes, t, world), 2)
-            if t < best_gt:
-                best_grid, best_gt = g, t
-        comm.set_grid(best_grid)
-        algo = best
-        log(rank, f"tuner: selected {algo} grid={best_grid or 'auto'}")
-        if rank == 0 and args.tune_out:
-            with open(args.tune_out, "a") as f:  # "nranks bytes spec" (cost_model.hpp TuneTable)
-                f.write(f"{world} {nbytes} {algo}\n")
+            log(rank, f"tuner: {spec:14s} {t*1e3:8.3f} ms  busbw {busbw_gbps(nbytes, t, world):8.1f} GB/s")
+        if not timings or fallback:
+            fallback = fallback or "no flexar algorithm produced correct results on this node"
+            log(rank, f"tuner: {fallback}; measuring RCCL instead")
+            algo = "rccl"
+            if not isinstance(comm, RcclOnly):
+                comm.close()
+                comm = RcclOnly(dist)
+        else:
+            # workgroup count for the two fastest schedules: remote (xGMI) loads/stores are latency bound
+            # per wave, so more workgroups can pay; 512 = 2 per CU, still co-resident
+            grids = [g for g in (64, 128, 512) if not shared or g <= int(os.environ["FLEXAR_MAX_GRID"])]
+            best, best_grid, best_t = None, 0, float("inf")
+            for spec in sorted(timings, key=timings.get)[:2]:
+                if timings[spec] < best_t:
+                    best, best_grid, best_t = spec, 0, timings[spec]
+                for g in grids:
+                    comm.set_grid(g)
+                    t = timed(spec, 3)
+                    tune_log[f"{spec}@grid{g}"] = round(busbw_gbps(nbytes, t, world), 2)
+                    if t < best_t:
+                        best, best_grid, best_t = spec, g, t
+            comm.set_grid(best_grid)
+            algo = best
+            log(rank, f"tuner: selected {algo} grid={best_grid or 'auto'}")
+            if rank == 0 and args.tune_out:
+                with open(args.tune_out, "a") as f:  # "nranks bytes spec" (cost_model.hpp TuneTable)
+                    f.write(f"{world} {nbytes} {algo}\n")
 
     ok, err = check(algo)
     if max_over_ranks(0.0 if ok else 1.0) != 0.0:
-        raise SystemExit(f"flexar result mismatch vs RCCL (max err {err:.3g})")
+        raise SystemExit(f"{algo} result mismatch vs RCCL (max rel err {err:.3g})")
     desc = comm.describe(count, dtype) if algo == "auto" else algo
-    log(rank, f"correctness vs {'RCCL' if world > 1 else 'input'}: max err {err:.3g} (ok); running {desc}")
+    log(rank, f"correctness vs {'RCCL' if world > 1 else 'input'}: max rel err {err:.3g} (ok); running {desc}")
 
     # ---------------------------------------------------------------- timed region
     a = None if algo == "auto" else algo
@@ -231,6 +303,10 @@ def main():
     elapsed = max_over_ranks(time.perf_counter() - t0)
     comm.check()
     t_step = elapsed / max(1, args.steps)
+    # the timed calls must have produced correct results too (checked again right after, same protocol state)
+    ok, err_after = check(algo)
+    if max_over_ranks(0.0 if ok else 1.0) != 0.0:
+        raise SystemExit(f"{algo} result mismatch vs RCCL after the timed run (max rel err {err_after:.3g})")
 
     rccl_busbw = None
     if world > 1 and not args.no_rccl and dtype != torch.float8_e4m3fn:
@@ -249,7 +325,7 @@ def main():
 
     algbw = algbw_gbps(nbytes, t_step)
     busbw = busbw_gbps(nbytes, t_step, world)
-    value = busbw if world > 1 else algbw
+    value = busbw * world if world > 1 else algbw
     out = {
         "metric": "allreduce bus bandwidth (GB/s)",
         "value": round(value, 2),
@@ -260,9 +336,9 @@ def main():
         "ms_per_step": round(t_step * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(value / BASELINE_BUSBW_256MIB, 2) if (world > 1 and args.size_mb == 256.0) else None,
+        "vs_baseline": round(busbw / BASELINE_BUSBW_256MIB, 2) if (world > 1 and args.size_mb == 256.0) else None,
         "dtype": {"float32": "fp32", "bfloat16": "bf16", "float16": "fp16", "float8_e4m3fn": "fp8_e4m3"}[args.dtype],
-        "data": "synthetic (torch.randn per rank, seeded); result checked against RCCL before timing"
+        "data": "synthetic (torch.randn per rank, seeded); results checked against RCCL before and after timing"
                 + ("; REHEARSAL: all ranks share one GPU (gloo reference), not an xGMI measurement" if shared else ""),
         "config": {
             "model": f"allreduce {args.dtype} {args.size_mb:g}MiB buffer per rank"
@@ -273,10 +349,13 @@ def main():
             "parallelism": f"dp{world}",
             "algorithm": desc,
         },
+        "value_definition": ("per-rank busbw (rccl-tests: algbw * 2(N-1)/N) summed over the N ranks" if world > 1
+                             else "algbw of the out-of-place allreduce (N=1: the busbw factor 2(N-1)/N is 0)"),
         "busbw_GBps": round(busbw, 2),
         "algbw_GBps": round(algbw, 2),
         "aggregate_busbw_GBps": round(busbw * world, 2),
         "rccl_busbw_GBps": rccl_busbw,
+        "fallback": fallback,
         "tuner": tune_log or None,
     }
     if args.sweep:

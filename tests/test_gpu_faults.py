@@ -28,6 +28,32 @@ def test_delayed_peer_is_still_correct(cuda, monkeypatch):
         g.close()
 
 
+def test_consecutive_calls_never_read_stale_staging(cuda, monkeypatch):
+    """The hand-off test the CDNA guide asks for (Guideline 16): uneven load and inputs that change every
+    call. Calls alternate staging halves, so a consumer that read a line left over from the previous call
+    or from the one before (same half) would return a result scaled by 2x or 4x. Rank 2 signals late."""
+    from allreduce_over_mpi_amd.parallel import LocalGroup
+
+    monkeypatch.setenv("FLEXAR_FAULT_INJECT", "delay:2:0:300")
+    g = LocalGroup(4, workspace_bytes=32 << 20)
+    try:
+        gen = torch.Generator(device=cuda).manual_seed(77)
+        base = [torch.randn(200003, device=cuda, generator=gen) for _ in range(4)]
+        ref = torch.stack([b.double() for b in base]).sum(0)
+        for spec in ("flat", "flat+push", "flat+wt", "flat+push+nts", "ring", "ring:2+wt", "rhd", "tree:2,2+push",
+                     "oneshot", "ll", "dma"):
+            for it in range(6):
+                s = 2.0 ** -(it % 3)
+                outs = g.all_reduce([b * s for b in base], algo=spec)
+                torch.cuda.synchronize()
+                for r, o in enumerate(outs):
+                    err = (o.double() - ref * s).abs().max().item()
+                    assert err < 1e-4, (spec, it, r, err)
+        g.check()
+    finally:
+        g.close()
+
+
 def test_dropped_signal_times_out(cuda, monkeypatch):
     from allreduce_over_mpi_amd import FlexarError
     from allreduce_over_mpi_amd.parallel import LocalGroup

@@ -1,0 +1,99 @@
+"""One process per GPU (the production topology): every rank on its own device, workspaces mapped
+across devices through HIP IPC over xGMI, bootstrap through torch.distributed (gloo).
+
+A 1-GPU box skips this module (tests/test_gpu_ipc.py covers the same protocol with every process on
+device 0). On a multi-GPU node it checks every algorithm family against a float64 host reference on
+fp32/bf16, uneven tail sizes, SUM and the fused AVG post-scale, with inputs that change every call
+(x, x/2, x/4 on alternating staging parities) so a stale staging line cannot go unnoticed.
+"""
+import os
+import socket
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ngpu() -> int:
+    try:
+        return torch.cuda.device_count()
+    except Exception:
+        return 0
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, specs, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_TIMEOUT_MS="20000")
+        import torch.distributed as dist
+
+        torch.cuda.set_device(rank)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from allreduce_over_mpi_amd.parallel import Communicator
+
+        comm = Communicator(workspace_bytes=128 << 20)
+        dev = torch.device("cuda", rank)
+        results = {}
+        for spec in specs:
+            for dtype in (torch.float32, torch.bfloat16):
+                for size in (5, 4096, 1000003):
+                    xs = [torch.randn(size, generator=torch.Generator().manual_seed(100 * r + size)).to(dtype)
+                          for r in range(world)]
+                    ref = torch.stack([x.double() for x in xs]).sum(0)
+                    for op in ("sum", "avg"):
+                        worst = 0.0
+                        for s in (1.0, 0.5, 0.25):
+                            x = (xs[rank].double() * s).to(dtype).to(dev)
+                            y = comm.all_reduce(x, op=op, algo=spec)
+                            torch.cuda.synchronize()
+                            want = ref * s / (world if op == "avg" else 1)
+                            err = ((y.double().cpu() - want).abs().max() / (want.abs().max() + 1e-12)).item()
+                            worst = max(worst, err)
+                        results[(spec, str(dtype), size, op)] = worst
+        comm.check()
+        comm.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, results, None))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.skipif(_ngpu() < 2, reason="needs >= 2 GPUs (one process per device)")
+def test_allreduce_one_process_per_gpu(cuda):
+    import torch.multiprocessing as mp
+
+    world = min(_ngpu(), 8)
+    specs = ["flat", "flat+push", "flat+wt", "ring", "ring+wt", "oneshot", "ll", "dma"]
+    if world > 2:
+        specs.append("ring:2")
+    if world >= 4 and (world & (world - 1)) == 0:
+        specs.append("rhd")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, specs, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        rank, res, err = q.get(timeout=600)
+        assert err is None, f"rank {rank} failed:\n{err}"
+        out[rank] = res
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, res in out.items():
+        for key, err in res.items():
+            tol = 1e-5 if "float32" in key[1] else 2e-2
+            assert err < tol, (rank, key, err)
