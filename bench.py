@@ -259,9 +259,10 @@ def main():
                 comm.close()
                 comm = RcclOnly(dist)
         else:
-            # workgroup count for the two fastest schedules: remote (xGMI) loads/stores are latency bound
-            # per wave, so more workgroups can pay; 512 = 2 per CU, still co-resident
-            grids = [g for g in (64, 128, 512) if not shared or g <= int(os.environ["FLEXAR_MAX_GRID"])]
+            # workgroup count for the two fastest schedules (auto = one per 32 KiB, at most 256 = one per CU;
+            # the executor needs 141 VGPRs, so 512-thread workgroups are resident one per CU and larger grids
+            # would not be co-resident)
+            grids = [g for g in (32, 64, 128) if not shared or g <= int(os.environ["FLEXAR_MAX_GRID"])]
             best, best_grid, best_t = None, 0, float("inf")
             for spec in sorted(timings, key=timings.get)[:2]:
                 if timings[spec] < best_t:
