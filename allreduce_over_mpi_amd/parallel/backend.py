@@ -171,6 +171,17 @@ class FlexarProcessGroup(dist.ProcessGroup):
         return self._fallback(tensor_list).broadcast(tensor_list, opts)
 
     def allgather(self, output_tensors, input_tensor, opts=AllgatherOptions()):
+        """List form (``dist.all_gather``): flexar all-gather into one packed buffer, then unpacked."""
+        if len(input_tensor) == 1 and len(output_tensors) == 1 and len(output_tensors[0]) == self._world:
+            inp, outs = input_tensor[0], output_tensors[0]
+            if all(o.numel() == inp.numel() and o.dtype == inp.dtype and o.device == inp.device for o in outs) \
+                    and self._flexar_ok([inp] + list(outs), "sum") and inp.dtype != torch.bool:
+                def run(c):
+                    flat = torch.empty(inp.numel() * self._world, dtype=inp.dtype, device=inp.device)
+                    c.all_gather(inp.contiguous().reshape(-1), flat)
+                    for r, o in enumerate(outs):
+                        o.copy_(flat[r * inp.numel():(r + 1) * inp.numel()].view_as(o))
+                return self._on_side([inp] + list(outs), run, output_tensors)
         return self._fallback(input_tensor).allgather(output_tensors, input_tensor, opts)
 
     def _allgather_base(self, output_tensor, input_tensor, opts=AllgatherOptions()):
@@ -180,10 +191,41 @@ class FlexarProcessGroup(dist.ProcessGroup):
                                  [output_tensor])
         return self._fallback([input_tensor])._allgather_base(output_tensor, input_tensor, opts)
 
+    def _ag_ok(self, inp, out):
+        return self._flexar_ok([inp, out], "sum") and inp.dtype != torch.bool and out.dtype == inp.dtype and \
+            out.numel() == inp.numel() * self._world
+
+    def _rs_ok(self, out, inp, opname):
+        return self._flexar_ok([inp, out], opname) and inp.dtype != torch.bool and out.dtype == inp.dtype and \
+            inp.numel() == out.numel() * self._world
+
     def allgather_into_tensor_coalesced(self, output_tensors, input_tensors, opts=AllgatherOptions()):
-        return self._fallback(input_tensors).allgather_into_tensor_coalesced(output_tensors, input_tensors, opts)
+        """FSDP2's all-gather of many parameter shards: one flexar all-gather per pair, all on the side stream."""
+        if not all(self._ag_ok(i, o) for i, o in zip(input_tensors, output_tensors)):
+            return self._fallback(input_tensors).allgather_into_tensor_coalesced(output_tensors, input_tensors, opts)
+
+        def run(c):
+            for i, o in zip(input_tensors, output_tensors):
+                c.all_gather(i, o)
+        return self._on_side(list(input_tensors) + list(output_tensors), run, list(output_tensors))
+
+    def allgather_coalesced(self, output_lists, input_tensors, opts=AllgatherOptions()):
+        return self._fallback(input_tensors).allgather_coalesced(output_lists, input_tensors, opts)
 
     def reduce_scatter(self, output_tensors, input_tensors, opts=ReduceScatterOptions()):
+        """List form (``dist.reduce_scatter``): the N input chunks are packed into one buffer, reduced by the
+        flexar reduce-scatter, and the rank's block lands in ``output_tensors[0]``."""
+        opname = _redop_name(opts.reduceOp)
+        if len(output_tensors) == 1 and len(input_tensors) == 1 and len(input_tensors[0]) == self._world:
+            out, chunks = output_tensors[0], input_tensors[0]
+            if all(c.numel() == out.numel() and c.dtype == out.dtype and c.device == out.device for c in chunks) \
+                    and self._flexar_ok([out] + list(chunks), opname) and out.dtype != torch.bool:
+                def run(c):
+                    flat = torch.cat([t.reshape(-1) for t in chunks])
+                    res = torch.empty(out.numel(), dtype=out.dtype, device=out.device)
+                    c.reduce_scatter(flat, res, op=opname)
+                    out.copy_(res.view_as(out))
+                return self._on_side([out] + list(chunks), run, output_tensors)
         return self._fallback(output_tensors).reduce_scatter(output_tensors, input_tensors, opts)
 
     def _reduce_scatter_base(self, output_tensor, input_tensor, opts=ReduceScatterOptions()):
@@ -213,7 +255,15 @@ class FlexarProcessGroup(dist.ProcessGroup):
         return _create_work_from_future(fut)
 
     def reduce_scatter_tensor_coalesced(self, output_tensors, input_tensors, opts=ReduceScatterOptions()):
-        return self._fallback(input_tensors).reduce_scatter_tensor_coalesced(output_tensors, input_tensors, opts)
+        """FSDP2's gradient reduce-scatter of many buckets: one flexar reduce-scatter per pair, side stream."""
+        opname = _redop_name(opts.reduceOp)
+        if not all(self._rs_ok(o, i, opname) for o, i in zip(output_tensors, input_tensors)):
+            return self._fallback(input_tensors).reduce_scatter_tensor_coalesced(output_tensors, input_tensors, opts)
+
+        def run(c):
+            for o, i in zip(output_tensors, input_tensors):
+                c.reduce_scatter(i, o, op=opname)
+        return self._on_side(list(input_tensors) + list(output_tensors), run, list(output_tensors))
 
     def alltoall_base(self, output, input, output_split_sizes, input_split_sizes, opts=AllToAllOptions()):
         return self._fallback([input]).alltoall_base(output, input, output_split_sizes, input_split_sizes, opts)

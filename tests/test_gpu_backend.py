@@ -125,9 +125,28 @@ def _colls(rank, world, port, q):
         x = torch.ones(5, device=dev)
         dist.all_reduce(x, op=dist.ReduceOp.AVG)
         e3 = (x - 1).abs().max().item()
+        # list forms (dist.all_gather / dist.reduce_scatter) and the coalesced tensor forms FSDP2 issues
+        outs = [torch.empty(7, 3, device=dev) for _ in range(world)]
+        dist.all_gather(outs, torch.full((7, 3), float(rank + 1), device=dev))
+        e4 = max((o - (r + 1)).abs().max().item() for r, o in enumerate(outs))
+        chunks = [torch.full((9,), float((rank + 1) * (c + 1)), device=dev) for c in range(world)]
+        rs = torch.empty(9, device=dev)
+        dist.reduce_scatter(rs, chunks)
+        e5 = (rs - (rank + 1) * sum(r + 1 for r in range(world))).abs().max().item()
+        pg = dist.group.WORLD
+        ins = [torch.full((m,), float(rank), device=dev), torch.full((3,), float(rank) + 0.5, device=dev)]
+        gos = [torch.empty(world * m, device=dev), torch.empty(world * 3, device=dev)]
+        pg.allgather_into_tensor_coalesced(gos, ins).wait()
+        e6 = max((gos[0] - torch.arange(world, device=dev).float().repeat_interleave(m)).abs().max().item(),
+                 (gos[1] - (torch.arange(world, device=dev).float() + 0.5).repeat_interleave(3)).abs().max().item())
+        rsi = [torch.ones(world * 4, device=dev) * (rank + 1), torch.ones(world * 2, device=dev)]
+        rso = [torch.empty(4, device=dev), torch.empty(2, device=dev)]
+        pg.reduce_scatter_tensor_coalesced(rso, rsi).wait()
+        e7 = max((rso[0] - sum(r + 1 for r in range(world))).abs().max().item(), (rso[1] - world).abs().max().item())
+        torch.cuda.synchronize()
         used = dist.group.WORLD.stats["flexar_allreduce"]
         dist.destroy_process_group()
-        q.put((rank, max(e1, e2, e3), used, None))
+        q.put((rank, max(e1, e2, e3, e4, e5, e6, e7), used, None))
     except Exception:
         import traceback
 
@@ -148,7 +167,7 @@ def test_backend_reduce_scatter_all_gather(cuda):
         p.join(60)
     for rank, err, used, tb in res:
         assert tb is None, tb
-        assert err == 0.0 and used >= 3, (rank, err, used)
+        assert err == 0.0 and used >= 7, (rank, err, used)
 
 
 def test_rccl_algo_routing_single_rank():
