@@ -9,13 +9,17 @@ PyTorch-ROCm equivalent is a c10d backend:
     dist.init_process_group("flexar", ...)            # or "cuda:flexar,cpu:gloo"
 
 * ``allreduce`` / ``allreduce_coalesced`` on ROCm tensors run the flexar executor
-  kernel (stream-ordered on the current stream, no host sync);
-* every other collective (broadcast, all-gather, reduce-scatter, all-to-all,
-  barrier, send/recv) and unsupported dtypes/ops delegate to an internal RCCL
-  group (``FLEXAR_PG_FALLBACK=nccl``, default) or gloo; CPU tensors use gloo.
+  kernel (on a side stream ordered after the caller's stream, no host sync);
+* ``all_gather`` / ``all_gather_into_tensor`` / ``reduce_scatter`` /
+  ``reduce_scatter_tensor`` and their coalesced forms (FSDP/ZeRO) run the flexar
+  reduce-scatter / all-gather programs;
+* every other collective (broadcast, all-to-all, barrier, send/recv) and
+  unsupported dtypes/ops delegate to an internal RCCL group
+  (``FLEXAR_PG_FALLBACK=nccl``, default) or gloo; CPU tensors use gloo.
 
 ``flexar_allreduce_hook`` is the lighter-weight alternative: keep RCCL as the
-process group and route only DDP's gradient buckets through flexar.
+process group and route only DDP's gradient buckets through flexar;
+``flexar_fp8_compress_hook`` does the same with fp8 e4m3 on the wire.
 """
 from __future__ import annotations
 
@@ -334,5 +338,37 @@ def flexar_allreduce_hook(state, bucket):
         state.comm.all_reduce(buf, op="avg" if buf.is_floating_point() else "sum", algo=state.algo)
         fut = torch.futures.Future(devices=[buf.device])
         fut.set_result(buf)  # CUDA-aware: DDP's wait joins the side stream, backward keeps overlapping
+    state.calls += 1
+    return fut
+
+
+def flexar_fp8_compress_hook(state, bucket):
+    """DDP comm hook: fp8 (OCP e4m3) compressed gradient allreduce — BASELINE config #5 in a training step.
+
+    1. one 4-byte MAX allreduce (flexar LL protocol) agrees on the bucket's global amax;
+    2. every rank pre-scales its bucket by s = 448 / (N * amax) and casts to fp8 e4m3 (N * |x| * s <= 448,
+       so no partial sum can saturate);
+    3. the fp8 buffer is allreduced with the 1/N post-scale fused into the reduction kernel (fp32
+       accumulate, one rounding), i.e. the kernel produces fp8(mean * s);
+    4. the mean is decompressed as fp8 / s into the bucket.
+    Moves 1/4 of the fp32 bytes (1/2 of bf16) over xGMI; the error is e4m3's 2^-4 relative step of the
+    largest |gradient| per bucket. Use like ``flexar_allreduce_hook`` with a ``FlexarHookState``."""
+    buf = bucket.buffer()
+    if not buf.is_floating_point():
+        return flexar_allreduce_hook(state, bucket)
+    cur = torch.cuda.current_stream(buf.device)
+    side = state.stream(buf.device)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        buf.record_stream(side)
+        n = state.comm.world_size
+        amax = buf.abs().max().float().reshape(1)
+        state.comm.all_reduce(amax, op="max")
+        s = torch.where(amax > 0, 448.0 / (n * amax), torch.ones_like(amax))
+        q = (buf.float() * s).to(torch.float8_e4m3fn)
+        state.comm.all_reduce(q, op="avg", algo=state.algo)
+        buf.copy_(q.float() / s)
+        fut = torch.futures.Future(devices=[buf.device])
+        fut.set_result(buf)
     state.calls += 1
     return fut
