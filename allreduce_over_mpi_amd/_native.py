@@ -70,6 +70,9 @@ def _sig(lib):
         "flexar_reduce_scatter": (i, [vp, vp, vp, sz, i, i, vp, cp]),
         "flexar_all_gather": (i, [vp, vp, vp, sz, i, vp, cp]),
         "flexar_group_collective": (i, [c.POINTER(vp), i, i, c.POINTER(vp), c.POINTER(vp), sz, i, i, vp, cp]),
+        "flexar_broadcast": (i, [vp, vp, vp, sz, i, i, vp, cp]),
+        "flexar_group_broadcast": (i, [c.POINTER(vp), i, i, c.POINTER(vp), c.POINTER(vp), sz, i, vp, cp]),
+        "flexar_simulate_bcast": (i, [cp, i, sz, i, i, c.POINTER(vp), c.POINTER(vp), i, i]),
     }
     for name, (res, args) in table.items():
         fn = getattr(lib, name)
@@ -250,4 +253,18 @@ def simulate_coll(coll: str, spec: str, inputs, count: int, dtype: str = "float3
                                     _ptr_array([x.ctypes.data for x in ins]), _ptr_array([o.ctypes.data for o in outs]),
                                     grid, ncalls, float(scale))
     check(rc, "simulate_coll")
+    return outs
+
+
+def simulate_bcast(spec: str, data, nranks: int, root: int = 0, dtype: str = "float32", grid=2, ncalls=2):
+    """Simulate a broadcast of the numpy array ``data`` (the root's input) to ``nranks`` ranks."""
+    import numpy as np
+
+    src = np.ascontiguousarray(data)
+    ins = [src if r == root else np.zeros_like(src) for r in range(nranks)]
+    outs = [np.zeros_like(src) for _ in range(nranks)]
+    rc = lib().flexar_simulate_bcast(spec.encode(), nranks, src.size, DTYPES[dtype], root,
+                                     _ptr_array([x.ctypes.data for x in ins]), _ptr_array([o.ctypes.data for o in outs]),
+                                     grid, ncalls)
+    check(rc, "simulate_bcast")
     return outs

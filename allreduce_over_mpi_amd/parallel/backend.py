@@ -13,7 +13,8 @@ PyTorch-ROCm equivalent is a c10d backend:
 * ``all_gather`` / ``all_gather_into_tensor`` / ``reduce_scatter`` /
   ``reduce_scatter_tensor`` and their coalesced forms (FSDP/ZeRO) run the flexar
   reduce-scatter / all-gather programs;
-* every other collective (broadcast, all-to-all, barrier, send/recv) and
+* ``broadcast`` runs the flexar broadcast programs;
+* every other collective (all-to-all, barrier, send/recv) and
   unsupported dtypes/ops delegate to an internal RCCL group
   (``FLEXAR_PG_FALLBACK=nccl``, default) or gloo; CPU tensors use gloo.
 
@@ -172,6 +173,13 @@ class FlexarProcessGroup(dist.ProcessGroup):
         return self._gloo.barrier(opts)
 
     def broadcast(self, tensor_list, opts=BroadcastOptions()):
+        """DDP's initial parameter/buffer sync and model-state broadcasts: flexar direct multicast (small) or
+        scatter + all-gather (large) from the root."""
+        if len(tensor_list) == 1 and self._flexar_ok(tensor_list, "sum"):
+            t = tensor_list[0]
+            root = opts.rootRank
+            return self._on_side([t], lambda c: c.broadcast(t.view(torch.uint8) if t.dtype == torch.bool else t,
+                                                            root=root), tensor_list)
         return self._fallback(tensor_list).broadcast(tensor_list, opts)
 
     def allgather(self, output_tensors, input_tensor, opts=AllgatherOptions()):

@@ -170,6 +170,19 @@ class Communicator:
                                              algo.encode() if algo else None), "all_gather")
         return output
 
+    def broadcast(self, tensor, root: int = 0, out=None, algo: Optional[str] = None, stream=None):
+        """Broadcast ``tensor`` of rank ``root`` (in place unless ``out`` is given) to every rank."""
+        _require_cuda(tensor)
+        dst = tensor if out is None else out
+        if out is not None:
+            _require_cuda(out, "out")
+            if out.numel() != tensor.numel() or out.dtype != tensor.dtype:
+                raise nv.FlexarError(1, "out must match tensor in size and dtype")
+        nv.check(self._lib.flexar_broadcast(self._h, tensor.data_ptr(), dst.data_ptr(), tensor.numel(),
+                                            nv.dtype_code(tensor.dtype), int(root), _stream_handle(stream),
+                                            algo.encode() if algo else None), "broadcast")
+        return dst
+
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
             self._lib.flexar_comm_destroy(self._h)
@@ -273,6 +286,15 @@ class LocalGroup:
         nv.check(self._lib.flexar_group_collective(self._comms, self.nranks, code, a, b, count,
                                                    nv.dtype_code(ins[0].dtype), nv.op_code(op), _stream_handle(stream),
                                                    algo.encode() if algo else None), coll)
+        return outs
+
+    def broadcast(self, ins: Sequence, outs: Sequence, root: int = 0, algo: Optional[str] = None, stream=None):
+        """Broadcast ``ins[root]`` into every ``outs[r]`` in one launch."""
+        a = (ctypes.c_void_p * self.nranks)(*[t.data_ptr() for t in ins])
+        b = (ctypes.c_void_p * self.nranks)(*[t.data_ptr() for t in outs])
+        nv.check(self._lib.flexar_group_broadcast(self._comms, self.nranks, int(root), a, b, outs[0].numel(),
+                                                  nv.dtype_code(outs[0].dtype), _stream_handle(stream),
+                                                  algo.encode() if algo else None), "broadcast")
         return outs
 
     def check(self):

@@ -118,6 +118,11 @@ int flexar_reduce_scatter(flexar_comm_t comm, const void* sendbuf, void* recvbuf
                           void* hip_stream, const char* algo);
 int flexar_all_gather(flexar_comm_t comm, const void* sendbuf, void* recvbuf, size_t count, int dtype,
                       void* hip_stream, const char* algo);
+/* Broadcast `count` elements from `root`: the root reads sendbuf (NULL = recvbuf), every rank writes
+ * recvbuf. algo: "oneshot" = direct multicast from the root; "flat" (or any other spec) = scatter +
+ * all-gather (~2 S / N per link); NULL/"auto" = direct up to 256 KiB, scatter + all-gather above. */
+int flexar_broadcast(flexar_comm_t comm, const void* sendbuf, void* recvbuf, size_t count, int dtype, int root,
+                     void* hip_stream, const char* algo);
 /* Non-blocking health check: returns FLEXAR_ERR_TIMEOUT (and fills flexar_last_error)
  * if a device-side wait timed out in any previous call. */
 int flexar_comm_check(flexar_comm_t comm);
@@ -136,6 +141,8 @@ int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
 /* coll: 1 = reduce-scatter, 2 = all-gather (count = elements per rank block). */
 int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const void* const* ins, void* const* outs,
                             size_t count, int dtype, int op, void* hip_stream, const char* algo);
+int flexar_group_broadcast(flexar_comm_t* comms, int nranks, int root, const void* const* ins, void* const* outs,
+                           size_t count, int dtype, void* hip_stream, const char* algo);
 
 /* ---- standalone device reduction kernel ----------------------------------- */
 /* dst[i] = scale * OP_k srcs[k][i], k < nsrc (1..64), fp32 accumulation for 16/8-bit floats. */
@@ -178,6 +185,9 @@ int flexar_simulate_coll(int coll, const char* spec, int nranks, size_t count, i
                          const void* const* inputs, void* const* outputs, int grid, int ncalls, float scale);
 int flexar_simulate(const char* spec, int nranks, size_t count, int dtype, int op, const void* const* inputs,
                     void* const* outputs, int grid, int ncalls, int in_place, float scale);
+/* Broadcast programs from `root` (inputs: root's source; outputs: every rank's destination). */
+int flexar_simulate_bcast(const char* spec, int nranks, size_t count, int dtype, int root, const void* const* inputs,
+                          void* const* outputs, int grid, int ncalls);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -44,7 +44,7 @@ struct Program {
   std::string desc;
 };
 
-enum class Coll { ALLREDUCE = 0, REDUCE_SCATTER = 1, ALL_GATHER = 2 };
+enum class Coll { ALLREDUCE = 0, REDUCE_SCATTER = 1, ALL_GATHER = 2, BROADCAST = 3 };
 
 class Planner {
  public:
@@ -110,8 +110,33 @@ class Planner {
   // Reduce-scatter / all-gather programs. `count` = elements per rank-block (m); `stride` = elements
   // between consecutive rank-blocks of the N*m side (IN for reduce-scatter, OUT for all-gather), so a
   // call can be split into pieces along m. Ring for "ring*", otherwise the direct (flat) exchange.
+  // Broadcast: `stride` is the root rank; "oneshot" = direct multicast, otherwise scatter + all-gather.
   bool build_coll(Coll coll, const AlgoSpec& spec, uint64_t stride, Program* P, std::string* err) {
     if (coll == Coll::ALLREDUCE) return build(spec, P, err);
+    if (coll == Coll::BROADCAST) {
+      if (stride >= N) { if (err) *err = "broadcast root out of range"; return false; }
+      prog = P;
+      *P = Program();
+      P->count = count;
+      P->esize = esize;
+      P->chan_start.push_back(0);
+      stg = 0;
+      if (N == 1) {
+        if (count) xfer(count, {loc(BUF_IN, r, 0)}, {loc(BUF_OUT, r, 0)}, 1.0f);
+        finish_channel();
+        P->desc = "copy";
+      } else if (spec.kind == AlgoKind::ONESHOT || spec.kind == AlgoKind::LL) {
+        build_bcast_direct((uint32_t)stride);
+        P->desc = "bcast-direct";
+      } else {
+        build_bcast_scatter_ag((uint32_t)stride);
+        P->desc = "bcast-scatter-ag";
+      }
+      P->stg_elems = stg;
+      P->nchan = (uint32_t)P->chan_start.size() - 1;
+      mark_runs(*P, r);
+      return true;
+    }
     prog = P;
     *P = Program();
     P->count = count;
@@ -582,6 +607,68 @@ class Planner {
       if (i + 2 < N) dsts.push_back(loc(BUF_STG, right, base + (i + 1) * m_al));
       xfer(m, {loc(BUF_STG, r, base + i * m_al)}, dsts, 1.0f);
       if (i + 2 < N) signal({right}, i + 1);
+    }
+    finish_channel();
+  }
+
+  // ------------------------------------------------------------------ broadcast
+  // Every non-root rank acknowledges (slot 2) once it has consumed its staging, and the root waits for
+  // all acks before its call ends: without this back edge a root that never waits could run two calls
+  // ahead and overwrite a staging half a peer is still reading.
+  std::vector<uint32_t> others_of(uint32_t root) const {
+    std::vector<uint32_t> v;
+    for (uint32_t jj = 1; jj < N; ++jj)
+      if ((r + jj) % N != root) v.push_back((r + jj) % N);
+    return v;
+  }
+  // Small buffers: one hop. The root multicasts the whole buffer into every peer's staging.
+  void build_bcast_direct(uint32_t root) {
+    const uint64_t base = alloc(count);
+    if (r == root) {
+      std::vector<Loc> dsts{loc(BUF_OUT, r, 0)};
+      for (uint32_t p : rotated_peers()) dsts.push_back(loc(BUF_STG, p, base));
+      xfer(count, {loc(BUF_IN, r, 0)}, dsts, 1.0f);
+      signal(rotated_peers(), 0);
+      wait(rotated_peers(), 2);
+    } else {
+      wait({root}, 0);
+      xfer(count, {loc(BUF_STG, r, base)}, {loc(BUF_OUT, r, 0)}, 1.0f);
+      signal({root}, 2);
+    }
+    finish_channel();
+  }
+  // Large buffers: the root scatters block p to rank p (and multicasts its own block), then the
+  // non-root ranks all-gather their blocks. Every link carries ~2 S / N instead of S out of the root.
+  void build_bcast_scatter_ag(uint32_t root) {
+    const uint64_t split = round_up((count + N - 1) / N);
+    auto blen = [&](uint32_t k) -> uint64_t {
+      uint64_t s0 = (uint64_t)k * split;
+      return s0 >= count ? 0 : std::min(split, count - s0);
+    };
+    auto boff = [&](uint32_t k) { return (uint64_t)k * split; };
+    const uint64_t base = alloc((uint64_t)N * split);  // slot k holds block k
+    if (r == root) {
+      auto peers = rotated_peers();
+      for (uint32_t p : peers) xfer(blen(p), {loc(BUF_IN, r, boff(p))}, {loc(BUF_STG, p, base + boff(p))}, 1.0f);
+      std::vector<Loc> mine{loc(BUF_OUT, r, boff(r))};
+      for (uint32_t p : peers) mine.push_back(loc(BUF_STG, p, base + boff(r)));
+      xfer(blen(r), {loc(BUF_IN, r, boff(r))}, mine, 1.0f);
+      for (uint32_t p : peers) xfer(blen(p), {loc(BUF_IN, r, boff(p))}, {loc(BUF_OUT, r, boff(p))}, 1.0f);
+      signal(peers, 0);
+      wait(peers, 2);
+    } else {
+      auto others = others_of(root);
+      wait({root}, 0);
+      std::vector<Loc> fwd{loc(BUF_OUT, r, boff(r))};
+      for (uint32_t q : others) fwd.push_back(loc(BUF_STG, q, base + boff(r)));
+      xfer(blen(r), {loc(BUF_STG, r, base + boff(r))}, fwd, 1.0f);
+      xfer(blen(root), {loc(BUF_STG, r, base + boff(root))}, {loc(BUF_OUT, r, boff(root))}, 1.0f);
+      if (!others.empty()) {
+        signal(others, 1);
+        wait(others, 1);
+        for (uint32_t q : others) xfer(blen(q), {loc(BUF_STG, r, base + boff(q))}, {loc(BUF_OUT, r, boff(q))}, 1.0f);
+      }
+      signal({root}, 2);
     }
     finish_channel();
   }

@@ -233,6 +233,26 @@ int flexar_simulate_coll(int coll, const char* spec, int nranks, size_t count, i
                                    outputs, count);
 }
 
+int flexar_simulate_bcast(const char* spec, int nranks, size_t count, int dtype, int root, const void* const* inputs,
+                          void* const* outputs, int grid, int ncalls) {
+  size_t es = dtype_size(dtype);
+  if (!es || nranks < 1 || nranks > 64 || grid < 1 || grid > 64 || ncalls < 1 || !inputs || !outputs || root < 0 ||
+      root >= nranks) {
+    set_error("bad simulate arguments");
+    return FLEXAR_ERR_INVALID;
+  }
+  AlgoSpec s;
+  std::string err;
+  if (!parse_algo(spec ? spec : "auto", nranks, &s, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  if (s.kind == AlgoKind::AUTO) s.kind = count * es <= (256u << 10) ? AlgoKind::ONESHOT : AlgoKind::TREE;
+  std::vector<Program> progs(nranks);
+  for (int r = 0; r < nranks; ++r) {
+    Planner pl(nranks, r, count, (uint32_t)es, 1.0f);
+    if (!pl.build_coll(Coll::BROADCAST, s, (uint64_t)root, &progs[r], &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  }
+  return dispatch_dtype_op<SimRun>(dtype, FLEXAR_SUM, progs, nranks, grid, ncalls, 0, inputs, outputs, count);
+}
+
 int flexar_reduce_host(void* dst, const void* const* srcs, int nsrc, size_t count, int dtype, int op, float scale) {
   if (!dst || !srcs || nsrc < 1) { set_error("bad reduce arguments"); return FLEXAR_ERR_INVALID; }
   float fs = scale * (op == FLEXAR_AVG ? 1.0f / (float)nsrc : 1.0f);

@@ -336,6 +336,53 @@ static int run_rs_ag(flexar_comm* c, Coll coll, const void* in, void* out, size_
   return 0;
 }
 
+// Broadcast spec: "oneshot"/"ll" = direct multicast from the root, any other explicit spec = scatter +
+// all-gather (its "+wt"/"+nts" protocol modifiers apply); auto: direct up to 256 KiB (one hop wins while
+// latency bound), scatter + all-gather above (~2 S / N per link instead of S out of the root).
+static int bcast_spec(flexar_comm* c, const char* algo, uint64_t bytes, AlgoSpec* out) {
+  AlgoSpec s;
+  if (algo && *algo) {
+    std::string err;
+    if (!parse_algo(algo, c->nranks, &s, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  }
+  if (s.kind == AlgoKind::AUTO || s.kind == AlgoKind::DMA) s.kind = bytes <= (256u << 10) ? AlgoKind::ONESHOT : AlgoKind::TREE;
+  if (s.kind == AlgoKind::LL) s.kind = AlgoKind::ONESHOT;
+  if (s.kind != AlgoKind::ONESHOT) s.kind = AlgoKind::TREE, s.widths = {c->nranks};
+  *out = s;
+  return 0;
+}
+
+// Broadcast of `count` elements from `root` (root reads `in`; every rank writes `out`), split into
+// pieces that fit one staging half. The executor only copies (K = 1), so the SUM instantiation runs.
+static int run_bcast(flexar_comm* c, const void* in, void* out, size_t count, int dtype, int root, hipStream_t st,
+                     const char* algo) {
+  const uint32_t es = (uint32_t)dtype_size(dtype);
+  AlgoSpec s;
+  int rc = bcast_spec(c, algo, (uint64_t)count * es, &s);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  uint64_t piece = count;
+  if (c->nranks > 1 && (rc = plan_pieces(c, s, count, es, 1.0f, &piece, Coll::BROADCAST, (uint64_t)root))) return rc;
+  for (uint64_t off = 0; off < count; off += piece) {
+    uint64_t n = std::min<uint64_t>(piece, count - off);
+    DevProgram* dp = nullptr;
+    if ((rc = get_program(c, s, n, es, 1.0f, &dp, Coll::BROADCAST, (uint64_t)root))) return rc;
+    DevCtx x;
+    fill_ctx(c, dp, (const char*)in + off * es, (char*)out + off * es, &x);
+    LaunchArgs la;
+    la.kind = LAUNCH_EXEC;
+    la.ctx = x;
+    la.grid = choose_grid(c, n * es, dp->prog.nchan);
+    la.stream = st;
+    la.proto = proto_of(s);
+    if ((rc = launch_dtype(dtype, FLEXAR_SUM, la))) return rc;
+    c->launches++;
+  }
+  c->calls++;
+  c->bytes += count * es;
+  return 0;
+}
+
 // dst (and dst2, if given) = scale * OP(srcs[0..nsrc)) over `count` elements: groups of kMaxSrc
 // sources chain through dst (fan-in > 8: dst joins the next group; only the last group scales and
 // writes dst2).
@@ -860,6 +907,18 @@ int flexar_all_gather(flexar_comm_t c, const void* in, void* out, size_t count, 
   return run_rs_ag(c, Coll::ALL_GATHER, in, out, count, dtype, FLEXAR_SUM, (hipStream_t)stream, algo, 1.0f);
 }
 
+int flexar_broadcast(flexar_comm_t c, const void* in, void* out, size_t count, int dtype, int root, void* stream,
+                     const char* algo) {
+  int rc = validate_call(c, dtype, FLEXAR_SUM, 1.0f);
+  if (rc) return rc;
+  if (!out) { set_error("broadcast needs a recv buffer"); return FLEXAR_ERR_INVALID; }
+  if (root < 0 || root >= c->nranks) { set_error("broadcast root out of range"); return FLEXAR_ERR_INVALID; }
+  if ((rc = check_err(c))) return rc;
+  if (count == 0) return 0;
+  if (!in) in = out;
+  return run_bcast(c, in, out, count, dtype, root, (hipStream_t)stream, algo);
+}
+
 // ---- in-process group: N ranks on ONE device in one process (tests / calibration) -------------
 int flexar_group_create(int nranks, int device, size_t workspace_bytes, flexar_comm_t* comms) {
   if (!comms || nranks < 1 || nranks > (int)kMaxRanks) { set_error("invalid nranks"); return FLEXAR_ERR_INVALID; }
@@ -1017,6 +1076,49 @@ int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const vo
   la.stream = st;
   la.proto = proto;
   int rc = launch_dtype(dtype, op, la);
+  if (rc) return rc;
+  for (int r = 0; r < nranks; ++r) comms[r]->launches++;
+  FX_HIP(hipStreamSynchronize(st));
+  return 0;
+}
+
+// Broadcast for an in-process group (tests): one launch, every rank of the group.
+int flexar_group_broadcast(flexar_comm_t* comms, int nranks, int root, const void* const* ins, void* const* outs,
+                           size_t count, int dtype, void* stream, const char* algo) {
+  if (!comms || nranks < 1 || root < 0 || root >= nranks) { set_error("bad group broadcast arguments"); return FLEXAR_ERR_INVALID; }
+  for (int r = 0; r < nranks; ++r) {
+    int rc = validate_call(comms[r], dtype, FLEXAR_SUM, 1.0f);
+    if (rc) return rc;
+  }
+  if (count == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const uint32_t es = (uint32_t)dtype_size(dtype);
+  static thread_local DevCtx* d_ctx = nullptr;
+  if (!d_ctx) FX_HIP(hipMalloc(&d_ctx, sizeof(DevCtx) * kMaxRanks));
+  std::vector<DevCtx> h(nranks);
+  int grid = 0, proto = PM_FENCE;
+  for (int r = 0; r < nranks; ++r) {
+    AlgoSpec s;
+    int rc = bcast_spec(comms[r], algo, (uint64_t)count * es, &s);
+    if (rc) return rc;
+    proto = proto_of(s);
+    DevProgram* dp = nullptr;
+    if ((rc = get_program(comms[r], s, count, es, 1.0f, &dp, Coll::BROADCAST, (uint64_t)root))) return rc;
+    if (dp->prog.stg_elems * es > comms[r]->exec_half) { set_error("group broadcast exceeds workspace"); return FLEXAR_ERR_NOMEM; }
+    const void* in = ins && ins[r] ? ins[r] : outs[r];
+    fill_ctx(comms[r], dp, in, outs[r], &h[r]);
+    int g = choose_grid(comms[r], count * es, dp->prog.nchan);
+    grid = r == 0 ? g : grid;
+  }
+  FX_HIP(hipMemcpyAsync(d_ctx, h.data(), sizeof(DevCtx) * nranks, hipMemcpyHostToDevice, st));
+  LaunchArgs la;
+  la.kind = LAUNCH_GROUP;
+  la.d_ctxs = d_ctx;
+  la.nranks = nranks;
+  la.grid = grid;
+  la.stream = st;
+  la.proto = proto;
+  int rc = launch_dtype(dtype, FLEXAR_SUM, la);
   if (rc) return rc;
   for (int r = 0; r < nranks; ++r) comms[r]->launches++;
   FX_HIP(hipStreamSynchronize(st));

@@ -146,10 +146,13 @@ def _colls(rank, world, port, q):
         rso = [torch.empty(4, device=dev), torch.empty(2, device=dev)]
         pg.reduce_scatter_tensor_coalesced(rso, rsi).wait()
         e7 = max((rso[0] - sum(r + 1 for r in range(world))).abs().max().item(), (rso[1] - world).abs().max().item())
+        bc = torch.arange(100003, device=dev, dtype=torch.float32) * (rank + 1)
+        dist.broadcast(bc, src=1)
+        e8 = (bc - torch.arange(100003, device=dev).float() * 2).abs().max().item()
         torch.cuda.synchronize()
         used = dist.group.WORLD.stats["flexar_allreduce"]
         dist.destroy_process_group()
-        q.put((rank, max(e1, e2, e3, e4, e5, e6, e7), used, None))
+        q.put((rank, max(e1, e2, e3, e4, e5, e6, e7, e8), used, None))
     except Exception:
         import traceback
 
@@ -170,7 +173,7 @@ def test_backend_reduce_scatter_all_gather(cuda):
         p.join(60)
     for rank, err, used, tb in res:
         assert tb is None, tb
-        assert err == 0.0 and used >= 7, (rank, err, used)
+        assert err == 0.0 and used >= 8, (rank, err, used)
 
 
 def test_rccl_algo_routing_single_rank():

@@ -290,3 +290,23 @@ def test_chunk_and_channel_knobs(cuda, monkeypatch):
         grp.check()
     finally:
         grp.close()
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_group_broadcast(cuda, groups, n):
+    """Broadcast from every root: direct (small/auto) and scatter + all-gather (large/flat), fp32 and bf16,
+    with data that changes every call (stale staging would show)."""
+    grp = groups[n]
+    g = torch.Generator(device=cuda).manual_seed(51)
+    for dtype in (torch.float32, torch.bfloat16):
+        for size in (3, 4099, 300007):
+            for spec in (None, "oneshot", "flat", "flat+wt"):
+                for root in range(n):
+                    src = torch.randn(size, device=cuda, generator=g).to(dtype)
+                    ins = [src if r == root else torch.zeros_like(src) for r in range(n)]
+                    outs = [torch.full_like(src, -1) for _ in range(n)]
+                    grp.broadcast(ins, outs, root=root, algo=spec)
+                    torch.cuda.synchronize()
+                    for r, o in enumerate(outs):
+                        assert torch.equal(o, src), (dtype, size, spec, root, r)
+    grp.check()

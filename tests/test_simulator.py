@@ -167,3 +167,16 @@ def test_reduce_scatter_all_gather(nv, n, spec):
         outs = nv.simulate_coll("all_gather", spec, ins, m, grid=3)
         for o in outs:
             np.testing.assert_array_equal(o, np.concatenate(ins), err_msg=f"ag {spec} n={n} m={m}")
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
+@pytest.mark.parametrize("spec", ["oneshot", "flat", "flat+wt"])
+def test_broadcast(nv, n, spec):
+    """Direct multicast and scatter + all-gather from every root, tails included, consecutive calls."""
+    rng = np.random.default_rng(n)
+    for size in (1, 5, 1001, 65539):
+        data = rng.standard_normal(size).astype(np.float32)
+        for root in range(n):
+            outs = nv.simulate_bcast(spec, data, n, root=root, grid=3, ncalls=3)
+            for r, o in enumerate(outs):
+                np.testing.assert_array_equal(o, data, err_msg=f"{spec} n={n} size={size} root={root} r={r}")
