@@ -138,3 +138,52 @@ def test_ipc_allreduce_hip_graph_replay(cuda):
     for rank, errs, tb in res:
         assert tb is None, tb
         assert max(errs) == 0.0, (rank, errs)
+
+
+def _hier_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
+                          FLEXAR_TIMEOUT_MS="20000")
+        import torch.distributed as dist
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from allreduce_over_mpi_amd.parallel import HierarchicalCommunicator
+
+        hc = HierarchicalCommunicator(node_size=2, workspace_bytes=32 << 20)  # 2 virtual nodes x 2 ranks
+        dev = torch.device("cuda", 0)
+        errs = []
+        for size in (1, 3, 4097, 300001):
+            xs = [torch.randn(size, generator=torch.Generator().manual_seed(10 * r + size)) for r in range(world)]
+            st = torch.stack([x.double() for x in xs])
+            for op, want in (("sum", st.sum(0)), ("avg", st.mean(0)), ("max", st.max(0).values)):
+                y = hc.all_reduce(xs[rank].to(dev), op=op)
+                torch.cuda.synchronize()
+                errs.append((op, size, (y.double().cpu() - want).abs().max().item()))
+        hc.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, errs, None))
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_hierarchical_allreduce_virtual_nodes(cuda):
+    """Intra-node flexar RS/AG over IPC + cross-node allreduce of 1/L shards (2 virtual nodes x 2 ranks)."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hier_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(4)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, errs, tb in res:
+        assert tb is None, tb
+        for op, size, err in errs:
+            assert err < 1e-4, (rank, op, size, err)
