@@ -1,0 +1,57 @@
+"""fp8 (OCP e4m3) gradient compression kernels (csrc/src/k_quant.hip): one HBM pass each.
+
+    parts = fp8_amax(x)                    # FLEXAR_AMAX_PARTIALS per-workgroup max |x| (device, no host sync)
+    q = fp8_quantize(x, parts, num)        # e4m3(clamp(x * num / amax, +-448)), amax = parts.max()
+    fp8_dequantize(q, parts, num, out=x)   # x = q * amax / num
+
+Used by the fp8-compressed DDP hook (parallel/backend.py) between a MAX allreduce of the partials
+(1 KiB) and the fp8 allreduce with the fused 1/N post-scale (BASELINE config #5).
+"""
+from __future__ import annotations
+
+from .. import _native as nv
+from ..parallel.comm import _stream_handle
+
+
+def _check(t, what):
+    if not t.is_cuda or not t.is_contiguous():
+        raise nv.FlexarError(1, f"{what} must be a contiguous ROCm tensor")
+    if t.data_ptr() % 16:
+        raise nv.FlexarError(1, f"{what} must be 16-byte aligned")
+
+
+AMAX_PARTIALS = 256  # FLEXAR_AMAX_PARTIALS
+
+
+def fp8_amax(x, out=None, stream=None):
+    import torch
+
+    _check(x, "x")
+    out = torch.empty(AMAX_PARTIALS, dtype=torch.float32, device=x.device) if out is None else out
+    if out.numel() != AMAX_PARTIALS or out.dtype != torch.float32:
+        raise nv.FlexarError(1, f"amax partials must be {AMAX_PARTIALS} float32 values")
+    nv.check(nv.lib().flexar_amax(x.data_ptr(), x.numel(), nv.dtype_code(x.dtype), out.data_ptr(),
+                                  _stream_handle(stream)), "amax")
+    return out
+
+
+def fp8_quantize(x, amax, num: float = 448.0, out=None, stream=None):
+    import torch
+
+    _check(x, "x")
+    q = torch.empty(x.shape, dtype=torch.float8_e4m3fn, device=x.device) if out is None else out
+    _check(q, "out")
+    nv.check(nv.lib().flexar_quantize_fp8(x.data_ptr(), nv.dtype_code(x.dtype), q.data_ptr(), x.numel(),
+                                          amax.data_ptr(), float(num), _stream_handle(stream)), "quantize_fp8")
+    return q
+
+
+def fp8_dequantize(q, amax, num: float = 448.0, out=None, dtype=None, stream=None):
+    import torch
+
+    _check(q, "q")
+    x = torch.empty(q.shape, dtype=dtype or torch.float32, device=q.device) if out is None else out
+    _check(x, "out")
+    nv.check(nv.lib().flexar_dequantize_fp8(q.data_ptr(), x.data_ptr(), nv.dtype_code(x.dtype), q.numel(),
+                                            amax.data_ptr(), float(num), _stream_handle(stream)), "dequantize_fp8")
+    return x

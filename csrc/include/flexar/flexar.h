@@ -152,6 +152,17 @@ int flexar_reduce(void* dst, const void* const* srcs, int nsrc, size_t count, in
 int flexar_reduce_host(void* dst, const void* const* srcs, int nsrc, size_t count, int dtype, int op,
                        float scale);
 
+/* ---- fp8 (OCP e4m3) gradient compression (one HBM pass each) --------------- */
+#define FLEXAR_AMAX_PARTIALS 256
+/* parts_out: FLEXAR_AMAX_PARTIALS device floats of per-workgroup max |x| (their max = amax). */
+int flexar_amax(const void* x, size_t n, int dtype, float* parts_out, void* hip_stream);
+/* q = e4m3(clamp(x * num / amax, +-448)); amax = max over the partials (device pointer, no host sync). */
+int flexar_quantize_fp8(const void* x, int dtype, void* q, size_t n, const float* amax_parts, float num,
+                        void* hip_stream);
+/* x = q * amax / num (dtype: float32, bfloat16 or float16). */
+int flexar_dequantize_fp8(const void* q, void* x, int dtype, size_t n, const float* amax_parts, float num,
+                          void* hip_stream);
+
 /* ---- helpers --------------------------------------------------------------- */
 int flexar_pointer_is_device(const void* p); /* 1 if p is device memory */
 int flexar_current_device(void);

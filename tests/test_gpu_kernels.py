@@ -310,3 +310,26 @@ def test_group_broadcast(cuda, groups, n):
                     for r, o in enumerate(outs):
                         assert torch.equal(o, src), (dtype, size, spec, root, r)
     grp.check()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n", [1, 15, 4096, (1 << 20) + 7])
+def test_fp8_compression_kernels(cuda, dtype, n):
+    """amax / quantize / dequantize kernels against the PyTorch ops they fuse (bit-exact)."""
+    from allreduce_over_mpi_amd.ops import fp8_amax, fp8_dequantize, fp8_quantize
+
+    g = torch.Generator(device=cuda).manual_seed(n)
+    x = (torch.randn(n, device=cuda, generator=g) * 3).to(dtype)
+    amax = fp8_amax(x)
+    torch.cuda.synchronize()
+    assert amax.max().item() == x.float().abs().max().item()
+    num = 448.0 / 8
+    q = fp8_quantize(x, amax, num)
+    s = num / amax.max()
+    want_q = (x.float() * s).clamp(-448, 448).to(torch.float8_e4m3fn)
+    assert torch.equal(q.view(torch.uint8), want_q.view(torch.uint8))
+    y = fp8_dequantize(q, amax, num, dtype=dtype)
+    want_y = (q.float() * (1.0 / s)).to(dtype)
+    assert torch.equal(y, want_y)
+    # the round trip is within e4m3's half-step of the largest value
+    assert (y.float() - x.float()).abs().max().item() <= amax.max().item() * 2 ** -4 + 1e-6
