@@ -765,7 +765,8 @@ int flexar_comm_describe(flexar_comm_t c, size_t count, int dtype, char* buf, si
   rc = get_program(c, s, piece ? piece : 1, (uint32_t)es, 1.0f, &dp);
   if (rc) return rc;
   int grid = choose_grid(c, (uint64_t)piece * es, dp->prog.nchan);
-  snprintf(buf, buflen, "%s grid=%d pieces=%llu stg_bytes=%llu ops=%zu", s.str().c_str(), grid,
+  snprintf(buf, buflen, "%s grid=%d pieces=%llu stg_bytes=%llu ops=%zu",
+           c->nranks == 1 ? "copy (1 rank)" : s.str().c_str(), grid,
            (unsigned long long)(piece ? (count + piece - 1) / piece : 0),
            (unsigned long long)(dp->prog.stg_elems * es), dp->prog.ops.size());
   return 0;
