@@ -38,6 +38,8 @@ def candidates(world: int, nbytes: int) -> list[str]:
     c += ["ring", "ring+wt"] + [f"ring:{k}" for k in (2, 4) if k <= maxc]
     if world > 2 and (world & (world - 1)) == 0:
         c += ["rhd+pull"]
+    if world >= 8 and world % 4 == 0:
+        c += [f"tree:4,{world // 4}+pull", f"tree:{world // 4},4+pull"]
     if nbytes >= (1 << 20):
         c += ["dma"]
     return c
@@ -101,12 +103,17 @@ def main():
             failed = 0.0
             t = float("inf")
             try:
-                comm.all_reduce(x, out=y, algo=spec)
-                torch.cuda.synchronize()
-                comm.check()
-                err = float((y.float() - ref).abs().max().item())
+                # three calls on x, x/2, x/4 (exact scalings): a stale staging line from either of the two
+                # previous calls (same or other parity half) changes the result
                 tol = {torch.float32: 1e-5, torch.bfloat16: 2e-2, torch.float16: 4e-3}[dtype] * 4 * math.sqrt(world)
-                bad = err > tol * (float(ref.abs().max().item()) + 1e-6)
+                bad = False
+                for sc in (1.0, 0.5, 0.25):
+                    xs = x if sc == 1.0 else (x.float() * sc).to(dtype)
+                    comm.all_reduce(xs, out=y, algo=spec)
+                    torch.cuda.synchronize()
+                    err = float((y.float() - ref * sc).abs().max().item())
+                    bad |= err > tol * (float(ref.abs().max().item()) * sc + 1e-6)
+                comm.check()
                 if max_over_ranks(1.0 if bad else 0.0) == 0.0:
                     for _ in range(3):
                         comm.all_reduce(x, out=y, algo=spec)
