@@ -232,7 +232,7 @@ def main():
                     tune_log[spec] = f"WRONG (max rel err {err:.3g})"
                     log(rank, f"tuner: {spec} produced wrong results (rel err {err:.3g}); excluded")
                 else:
-                    t = timed(spec, 3)
+                    t = timed(spec, 5)
                     comm.check()
             except nv.FlexarError as e:
                 failed = 1.0
@@ -269,7 +269,7 @@ def main():
                     best, best_grid, best_t = spec, 0, timings[spec]
                 for g in grids:
                     comm.set_grid(g)
-                    t = timed(spec, 3)
+                    t = timed(spec, 5)
                     tune_log[f"{spec}@grid{g}"] = round(busbw_gbps(nbytes, t, world), 2)
                     if t < best_t:
                         best, best_grid, best_t = spec, g, t
