@@ -71,6 +71,7 @@ def _sig(lib):
         "flexar_all_gather": (i, [vp, vp, vp, sz, i, vp, cp]),
         "flexar_group_collective": (i, [c.POINTER(vp), i, i, c.POINTER(vp), c.POINTER(vp), sz, i, i, vp, cp]),
         "flexar_broadcast": (i, [vp, vp, vp, sz, i, i, vp, cp]),
+        "flexar_all_to_all": (i, [vp, vp, vp, sz, i, vp]),
         "flexar_amax": (i, [vp, sz, i, vp, vp]),
         "flexar_quantize_fp8": (i, [vp, i, vp, sz, vp, f, vp]),
         "flexar_dequantize_fp8": (i, [vp, vp, i, sz, vp, f, vp]),
@@ -240,17 +241,18 @@ def reduce_host(srcs, op="sum", scale=1.0, dtype: str | None = None):
     return out
 
 
-COLLS = {"allreduce": 0, "reduce_scatter": 1, "all_gather": 2}
+COLLS = {"allreduce": 0, "reduce_scatter": 1, "all_gather": 2, "all_to_all": 4}
 
 
 def simulate_coll(coll: str, spec: str, inputs, count: int, dtype: str = "float32", op="sum", grid=2, ncalls=2,
                   scale=1.0):
-    """Simulate reduce_scatter (inputs N*count, outputs count) or all_gather (inputs count, outputs N*count)."""
+    """Simulate reduce_scatter (inputs N*count, outputs count), all_gather (inputs count, outputs N*count)
+    or all_to_all (inputs and outputs N*count)."""
     import numpy as np
 
     n = len(inputs)
     ins = [np.ascontiguousarray(x) for x in inputs]
-    out_n = count if coll == "reduce_scatter" else (n * count if coll == "all_gather" else count)
+    out_n = count if coll == "reduce_scatter" else (n * count if coll in ("all_gather", "all_to_all") else count)
     outs = [np.zeros(out_n, dtype=ins[0].dtype) for _ in range(n)]
     rc = lib().flexar_simulate_coll(COLLS[coll], spec.encode(), n, count, DTYPES[dtype], op_code(op),
                                     _ptr_array([x.ctypes.data for x in ins]), _ptr_array([o.ctypes.data for o in outs]),

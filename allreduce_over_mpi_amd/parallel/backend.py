@@ -13,8 +13,9 @@ PyTorch-ROCm equivalent is a c10d backend:
 * ``all_gather`` / ``all_gather_into_tensor`` / ``reduce_scatter`` /
   ``reduce_scatter_tensor`` and their coalesced forms (FSDP/ZeRO) run the flexar
   reduce-scatter / all-gather programs;
-* ``broadcast`` runs the flexar broadcast programs;
-* every other collective (all-to-all, barrier, send/recv) and
+* ``broadcast`` runs the flexar broadcast programs, equal-split ``all_to_all_single`` the flexar
+  all-to-all (expert parallelism);
+* every other collective (uneven all-to-all, barrier, send/recv) and
   unsupported dtypes/ops delegate to an internal RCCL group
   (``FLEXAR_PG_FALLBACK=nccl``, default) or gloo; CPU tensors use gloo.
 
@@ -278,6 +279,12 @@ class FlexarProcessGroup(dist.ProcessGroup):
         return self._on_side(list(input_tensors) + list(output_tensors), run, list(output_tensors))
 
     def alltoall_base(self, output, input, output_split_sizes, input_split_sizes, opts=AllToAllOptions()):
+        """Equal splits (``dist.all_to_all_single`` without split sizes, the MoE dispatch/combine shape)
+        run the flexar direct exchange; uneven splits go to the fallback group."""
+        equal = not output_split_sizes and not input_split_sizes
+        if equal and self._flexar_ok([input, output], "sum") and input.dtype != torch.bool and \
+                input.numel() == output.numel() and input.numel() % self._world == 0 and input.dtype == output.dtype:
+            return self._on_side([input, output], lambda c: c.all_to_all(input.reshape(-1), output.view(-1)), [output])
         return self._fallback([input]).alltoall_base(output, input, output_split_sizes, input_split_sizes, opts)
 
     def alltoall(self, output_tensors, input_tensors, opts=AllToAllOptions()):

@@ -170,6 +170,18 @@ class Communicator:
                                              algo.encode() if algo else None), "all_gather")
         return output
 
+    def all_to_all(self, input, output, stream=None):
+        """Equal-split all-to-all (expert parallelism): block p of ``input`` (world_size blocks) goes to
+        rank p; block q of ``output`` comes from rank q. One direct exchange over all links."""
+        _require_cuda(input)
+        _require_cuda(output, "output")
+        if input.numel() != output.numel() or input.dtype != output.dtype or input.numel() % self.world_size:
+            raise nv.FlexarError(1, "input/output must have equal size (a multiple of world_size) and dtype")
+        nv.check(self._lib.flexar_all_to_all(self._h, input.data_ptr(), output.data_ptr(),
+                                             input.numel() // self.world_size, nv.dtype_code(input.dtype),
+                                             _stream_handle(stream)), "all_to_all")
+        return output
+
     def broadcast(self, tensor, root: int = 0, out=None, algo: Optional[str] = None, stream=None):
         """Broadcast ``tensor`` of rank ``root`` (in place unless ``out`` is given) to every rank."""
         _require_cuda(tensor)
@@ -278,9 +290,10 @@ class LocalGroup:
         return outs
 
     def collective(self, coll: str, ins: Sequence, outs: Sequence, op="sum", algo: Optional[str] = None, stream=None):
-        """``coll`` = "reduce_scatter" or "all_gather" for every rank of the group in one launch."""
+        """``coll`` = "reduce_scatter", "all_gather" or "all_to_all" for every rank of the group in one launch."""
         code = nv.COLLS[coll]
-        count = outs[0].numel() if coll == "reduce_scatter" else ins[0].numel()
+        count = outs[0].numel() if coll == "reduce_scatter" else (
+            ins[0].numel() // self.nranks if coll == "all_to_all" else ins[0].numel())
         a = (ctypes.c_void_p * self.nranks)(*[t.data_ptr() for t in ins])
         b = (ctypes.c_void_p * self.nranks)(*[t.data_ptr() for t in outs])
         nv.check(self._lib.flexar_group_collective(self._comms, self.nranks, code, a, b, count,

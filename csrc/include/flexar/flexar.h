@@ -118,6 +118,10 @@ int flexar_reduce_scatter(flexar_comm_t comm, const void* sendbuf, void* recvbuf
                           void* hip_stream, const char* algo);
 int flexar_all_gather(flexar_comm_t comm, const void* sendbuf, void* recvbuf, size_t count, int dtype,
                       void* hip_stream, const char* algo);
+/* All-to-all with equal splits (expert parallelism): sendbuf holds nranks blocks of `count` elements,
+ * block p goes to rank p; recvbuf receives nranks blocks, block q from rank q. One direct exchange. */
+int flexar_all_to_all(flexar_comm_t comm, const void* sendbuf, void* recvbuf, size_t count, int dtype,
+                      void* hip_stream);
 /* Broadcast `count` elements from `root`: the root reads sendbuf (NULL = recvbuf), every rank writes
  * recvbuf. algo: "oneshot" = direct multicast from the root; "flat" (or any other spec) = scatter +
  * all-gather (~2 S / N per link); NULL/"auto" = direct up to 256 KiB, scatter + all-gather above. */
@@ -138,7 +142,7 @@ int flexar_comm_describe(flexar_comm_t comm, size_t count, int dtype, char* buf,
 int flexar_group_create(int nranks, int device, size_t workspace_bytes, flexar_comm_t* comms_out);
 int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* ins, void* const* outs, size_t count,
                            int dtype, int op, void* hip_stream, const char* algo, float scale);
-/* coll: 1 = reduce-scatter, 2 = all-gather (count = elements per rank block). */
+/* coll: 1 = reduce-scatter, 2 = all-gather, 4 = all-to-all (count = elements per rank block). */
 int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const void* const* ins, void* const* outs,
                             size_t count, int dtype, int op, void* hip_stream, const char* algo);
 int flexar_group_broadcast(flexar_comm_t* comms, int nranks, int root, const void* const* ins, void* const* outs,

@@ -44,7 +44,7 @@ struct Program {
   std::string desc;
 };
 
-enum class Coll { ALLREDUCE = 0, REDUCE_SCATTER = 1, ALL_GATHER = 2, BROADCAST = 3 };
+enum class Coll { ALLREDUCE = 0, REDUCE_SCATTER = 1, ALL_GATHER = 2, BROADCAST = 3, ALL_TO_ALL = 4 };
 
 class Planner {
  public:
@@ -148,6 +148,9 @@ class Planner {
       if (count) xfer(count, {loc(BUF_IN, r, 0)}, {loc(BUF_OUT, r, 0)}, coll == Coll::REDUCE_SCATTER ? scale : 1.0f);
       finish_channel();
       P->desc = "copy";
+    } else if (coll == Coll::ALL_TO_ALL) {
+      build_flat_a2a(stride);
+      P->desc = "flat-a2a";
     } else if (coll == Coll::REDUCE_SCATTER) {
       ring ? build_ring_rs(stride) : build_flat_rs(stride);
       P->desc = ring ? "ring-rs" : "flat-rs";
@@ -558,6 +561,19 @@ class Planner {
     std::vector<Loc> dsts{loc(BUF_OUT, r, (uint64_t)r * stride)};
     for (uint32_t p : peers) dsts.push_back(loc(BUF_STG, p, base + r * m_al));
     xfer(m, {loc(BUF_IN, r, 0)}, dsts, 1.0f);
+    signal(peers, 0);
+    wait(peers, 0);
+    for (uint32_t p : peers) xfer(m, {loc(BUF_STG, r, base + p * m_al)}, {loc(BUF_OUT, r, (uint64_t)p * stride)}, 1.0f);
+    finish_channel();
+  }
+  // All-to-all (expert parallelism): block p of IN goes to rank p, block q of OUT comes from rank q.
+  // One direct exchange over all N-1 links (rotated run), then the landed blocks are copied out.
+  void build_flat_a2a(uint64_t stride) {
+    const uint64_t m = count, m_al = round_up(m);
+    uint64_t base = alloc((uint64_t)N * m_al);
+    auto peers = rotated_peers();
+    for (uint32_t p : peers) xfer(m, {loc(BUF_IN, r, (uint64_t)p * stride)}, {loc(BUF_STG, p, base + r * m_al)}, 1.0f);
+    xfer(m, {loc(BUF_IN, r, (uint64_t)r * stride)}, {loc(BUF_OUT, r, (uint64_t)r * stride)}, 1.0f);
     signal(peers, 0);
     wait(peers, 0);
     for (uint32_t p : peers) xfer(m, {loc(BUF_STG, r, base + p * m_al)}, {loc(BUF_OUT, r, (uint64_t)p * stride)}, 1.0f);

@@ -214,7 +214,7 @@ int flexar_simulate_coll(int coll, const char* spec, int nranks, size_t count, i
                          const void* const* inputs, void* const* outputs, int grid, int ncalls, float scale) {
   size_t es = dtype_size(dtype);
   if (!es || nranks < 1 || nranks > 64 || grid < 1 || grid > 64 || ncalls < 1 || !inputs || !outputs || coll < 0 ||
-      coll > 2) {
+      coll > 4 || coll == 3) {
     set_error("bad simulate arguments");
     return FLEXAR_ERR_INVALID;
   }
@@ -229,7 +229,7 @@ int flexar_simulate_coll(int coll, const char* spec, int nranks, size_t count, i
     if (!pl.build_coll((Coll)coll, s, count, &progs[r], &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
   }
   if (grid % progs[0].nchan) { set_error("grid must be a multiple of the channel count"); return FLEXAR_ERR_INVALID; }
-  return dispatch_dtype_op<SimRun>(dtype, coll == 2 ? FLEXAR_SUM : op, progs, nranks, grid, ncalls, 0, inputs,
+  return dispatch_dtype_op<SimRun>(dtype, (coll == 2 || coll == 4) ? FLEXAR_SUM : op, progs, nranks, grid, ncalls, 0, inputs,
                                    outputs, count);
 }
 

@@ -908,6 +908,15 @@ int flexar_all_gather(flexar_comm_t c, const void* in, void* out, size_t count, 
   return run_rs_ag(c, Coll::ALL_GATHER, in, out, count, dtype, FLEXAR_SUM, (hipStream_t)stream, algo, 1.0f);
 }
 
+int flexar_all_to_all(flexar_comm_t c, const void* in, void* out, size_t count, int dtype, void* stream) {
+  int rc = validate_call(c, dtype, FLEXAR_SUM, 1.0f);
+  if (rc) return rc;
+  if (!in || !out || in == out) { set_error("all_to_all needs distinct send/recv buffers"); return FLEXAR_ERR_INVALID; }
+  if ((rc = check_err(c))) return rc;
+  if (count == 0) return 0;
+  return run_rs_ag(c, Coll::ALL_TO_ALL, in, out, count, dtype, FLEXAR_SUM, (hipStream_t)stream, nullptr, 1.0f);
+}
+
 int flexar_broadcast(flexar_comm_t c, const void* in, void* out, size_t count, int dtype, int root, void* stream,
                      const char* algo) {
   int rc = validate_call(c, dtype, FLEXAR_SUM, 1.0f);
@@ -1040,8 +1049,8 @@ int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
 // Reduce-scatter / all-gather for an in-process group (tests): one launch, every rank of the group.
 int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const void* const* ins, void* const* outs,
                             size_t count, int dtype, int op, void* stream, const char* algo) {
-  if (!comms || nranks < 1 || (coll != 1 && coll != 2)) return FLEXAR_ERR_INVALID;
-  if (coll == 2) op = FLEXAR_SUM;
+  if (!comms || nranks < 1 || (coll != 1 && coll != 2 && coll != 4)) return FLEXAR_ERR_INVALID;
+  if (coll == 2 || coll == 4) op = FLEXAR_SUM;
   for (int r = 0; r < nranks; ++r) {
     int rc = validate_call(comms[r], dtype, op, 1.0f);
     if (rc) return rc;

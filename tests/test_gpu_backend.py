@@ -146,13 +146,18 @@ def _colls(rank, world, port, q):
         rso = [torch.empty(4, device=dev), torch.empty(2, device=dev)]
         pg.reduce_scatter_tensor_coalesced(rso, rsi).wait()
         e7 = max((rso[0] - sum(r + 1 for r in range(world))).abs().max().item(), (rso[1] - world).abs().max().item())
+        a2i = torch.arange(world * 5, device=dev, dtype=torch.float32) + 100 * rank
+        a2o = torch.empty_like(a2i)
+        dist.all_to_all_single(a2o, a2i)
+        want_a2 = torch.cat([torch.arange(rank * 5, rank * 5 + 5, device=dev).float() + 100 * r for r in range(world)])
+        e9 = (a2o - want_a2).abs().max().item()
         bc = torch.arange(100003, device=dev, dtype=torch.float32) * (rank + 1)
         dist.broadcast(bc, src=1)
         e8 = (bc - torch.arange(100003, device=dev).float() * 2).abs().max().item()
         torch.cuda.synchronize()
         used = dist.group.WORLD.stats["flexar_allreduce"]
         dist.destroy_process_group()
-        q.put((rank, max(e1, e2, e3, e4, e5, e6, e7, e8), used, None))
+        q.put((rank, max(e1, e2, e3, e4, e5, e6, e7, e8, e9), used, None))
     except Exception:
         import traceback
 
@@ -173,7 +178,7 @@ def test_backend_reduce_scatter_all_gather(cuda):
         p.join(60)
     for rank, err, used, tb in res:
         assert tb is None, tb
-        assert err == 0.0 and used >= 8, (rank, err, used)
+        assert err == 0.0 and used >= 9, (rank, err, used)
 
 
 def test_rccl_algo_routing_single_rank():

@@ -333,3 +333,23 @@ def test_fp8_compression_kernels(cuda, dtype, n):
     assert torch.equal(y, want_y)
     # the round trip is within e4m3's half-step of the largest value
     assert (y.float() - x.float()).abs().max().item() <= amax.max().item() * 2 ** -4 + 1e-6
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_group_all_to_all(cuda, groups, n):
+    grp = groups[n]
+    g = torch.Generator(device=cuda).manual_seed(61)
+    for dtype in (torch.float32, torch.bfloat16, torch.int8):
+        for m in (1, 37, 100003):
+            for it in range(2):  # consecutive calls: both staging halves
+                if dtype == torch.int8:
+                    ins = [torch.randint(-100, 100, (n * m,), device=cuda, generator=g, dtype=dtype) for _ in range(n)]
+                else:
+                    ins = [torch.randn(n * m, device=cuda, generator=g).to(dtype) for _ in range(n)]
+                outs = [torch.empty_like(x) for x in ins]
+                grp.collective("all_to_all", ins, outs)
+                torch.cuda.synchronize()
+                for p in range(n):
+                    want = torch.cat([ins[r][p * m:(p + 1) * m] for r in range(n)])
+                    assert torch.equal(outs[p], want), (dtype, m, p)
+    grp.check()

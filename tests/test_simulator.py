@@ -180,3 +180,15 @@ def test_broadcast(nv, n, spec):
             outs = nv.simulate_bcast(spec, data, n, root=root, grid=3, ncalls=3)
             for r, o in enumerate(outs):
                 np.testing.assert_array_equal(o, data, err_msg=f"{spec} n={n} size={size} root={root} r={r}")
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 8])
+def test_all_to_all(nv, n):
+    """Equal-split all-to-all: block p of rank r's input lands in block r of rank p's output."""
+    rng = np.random.default_rng(n)
+    for m in (1, 7, 1001, 4099):
+        ins = [rng.integers(-1000, 1000, n * m).astype(np.int32) for _ in range(n)]
+        outs = nv.simulate_coll("all_to_all", "flat", ins, m, dtype="int32", grid=3, ncalls=3)
+        for p in range(n):
+            want = np.concatenate([ins[r][p * m:(p + 1) * m] for r in range(n)])
+            np.testing.assert_array_equal(outs[p], want, err_msg=f"n={n} m={m} p={p}")
