@@ -78,6 +78,7 @@ class FlexarProcessGroup(dist.ProcessGroup):
         # (DDP backward); the returned Work's CUDA-aware future makes the consumer stream wait on it
         self.async_stream = os.environ.get("FLEXAR_PG_SYNC_STREAM", "0") != "1"
         self._streams = {}
+        self.hierarchical = False
 
     # ------------------------------------------------------------------ plumbing
     def getBackendName(self):
@@ -93,10 +94,27 @@ class FlexarProcessGroup(dist.ProcessGroup):
         return f"FlexarProcessGroup(rank={self._rank}, size={self._world})"
 
     def comm(self, device: int | None = None) -> Communicator:
+        """The device communicator, created on first use. Ranks on several hosts (or FLEXAR_NODE_SIZE
+        virtual nodes) get the hierarchical one: flexar inside each node over xGMI, the fallback kind
+        (RCCL by default) across nodes on 1/L shards."""
         if self._comm is None:
+            import socket
+
+            from .hierarchical import HierarchicalCommunicator, node_size_from_hosts
+
             dev = torch.cuda.current_device() if device is None else device
-            self._comm = Communicator(device=dev, rank=self._rank, world_size=self._world,
-                                      exchange=store_exchange(self._store, self._rank, self._world, "flexar_comm"))
+            L = int(os.environ.get("FLEXAR_NODE_SIZE", "0") or 0)
+            if L <= 0:
+                hosts = store_exchange(self._store, self._rank, self._world, "flexar_hosts")(socket.gethostname().encode())
+                L = node_size_from_hosts(hosts)
+            if L >= self._world:
+                self._comm = Communicator(device=dev, rank=self._rank, world_size=self._world,
+                                          exchange=store_exchange(self._store, self._rank, self._world, "flexar_comm"))
+            else:
+                self._comm = HierarchicalCommunicator.from_store(
+                    self._store, self._rank, self._world, L, dev,
+                    cross_kind="gloo" if self._fallback_kind == "gloo" else "nccl", timeout=self._timeout)
+            self.hierarchical = L < self._world
         return self._comm
 
     def _fallback(self, tensors):
@@ -113,6 +131,12 @@ class FlexarProcessGroup(dist.ProcessGroup):
         return self._gloo
 
     # ------------------------------------------------------------------ allreduce (flexar)
+    def _flat_comm_ok(self, t):
+        """Collectives other than allreduce need one flexar communicator spanning every rank (one node);
+        creating it is collective, and every rank reaches this point in the same collective."""
+        self.comm(t.device.index)
+        return not self.hierarchical
+
     def _flexar_ok(self, tensors, opname):
         return (opname is not None and all(t.is_cuda and t.is_contiguous() and t.dtype in _FLEXAR_DTYPES
                                            for t in tensors)
@@ -176,7 +200,7 @@ class FlexarProcessGroup(dist.ProcessGroup):
     def broadcast(self, tensor_list, opts=BroadcastOptions()):
         """DDP's initial parameter/buffer sync and model-state broadcasts: flexar direct multicast (small) or
         scatter + all-gather (large) from the root."""
-        if len(tensor_list) == 1 and self._flexar_ok(tensor_list, "sum"):
+        if len(tensor_list) == 1 and self._flexar_ok(tensor_list, "sum") and self._flat_comm_ok(tensor_list[0]):
             t = tensor_list[0]
             root = opts.rootRank
             return self._on_side([t], lambda c: c.broadcast(t.view(torch.uint8) if t.dtype == torch.bool else t,
@@ -188,7 +212,8 @@ class FlexarProcessGroup(dist.ProcessGroup):
         if len(input_tensor) == 1 and len(output_tensors) == 1 and len(output_tensors[0]) == self._world:
             inp, outs = input_tensor[0], output_tensors[0]
             if all(o.numel() == inp.numel() and o.dtype == inp.dtype and o.device == inp.device for o in outs) \
-                    and self._flexar_ok([inp] + list(outs), "sum") and inp.dtype != torch.bool:
+                    and self._flexar_ok([inp] + list(outs), "sum") and inp.dtype != torch.bool \
+                    and self._flat_comm_ok(inp):
                 def run(c):
                     flat = torch.empty(inp.numel() * self._world, dtype=inp.dtype, device=inp.device)
                     c.all_gather(inp.contiguous().reshape(-1), flat)
@@ -199,18 +224,18 @@ class FlexarProcessGroup(dist.ProcessGroup):
 
     def _allgather_base(self, output_tensor, input_tensor, opts=AllgatherOptions()):
         if self._flexar_ok([input_tensor, output_tensor], "sum") and input_tensor.dtype != torch.bool and \
-                output_tensor.numel() == input_tensor.numel() * self._world:
+                output_tensor.numel() == input_tensor.numel() * self._world and self._flat_comm_ok(input_tensor):
             return self._on_side([input_tensor, output_tensor], lambda c: c.all_gather(input_tensor, output_tensor),
                                  [output_tensor])
         return self._fallback([input_tensor])._allgather_base(output_tensor, input_tensor, opts)
 
     def _ag_ok(self, inp, out):
         return self._flexar_ok([inp, out], "sum") and inp.dtype != torch.bool and out.dtype == inp.dtype and \
-            out.numel() == inp.numel() * self._world
+            out.numel() == inp.numel() * self._world and self._flat_comm_ok(inp)
 
     def _rs_ok(self, out, inp, opname):
         return self._flexar_ok([inp, out], opname) and inp.dtype != torch.bool and out.dtype == inp.dtype and \
-            inp.numel() == out.numel() * self._world
+            inp.numel() == out.numel() * self._world and self._flat_comm_ok(inp)
 
     def allgather_into_tensor_coalesced(self, output_tensors, input_tensors, opts=AllgatherOptions()):
         """FSDP2's all-gather of many parameter shards: one flexar all-gather per pair, all on the side stream."""
@@ -232,7 +257,8 @@ class FlexarProcessGroup(dist.ProcessGroup):
         if len(output_tensors) == 1 and len(input_tensors) == 1 and len(input_tensors[0]) == self._world:
             out, chunks = output_tensors[0], input_tensors[0]
             if all(c.numel() == out.numel() and c.dtype == out.dtype and c.device == out.device for c in chunks) \
-                    and self._flexar_ok([out] + list(chunks), opname) and out.dtype != torch.bool:
+                    and self._flexar_ok([out] + list(chunks), opname) and out.dtype != torch.bool \
+                    and self._flat_comm_ok(out):
                 def run(c):
                     flat = torch.cat([t.reshape(-1) for t in chunks])
                     res = torch.empty(out.numel(), dtype=out.dtype, device=out.device)
@@ -244,7 +270,7 @@ class FlexarProcessGroup(dist.ProcessGroup):
     def _reduce_scatter_base(self, output_tensor, input_tensor, opts=ReduceScatterOptions()):
         opname = _redop_name(opts.reduceOp)
         if self._flexar_ok([input_tensor, output_tensor], opname) and input_tensor.dtype != torch.bool and \
-                input_tensor.numel() == output_tensor.numel() * self._world:
+                input_tensor.numel() == output_tensor.numel() * self._world and self._flat_comm_ok(input_tensor):
             return self._on_side([input_tensor, output_tensor],
                                  lambda c: c.reduce_scatter(input_tensor, output_tensor, op=opname), [output_tensor])
         return self._fallback([input_tensor])._reduce_scatter_base(output_tensor, input_tensor, opts)
@@ -283,7 +309,8 @@ class FlexarProcessGroup(dist.ProcessGroup):
         run the flexar direct exchange; uneven splits go to the fallback group."""
         equal = not output_split_sizes and not input_split_sizes
         if equal and self._flexar_ok([input, output], "sum") and input.dtype != torch.bool and \
-                input.numel() == output.numel() and input.numel() % self._world == 0 and input.dtype == output.dtype:
+                input.numel() == output.numel() and input.numel() % self._world == 0 and input.dtype == output.dtype \
+                and self._flat_comm_ok(input):
             return self._on_side([input, output], lambda c: c.all_to_all(input.reshape(-1), output.view(-1)), [output])
         return self._fallback([input]).alltoall_base(output, input, output_split_sizes, input_split_sizes, opts)
 

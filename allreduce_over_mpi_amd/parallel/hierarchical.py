@@ -25,6 +25,15 @@ from .. import _native as nv
 from .comm import Communicator
 
 
+def node_size_from_hosts(hosts) -> int:
+    """Ranks per node from every rank's hostname: contiguous, equal-sized blocks of ranks per host."""
+    world = len(hosts)
+    L = hosts.count(hosts[0])
+    if world % L or any(hosts[i] != hosts[(i // L) * L] for i in range(world)) or len(set(hosts)) != world // L:
+        raise nv.FlexarError(1, "hierarchical allreduce needs contiguous, equal-sized blocks of ranks per host")
+    return L
+
+
 def _node_size(group, world: int) -> int:
     import torch.distributed as dist
 
@@ -33,20 +42,29 @@ def _node_size(group, world: int) -> int:
         return env
     hosts = [None] * world
     dist.all_gather_object(hosts, socket.gethostname(), group=group)
-    L = hosts.count(hosts[0])
-    if world % L or any(hosts[i] != hosts[(i // L) * L] for i in range(world)) or len(set(hosts)) != world // L:
-        raise nv.FlexarError(1, "hierarchical allreduce needs contiguous, equal-sized blocks of ranks per host")
-    return L
+    return node_size_from_hosts(hosts)
 
 
 class HierarchicalCommunicator:
-    """Allreduce over ``group`` (default: WORLD) as intra-node flexar RS -> cross-node allreduce -> AG."""
+    """Allreduce over ``group`` (default: WORLD) as intra-node flexar RS -> cross-node allreduce -> AG.
+
+    ``cross_pg``: the cross-node group as a c10d ProcessGroup (the backend builds it from its Store);
+    by default it is created with ``torch.distributed.new_group`` (``cross_backend``)."""
 
     def __init__(self, group=None, node_size: Optional[int] = None, workspace_bytes: int = 0,
-                 cross_backend: Optional[str] = None):
+                 cross_backend: Optional[str] = None, *, _parts=None):
         import torch
         import torch.distributed as dist
 
+        self._torch = torch
+        self._dist = dist
+        if _parts is not None:  # from_store()
+            (self.rank, self.world, self.L, self.local, self.cross_pg, self.cross_on_host) = _parts
+            self.world_size = self.world
+            self.nodes = self.world // self.L
+            self.local_rank, self.node = self.rank % self.L, self.rank // self.L
+            self.group = self.local_group = self.cross_group = None
+            return
         self.group = group
         ranks = dist.get_process_group_ranks(group or dist.group.WORLD)
         self.world = self.world_size = len(ranks)
@@ -66,23 +84,51 @@ class HierarchicalCommunicator:
             g = dist.new_group(ranks[l::L], backend=cross_backend)
             if l == self.local_rank:
                 self.cross_group = g
+        self.cross_pg = None
         self.cross_on_host = (cross_backend or dist.get_backend(group)) == "gloo"
         self.local = Communicator(group=self.local_group, workspace_bytes=workspace_bytes)
-        self._torch = torch
-        self._dist = dist
+
+    @classmethod
+    def from_store(cls, store, rank: int, world: int, node_size: int, device: int, cross_kind: str = "nccl",
+                   workspace_bytes: int = 0, timeout=None):
+        """Build from a c10d Store (no torch.distributed default group needed): the node's flexar
+        communicator bootstraps through a node-prefixed Store, the cross-node group is a ProcessGroupNCCL
+        (RCCL) or ProcessGroupGloo over a prefixed Store, ranked by node index."""
+        import datetime
+
+        import torch.distributed as dist
+
+        from .comm import store_exchange
+
+        L = node_size
+        if L < 1 or world % L:
+            raise nv.FlexarError(1, f"node size {L} does not divide the world size {world}")
+        node, lr, nodes = rank // L, rank % L, world // L
+        local = Communicator(device=device, rank=lr, world_size=L, workspace_bytes=workspace_bytes,
+                             exchange=store_exchange(dist.PrefixStore(f"flexar_node{node}/", store), lr, L, "comm"))
+        cstore = dist.PrefixStore(f"flexar_cross{lr}/", store)
+        if cross_kind == "gloo":
+            cross = dist.ProcessGroupGloo(cstore, node, nodes, timeout or datetime.timedelta(minutes=10))
+        else:
+            cross = dist.ProcessGroupNCCL(cstore, node, nodes, dist.ProcessGroupNCCL.Options())
+        return cls(_parts=(rank, world, L, local, cross, cross_kind == "gloo"))
 
     def _cross_all_reduce(self, t, op: str):
         if self.nodes == 1:
             return t
         dist = self._dist
         rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN,
-               "prod": dist.ReduceOp.PRODUCT}[op]
-        if self.cross_on_host:  # gloo moves host tensors
-            h = t.cpu()
-            dist.all_reduce(h, op=rop, group=self.cross_group)
-            t.copy_(h)
+               "prod": dist.ReduceOp.PRODUCT, "band": dist.ReduceOp.BAND, "bor": dist.ReduceOp.BOR,
+               "bxor": dist.ReduceOp.BXOR}[op]
+        h = t.cpu() if self.cross_on_host else t  # gloo moves host tensors
+        if self.cross_pg is not None:
+            o = dist.AllreduceOptions()
+            o.reduceOp = rop
+            self.cross_pg.allreduce([h], o).wait()
         else:
-            dist.all_reduce(t, op=rop, group=self.cross_group)
+            dist.all_reduce(h, op=rop, group=self.cross_group)
+        if h is not t:
+            t.copy_(h)
         return t
 
     def all_reduce(self, tensor, op: str = "sum", out=None, algo: Optional[str] = None):

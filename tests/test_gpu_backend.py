@@ -212,3 +212,55 @@ print("rccl routing ok")
     env = dict(os.environ, PORT=str(_port()), PYTHONPATH=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "rccl routing ok" in r.stdout, r.stdout + r.stderr
+
+
+def _hier_backend(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
+                          FLEXAR_PG_FALLBACK="gloo", FLEXAR_TIMEOUT_MS="20000", FLEXAR_NODE_SIZE="2")
+        import torch.distributed as dist
+
+        from allreduce_over_mpi_amd.parallel import backend as fb  # noqa: F401
+
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        dist.init_process_group("flexar", rank=rank, world_size=world)
+        errs = []
+        for n in (1, 7, 100003):
+            x = torch.arange(n, device=dev, dtype=torch.float32) + rank
+            dist.all_reduce(x)
+            want = torch.arange(n, device=dev).float() * world + sum(range(world))
+            errs.append((x - want).abs().max().item())
+            y = torch.full((n,), float(rank + 1), device=dev)
+            dist.all_reduce(y, op=dist.ReduceOp.MAX)
+            errs.append((y - world).abs().max().item())
+        b = torch.full((33,), float(rank), device=dev)
+        dist.broadcast(b, src=3)  # hierarchical communicator: broadcast takes the fallback group
+        errs.append((b - 3).abs().max().item())
+        pg = dist.group.WORLD
+        ok = pg.hierarchical and pg.stats["flexar_allreduce"] >= 6 and pg.stats["fallback"] >= 1
+        dist.destroy_process_group()
+        q.put((rank, max(errs), ok, None))
+    except Exception:
+        import traceback
+
+        q.put((rank, None, None, traceback.format_exc()))
+
+
+def test_backend_hierarchical_virtual_nodes(cuda):
+    """init_process_group("flexar") over 2 virtual nodes x 2 ranks: dist.all_reduce runs intra-node flexar
+    reduce-scatter / all-gather around a cross-node allreduce of the shards."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_hier_backend, args=(r, 4, port, q)) for r in range(4)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(4)]
+    for p in ps:
+        p.join(60)
+    for rank, err, ok, tb in res:
+        assert tb is None, tb
+        assert err == 0.0 and ok, (rank, err, ok)
