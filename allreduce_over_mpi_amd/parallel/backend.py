@@ -79,6 +79,7 @@ class FlexarProcessGroup(dist.ProcessGroup):
         self.async_stream = os.environ.get("FLEXAR_PG_SYNC_STREAM", "0") != "1"
         self._streams = {}
         self.hierarchical = False
+        self._grid = int(os.environ.get("FLEXAR_PG_GRID", "0") or 0)  # executor workgroups (0 = auto)
 
     # ------------------------------------------------------------------ plumbing
     def getBackendName(self):
@@ -115,6 +116,8 @@ class FlexarProcessGroup(dist.ProcessGroup):
                     self._store, self._rank, self._world, L, dev,
                     cross_kind="gloo" if self._fallback_kind == "gloo" else "nccl", timeout=self._timeout)
             self.hierarchical = L < self._world
+            if self._grid:
+                (self._comm.local if self.hierarchical else self._comm).set_grid(self._grid)
         return self._comm
 
     def _fallback(self, tensors):
@@ -353,11 +356,18 @@ register()
 class FlexarHookState:
     """State for :func:`flexar_allreduce_hook`: a flexar Communicator over the DDP process group."""
 
-    def __init__(self, process_group=None, algo: str | None = None, communicator: Communicator | None = None):
+    def __init__(self, process_group=None, algo: str | None = None, communicator: Communicator | None = None,
+                 grid: int | None = None):
+        """``grid``: workgroups per executor launch (default: one per 32 KiB, at most 256 = one per CU).
+        Gradient buckets are reduced while backward still runs; a smaller grid leaves CUs to the
+        backward kernels (the xGMI links, not the CUs, bound a bucket's allreduce)."""
         self.comm = communicator or Communicator(group=process_group)
         self.algo = algo
         self.calls = 0
         self._streams = {}
+        grid = grid if grid is not None else int(os.environ.get("FLEXAR_HOOK_GRID", "0") or 0)
+        if grid and hasattr(self.comm, "set_grid"):
+            self.comm.set_grid(grid)
 
     def stream(self, dev):
         s = self._streams.get(dev.index)
