@@ -27,6 +27,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstdio>
@@ -210,8 +211,12 @@ struct HostComm {
     MPI_Comm_size(local, &ls);
     MPI_Comm_split(comm, lr, rank, &cross);
     MPI_Comm_size(cross, &nodes);
+    // reduce threads per rank: FLEXAR_HOST_THREADS, else this rank's share of the node's hardware threads
+    // (the reference runs a fixed 14-thread OpenMP team per reduce call, mpi_mod.hpp:253, oversubscribing
+    // a node whenever more than one rank shares it). Calls below 1 MiB per thread stay single-threaded.
     const char* t = getenv("FLEXAR_HOST_THREADS");
-    threads = t ? atoi(t) : 1;
+    const int hw = (int)std::thread::hardware_concurrency();
+    threads = t ? atoi(t) : std::max(1, hw / std::max(1, ls));
     if (threads < 1) threads = 1;
     if (threads > (int)kHostMaxGrid) threads = kHostMaxGrid;
     if (threads > 1) pool.reset(new Pool(threads - 1));
