@@ -94,6 +94,22 @@ class FlexarProcessGroup(dist.ProcessGroup):
     def __repr__(self):
         return f"FlexarProcessGroup(rank={self._rank}, size={self._world})"
 
+    # c10d keeps a group's name in its registered C++ backends; a Python ProcessGroup has none, so the
+    # name torch assigns (and registers the group under) is kept here. DeviceMesh / FSDP2 look it up.
+    def _set_group_name(self, name):
+        self._flexar_group_name = name
+
+    @property
+    def group_name(self):
+        return getattr(self, "_flexar_group_name", "")
+
+    def _set_group_desc(self, desc):
+        self._flexar_group_desc = desc
+
+    @property
+    def group_desc(self):
+        return getattr(self, "_flexar_group_desc", "")
+
     def comm(self, device: int | None = None) -> Communicator:
         """The device communicator, created on first use. Ranks on several hosts (or FLEXAR_NODE_SIZE
         virtual nodes) get the hierarchical one: flexar inside each node over xGMI, the fallback kind
