@@ -1,0 +1,119 @@
+"""Online algorithm selection: measure the candidate schedules on THIS node and install the winners.
+
+The reference chooses its tree offline: a closed-form cost model (cost_model/CostModel.h:82-120) prints a
+structure and a human exports FT_TOPO. flexar's runtime selector starts from an xGMI alpha-beta-gamma model
+(csrc/include/flexar/cost_model.hpp) and can be overridden by a measured table (FLEXAR_TUNE_FILE, written
+offline by tools/flexar_tune.py). ``autotune`` does the measurement in-process, at start-up, on the
+actual communicator:
+
+    comm = Communicator()
+    table = autotune(comm)          # collective: every rank calls it with the same arguments
+    # comm.all_reduce(...) now uses the measured winner for each size class
+
+For every size (x4 steps) each candidate is checked against ``torch.distributed.all_reduce`` of the
+communicator's group on three consecutive calls with inputs x, x/2, x/4 (a stale staging line from either
+of the two previous calls would change the result), then timed; the slowest rank's time counts. A
+candidate that fails or times out on any rank is dropped and the communicator's protocol state is
+reset by a fresh epoch (the call itself is never left half-way: every rank synchronises first).
+"""
+from __future__ import annotations
+
+import math
+import time
+from typing import Optional, Sequence
+
+from .. import _native as nv
+
+
+def default_candidates(world: int, nbytes: int) -> list[str]:
+    c = ["ll", "oneshot", "oneshot+wt"] if nbytes <= (1 << 20) else (["oneshot"] if nbytes <= (8 << 20) else [])
+    c += ["flat+pull", "flat+push", "flat+pull+wt", "flat+push+wt", "flat+pull+nts", "flat+push+nts"]
+    maxc = len([d for d in range(1, world) if math.gcd(d, world) == 1])
+    c += ["ring", "ring+wt"] + [f"ring:{k}" for k in (2, 4) if k <= maxc]
+    if world > 2 and (world & (world - 1)) == 0:
+        c.append("rhd+pull")
+    if world >= 8 and world % 4 == 0:
+        c += [f"tree:4,{world // 4}+pull", f"tree:{world // 4},4+pull"]
+    if nbytes >= (1 << 20):
+        c.append("dma")
+    return c
+
+
+def autotune(comm, sizes: Optional[Sequence[int]] = None, dtype=None, candidates=None, iters: int = 0,
+             install: bool = True, verbose: bool = False) -> list[tuple[int, str, float]]:
+    """Measure and (``install``) apply a per-size algorithm table. Returns [(bytes, spec, busbw_GBps)].
+    ``sizes``: buffer bytes (default 4 KiB .. 256 MiB, x4). Collective over the communicator's group."""
+    import torch
+    import torch.distributed as dist
+
+    from ..utils.perf import busbw_gbps
+
+    world = comm.world_size
+    if world < 2:
+        return []
+    dtype = dtype or torch.float32
+    es = torch.tensor([], dtype=dtype).element_size()
+    sizes = list(sizes) if sizes else [4096 << (2 * k) for k in range(9)]
+    dev = torch.device("cuda", comm.device)
+    group = comm.group
+    host_ref = dist.get_backend(group) == "gloo"
+
+    def agree_max(v: float) -> float:
+        t = torch.tensor([v], dtype=torch.float64, device="cpu" if host_ref else dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        return float(t.item())
+
+    table = []
+    tol = {torch.float32: 1e-5, torch.bfloat16: 2e-2, torch.float16: 4e-3}.get(dtype, 1e-5) * 4 * math.sqrt(world)
+    for nbytes in sizes:
+        n = max(1, nbytes // es)
+        x = torch.randn(n, device=dev).to(dtype)
+        y = torch.empty_like(x)
+        ref = x.float().cpu() if host_ref else x.float()
+        dist.all_reduce(ref, group=group)
+        ref = ref.to(dev)
+        scale = float(ref.abs().max().item()) + 1e-6
+        reps = iters or max(3, min(100, int(2e8 // max(nbytes, 1))))
+        best, best_t = None, float("inf")
+        for spec in (candidates or default_candidates(world, n * es)):
+            failed, t = 0.0, float("inf")
+            try:
+                for sc in (1.0, 0.5, 0.25):
+                    xs = x if sc == 1.0 else (x.float() * sc).to(dtype)
+                    comm.all_reduce(xs, out=y, algo=spec)
+                    torch.cuda.synchronize()
+                    if float((y.float() - ref * sc).abs().max().item()) > tol * scale * sc:
+                        failed = 1.0
+                comm.check()
+                if agree_max(failed) == 0.0:
+                    torch.cuda.synchronize()
+                    dist.barrier(group=group)
+                    t0 = time.perf_counter()
+                    for _ in range(reps):
+                        comm.all_reduce(x, out=y, algo=spec)
+                    torch.cuda.synchronize()
+                    t = (time.perf_counter() - t0) / reps
+                    comm.check()
+            except nv.FlexarError:
+                failed = 1.0
+            if agree_max(failed) != 0.0:
+                if verbose and comm.rank == 0:
+                    print(f"[autotune] {n * es:>11d} B  {spec:16s} excluded (wrong or failed on a rank)", flush=True)
+                continue
+            t = agree_max(t)
+            if verbose and comm.rank == 0:
+                print(f"[autotune] {n * es:>11d} B  {spec:16s} {t * 1e6:10.2f} us  "
+                      f"busbw {busbw_gbps(n * es, t, world):8.1f} GB/s", flush=True)
+            if t < best_t:
+                best, best_t = spec, t
+        if best is not None:
+            table.append((n * es, best, round(busbw_gbps(n * es, best_t, world), 2)))
+        del x, y, ref
+    if install and table:
+        lines, prev = [], None
+        for nbytes, spec, _ in table:
+            if spec != prev:  # a row covers every size up to the next row
+                lines.append(f"{world} {nbytes} {spec}")
+                prev = spec
+        comm.set_tune_table("\n".join(lines))
+    return table

@@ -115,6 +115,17 @@ class Communicator:
     def set_grid(self, grid: int):
         nv.check(self._lib.flexar_comm_set_grid(self._h, int(grid), 0), "set_grid")
 
+    def set_tune_table(self, text: str):
+        """Install a measured "nranks bytes spec" table (FLEXAR_TUNE_FILE format); "" = cost model."""
+        nv.check(self._lib.flexar_comm_set_tune_table(self._h, text.encode()), "set_tune_table")
+
+    def autotune(self, **kw):
+        """Measure the candidate schedules on this node and install the winners (collective);
+        see :func:`allreduce_over_mpi_amd.parallel.autotune.autotune`."""
+        from .autotune import autotune
+
+        return autotune(self, **kw)
+
     def describe(self, count: int, dtype) -> str:
         b = ctypes.create_string_buffer(512)
         nv.check(self._lib.flexar_comm_describe(self._h, int(count), nv.dtype_code(dtype), b, 512), "describe")

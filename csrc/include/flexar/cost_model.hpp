@@ -111,6 +111,15 @@ struct TuneTable {
     if (!path || !*path) return false;
     std::ifstream f(path);
     if (!f) return false;
+    return parse(f);
+  }
+  // the same "nranks bytes spec" lines from memory (Communicator.autotune installs its measurements)
+  bool load_text(const char* text) {
+    if (!text) return false;
+    std::istringstream f(text);
+    return parse(f);
+  }
+  bool parse(std::istream& f) {
     std::string line;
     while (std::getline(f, line)) {
       if (line.empty() || line[0] == '#') continue;

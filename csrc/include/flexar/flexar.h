@@ -102,6 +102,9 @@ int flexar_comm_size(flexar_comm_t comm);
  */
 int flexar_comm_set_algo(flexar_comm_t comm, const char* spec);
 int flexar_comm_set_grid(flexar_comm_t comm, int grid_blocks, int block_threads); /* 0 = auto */
+/* Replace the communicator's measured tune table ("nranks bytes spec" lines, FLEXAR_TUNE_FILE format;
+ * a row covers sizes >= bytes). NULL or "" clears it (back to the cost model). */
+int flexar_comm_set_tune_table(flexar_comm_t comm, const char* text);
 
 /* sendbuf == NULL or sendbuf == recvbuf => in place. count is size_t (no 2^31 cap). */
 int flexar_allreduce(flexar_comm_t comm, const void* sendbuf, void* recvbuf, size_t count, int dtype,

@@ -727,6 +727,24 @@ int flexar_comm_destroy(flexar_comm_t c) {
 int flexar_comm_rank(flexar_comm_t c) { return c ? c->rank : -1; }
 int flexar_comm_size(flexar_comm_t c) { return c ? c->nranks : -1; }
 
+int flexar_comm_set_tune_table(flexar_comm_t c, const char* text) {
+  if (!c) return FLEXAR_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  TuneTable t;
+  if (text && *text) {
+    if (!t.load_text(text)) { set_error("tune table: no 'nranks bytes spec' lines"); return FLEXAR_ERR_INVALID; }
+    for (auto& n : t.rows)
+      for (auto& row : n.second) {
+        AlgoSpec s;
+        std::string err;
+        if (!parse_algo(row.second, c->nranks, &s, &err)) { set_error("tune table: " + err); return FLEXAR_ERR_INVALID; }
+      }
+  }
+  c->tune = t;
+  c->have_tune = !t.rows.empty();
+  return 0;
+}
+
 int flexar_comm_set_algo(flexar_comm_t c, const char* spec) {
   if (!c) return FLEXAR_ERR_INVALID;
   std::string err;

@@ -187,3 +187,56 @@ def test_hierarchical_allreduce_virtual_nodes(cuda):
         assert tb is None, tb
         for op, size, err in errs:
             assert err < 1e-4, (rank, op, size, err)
+
+
+def _autotune_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
+                          FLEXAR_TIMEOUT_MS="20000")
+        import torch.distributed as dist
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from allreduce_over_mpi_amd.parallel import Communicator
+
+        comm = Communicator(workspace_bytes=64 << 20)
+        table = comm.autotune(sizes=[4096, 1 << 20, 8 << 20], iters=3)
+        chosen = [comm.describe(b // 4, torch.float32).split(" ")[0] for b, _, _ in table]
+        torch.manual_seed(5)  # same input on every rank
+        x = torch.randn(300001, device="cuda")
+        y = comm.all_reduce(x.clone())
+        torch.cuda.synchronize()
+        err = (y.double().cpu() - x.double().cpu() * world).abs().max().item()
+        comm.set_tune_table("")  # back to the cost model
+        comm.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, (table, chosen, err), None))
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_autotune_installs_measured_table(cuda):
+    """Communicator.autotune: validated, max-over-ranks timings; the installed winners drive auto calls."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_autotune_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    tables = []
+    for rank, out, tb in res:
+        assert tb is None, tb
+        table, chosen, err = out
+        assert len(table) == 3 and err < 1e-4, (table, err)
+        for (b, spec, bw), ch in zip(table, chosen):  # describe() reports the installed choice ("flat" = tree:N)
+            assert ch == spec.replace("flat", "tree:2"), (spec, ch)
+        tables.append([s for _, s, _ in table])
+    assert tables[0] == tables[1]  # every rank installed the same table
