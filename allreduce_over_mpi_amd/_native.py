@@ -53,6 +53,7 @@ def _sig(lib):
         "flexar_allreduce": (i, [vp, vp, vp, sz, i, i, vp]),
         "flexar_allreduce_ex": (i, [vp, vp, vp, sz, i, i, vp, cp, f]),
         "flexar_comm_check": (i, [vp]),
+        "flexar_comm_clear_error": (i, [vp]),
         "flexar_comm_describe": (i, [vp, sz, i, cp, sz]),
         "flexar_comm_stats": (i, [vp, cp, sz]),
         "flexar_group_create": (i, [i, i, sz, c.POINTER(vp)]),

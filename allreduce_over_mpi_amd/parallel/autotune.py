@@ -13,8 +13,9 @@ actual communicator:
 For every size (x4 steps) each candidate is checked against ``torch.distributed.all_reduce`` of the
 communicator's group on three consecutive calls with inputs x, x/2, x/4 (a stale staging line from either
 of the two previous calls would change the result), then timed; the slowest rank's time counts. A
-candidate that fails or times out on any rank is dropped and the communicator's protocol state is
-reset by a fresh epoch (the call itself is never left half-way: every rank synchronises first).
+candidate that fails or times out on any rank is dropped; every rank has synchronised by then, so the
+recorded timeout is cleared (epochs advance once per call on every rank, aborted or not) and the
+measurement goes on with the same communicator.
 """
 from __future__ import annotations
 
@@ -26,10 +27,13 @@ from .. import _native as nv
 
 
 def default_candidates(world: int, nbytes: int) -> list[str]:
+    """The schedules worth measuring for ``nbytes`` on ``world`` ranks (bench.py, tools/flexar_tune.py and
+    ``autotune`` share this list): latency protocols for small buffers, every flat-stage protocol, rings
+    on 1..4 arc-disjoint channels, RHD, the two-stage FlexTree factorizations and the copy engines."""
     c = ["ll", "oneshot", "oneshot+wt"] if nbytes <= (1 << 20) else (["oneshot"] if nbytes <= (8 << 20) else [])
-    c += ["flat+pull", "flat+push", "flat+pull+wt", "flat+push+wt", "flat+pull+nts", "flat+push+nts"]
+    c += ["flat+pull", "flat+push", "flat+pull+nts", "flat+push+nts", "flat+pull+wt", "flat+push+wt"]
     maxc = len([d for d in range(1, world) if math.gcd(d, world) == 1])
-    c += ["ring", "ring+wt"] + [f"ring:{k}" for k in (2, 4) if k <= maxc]
+    c += ["ring", "ring+wt"] + [f"ring:{k}{m}" for k in (2, 4) if k <= maxc for m in ("", "+wt")]
     if world > 2 and (world & (world - 1)) == 0:
         c.append("rhd+pull")
     if world >= 8 and world % 4 == 0:
@@ -97,6 +101,8 @@ def autotune(comm, sizes: Optional[Sequence[int]] = None, dtype=None, candidates
             except nv.FlexarError:
                 failed = 1.0
             if agree_max(failed) != 0.0:
+                torch.cuda.synchronize()
+                comm.clear_error()  # every rank is here, nothing in flight: a timeout must not poison the rest
                 if verbose and comm.rank == 0:
                     print(f"[autotune] {n * es:>11d} B  {spec:16s} excluded (wrong or failed on a rank)", flush=True)
                 continue

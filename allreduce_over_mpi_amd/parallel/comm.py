@@ -134,6 +134,10 @@ class Communicator:
     def check(self):
         nv.check(self._lib.flexar_comm_check(self._h), "comm_check")
 
+    def clear_error(self):
+        """Forget a recorded watchdog timeout (call on every rank after all of them synchronised)."""
+        nv.check(self._lib.flexar_comm_clear_error(self._h), "comm_clear_error")
+
     def stats(self) -> dict:
         """Call/byte counters; per-algorithm device time when FLEXAR_PROFILE=1 (synchronises those events)."""
         import json
@@ -324,6 +328,10 @@ class LocalGroup:
     def check(self):
         for r in range(self.nranks):
             nv.check(self._lib.flexar_comm_check(self._comms[r]), f"rank {r}")
+
+    def clear_error(self):
+        for r in range(self.nranks):
+            nv.check(self._lib.flexar_comm_clear_error(self._comms[r]), f"rank {r}")
 
     def close(self):
         if getattr(self, "_comms", None) is not None:

@@ -213,14 +213,11 @@ def main():
     if fallback:
         algo = "rccl"
     elif world > 1 and algo == "auto" and not args.no_tune:
-        cands = ["flat+pull", "flat+push", "flat+pull+nts", "flat+push+nts", "flat+pull+wt", "flat+push+wt"]
-        maxc = len([d for d in range(1, world) if math.gcd(d, world) == 1])
-        cands += ["ring", "ring+wt"] + [f"ring:{c}{m}" for c in (2, 4, 8) if c <= maxc for m in ("", "+wt")]
-        if world > 2 and (world & (world - 1)) == 0:
-            cands += ["rhd+pull"]
-        if world >= 8 and world % 4 == 0:  # two-stage FlexTree factorizations (3 + 1 / 1 + 3 links per stage)
-            cands += [f"tree:4,{world // 4}+pull", f"tree:{world // 4},4+pull"]
-        cands += ["dma"]  # copy engines (CU-free)
+        from allreduce_over_mpi_amd.parallel.autotune import default_candidates
+
+        # flat-stage protocols, rings on 1..4 arc-disjoint channels, RHD, two-stage FlexTree factorizations,
+        # the copy engines (and the latency protocols for small buffers)
+        cands = default_candidates(world, nbytes)
         timings = {}
         for spec in cands:
             failed = 0.0

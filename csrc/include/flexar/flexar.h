@@ -133,6 +133,8 @@ int flexar_broadcast(flexar_comm_t comm, const void* sendbuf, void* recvbuf, siz
 /* Non-blocking health check: returns FLEXAR_ERR_TIMEOUT (and fills flexar_last_error)
  * if a device-side wait timed out in any previous call. */
 int flexar_comm_check(flexar_comm_t comm);
+/* Clear a recorded timeout once every rank has synchronised (collective use: all ranks call it). */
+int flexar_comm_clear_error(flexar_comm_t comm);
 /* JSON statistics (calls, bytes; per-algorithm device time when FLEXAR_PROFILE=1). */
 int flexar_comm_stats(flexar_comm_t comm, char* buf, size_t buflen);
 /* Describe the algorithm the communicator would run for (count, dtype). */

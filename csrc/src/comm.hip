@@ -761,6 +761,17 @@ int flexar_comm_set_grid(flexar_comm_t c, int grid_blocks, int block_threads) {
   return 0;
 }
 
+// After every rank has synchronised (no kernel of this communicator in flight anywhere), forget a
+// recorded watchdog timeout: epochs advance once per call on every rank even when a call aborts, and
+// flags only ever grow, so the next call starts from a consistent state (the autotuner's recovery).
+int flexar_comm_clear_error(flexar_comm_t c) {
+  if (!c) return FLEXAR_ERR_INVALID;
+  FX_HIP(hipSetDevice(c->device));
+  FX_HIP(hipDeviceSynchronize());
+  __atomic_store_n(c->err_host, 0u, __ATOMIC_RELEASE);
+  return 0;
+}
+
 int flexar_comm_check(flexar_comm_t c) {
   if (!c) return FLEXAR_ERR_INVALID;
   return check_err(c);

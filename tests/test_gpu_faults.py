@@ -68,6 +68,17 @@ def test_dropped_signal_times_out(cuda, monkeypatch):
             torch.cuda.synchronize()
             g.check()
         assert "timed out" in str(ei.value)
+        # recovery: once everything has synchronised, clearing the recorded timeout lets the same group
+        # run again (LL has no SIGNAL ops, so the injected drop does not apply to it)
+        torch.cuda.synchronize()
+        g.clear_error()
+        xs = [torch.randn(4096, device=cuda) for _ in range(4)]
+        outs = g.all_reduce([x.clone() for x in xs], algo="ll")
+        torch.cuda.synchronize()
+        g.check()
+        ref = torch.stack(xs).sum(0)
+        for o in outs:
+            torch.testing.assert_close(o, ref, rtol=1e-5, atol=1e-5)
     finally:
         g.close()
 

@@ -32,17 +32,9 @@ def parse_bytes(v: str) -> int:
 
 
 def candidates(world: int, nbytes: int) -> list[str]:
-    c = ["ll", "oneshot", "oneshot+wt"] if nbytes <= (1 << 20) else ["oneshot"] if nbytes <= (8 << 20) else []
-    c += ["flat+pull", "flat+push", "flat+pull+wt", "flat+push+wt", "flat+pull+nts"]
-    maxc = len([d for d in range(1, world) if math.gcd(d, world) == 1])
-    c += ["ring", "ring+wt"] + [f"ring:{k}" for k in (2, 4) if k <= maxc]
-    if world > 2 and (world & (world - 1)) == 0:
-        c += ["rhd+pull"]
-    if world >= 8 and world % 4 == 0:
-        c += [f"tree:4,{world // 4}+pull", f"tree:{world // 4},4+pull"]
-    if nbytes >= (1 << 20):
-        c += ["dma"]
-    return c
+    from allreduce_over_mpi_amd.parallel.autotune import default_candidates
+
+    return default_candidates(world, nbytes)
 
 
 def main():
