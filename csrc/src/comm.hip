@@ -143,9 +143,33 @@ struct flexar_comm {
   bool dma_ready = false;
   hipStream_t dma_st[kMaxRanks] = {};
   hipEvent_t dma_fork = nullptr, dma_join[kMaxRanks] = {};
+  // call ordering across streams: calls share epochs/staging, so two calls of one communicator must never
+  // run concurrently (NCCL semantics). A call on a new stream waits for everything enqueued so far on the
+  // previous call's stream (an event recorded lazily, only when the stream changes).
+  hipStream_t last_st = nullptr;
+  bool have_last = false;
+  hipEvent_t order_ev = nullptr;
+  bool unordered = false;  // FLEXAR_UNORDERED_CALLS=1: test-only, shows the race the ordering prevents
 };
 
 namespace flexar {
+
+// Serialise this call behind the communicator's previous call when it is issued on another stream.
+// Under graph capture the application's graph orders its nodes, and a wait on an event recorded
+// outside the capture is not allowed, so nothing is inserted.
+static int order_call(flexar_comm* c, hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) { (void)hipGetLastError(); cs = hipStreamCaptureStatusNone; }
+  if (cs != hipStreamCaptureStatusNone || c->unordered) return 0;
+  if (c->have_last && c->last_st != st) {
+    if (!c->order_ev) FX_HIP(hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming));
+    FX_HIP(hipEventRecord(c->order_ev, c->last_st));
+    FX_HIP(hipStreamWaitEvent(st, c->order_ev, 0));
+  }
+  c->last_st = st;
+  c->have_last = true;
+  return 0;
+}
 
 static int resolve_spec(flexar_comm* c, const char* algo, double bytes, AlgoSpec* out) {
   AlgoSpec s = c->spec;
@@ -313,6 +337,7 @@ static int run_rs_ag(flexar_comm* c, Coll coll, const void* in, void* out, size_
   if (rc) return rc;
   if (s.kind != AlgoKind::RING) s.kind = AlgoKind::TREE, s.widths = {c->nranks}, s.ag = AgMode::PUSH;
   std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = order_call(c, st))) return rc;
   uint64_t piece = count;
   if (c->nranks > 1 && (rc = plan_pieces(c, s, count, es, fs, &piece, coll, count))) return rc;
   for (uint64_t off = 0; off < count; off += piece) {
@@ -361,6 +386,7 @@ static int run_bcast(flexar_comm* c, const void* in, void* out, size_t count, in
   int rc = bcast_spec(c, algo, (uint64_t)count * es, &s);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = order_call(c, st))) return rc;
   uint64_t piece = count;
   if (c->nranks > 1 && (rc = plan_pieces(c, s, count, es, 1.0f, &piece, Coll::BROADCAST, (uint64_t)root))) return rc;
   for (uint64_t off = 0; off < count; off += piece) {
@@ -603,6 +629,7 @@ static void init_defaults(flexar_comm* c) {
   c->chunk_bytes = env_u64("FLEXAR_CHUNK_BYTES", 0);
   c->nchannels = (int)env_u64("FLEXAR_NCHANNELS", 0);
   c->profile = env_u64("FLEXAR_PROFILE", 0) != 0;
+  c->unordered = env_u64("FLEXAR_UNORDERED_CALLS", 0) != 0;
   if (!c->min_block_bytes) c->min_block_bytes = 1;
   // FLEXAR_FAULT_INJECT=delay:RANK:SLOT:MICROSECONDS | drop:RANK:SLOT  (tests / race hunting)
   if (const char* fi = getenv("FLEXAR_FAULT_INJECT")) {
@@ -716,6 +743,7 @@ int flexar_comm_destroy(flexar_comm_t c) {
     if (c->dma_join[r]) (void)hipEventDestroy(c->dma_join[r]);
   }
   if (c->dma_fork) (void)hipEventDestroy(c->dma_fork);
+  if (c->order_ev) (void)hipEventDestroy(c->order_ev);
   (void)hipFree(c->stg);
   (void)hipFree(c->flags);
   (void)hipFree(c->epochs);
@@ -813,6 +841,7 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
   const uint32_t es = (uint32_t)dtype_size(dtype);
   float fs = scale * (op == FLEXAR_AVG ? 1.0f / (float)c->nranks : 1.0f);
   std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = order_call(c, st))) return rc;
   AlgoSpec s;
   if ((rc = resolve_spec(c, algo, (double)count * es, &s))) return rc;
   if (s.kind == AlgoKind::LL && !ll_usable(c, count, es)) s.kind = AlgoKind::ONESHOT;

@@ -240,3 +240,78 @@ def test_autotune_installs_measured_table(cuda):
             assert ch == spec.replace("flat", "tree:2"), (spec, ch)
         tables.append([s for _, s, _ in table])
     assert tables[0] == tables[1]  # every rank installed the same table
+
+
+def _stress_worker(rank, world, port, calls, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
+                          FLEXAR_TIMEOUT_MS="20000")
+        import random
+
+        import torch.distributed as dist
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from allreduce_over_mpi_amd.parallel import Communicator
+
+        comm = Communicator(workspace_bytes=32 << 20)
+        specs = ["flat", "flat+push", "flat+wt", "flat+push+nts", "ring", "ring+wt", "oneshot", "ll", "dma",
+                 "rhd", "tree:2,2+push"] if world == 4 else ["flat", "flat+push+wt", "ring", "oneshot", "ll", "dma"]
+        rnd = random.Random(1234)  # same call sequence on every rank
+        side = torch.cuda.Stream()
+        main = torch.cuda.current_stream()
+        bad, pending = [], []
+        for it in range(calls):
+            spec = rnd.choice(specs)
+            n = rnd.choice([1, 5, 4096, 65537, 300001, 2_000_003])
+            in_place = rnd.random() < 0.5
+            use_side = rnd.random() < 0.5
+            # small integers in fp32: every summation order gives the exact same result
+            gen = torch.Generator().manual_seed(it)
+            allx = torch.randint(-8, 9, (world, n), generator=gen).float()
+            x = allx[rank].to("cuda")
+            out = None if in_place else torch.empty_like(x)
+            stream = side if use_side else main
+            stream.wait_stream(main)  # x and out were made on the main stream
+            # NO host synchronisation between calls: consecutive calls on different streams must still be
+            # serialised by the communicator (they share epochs and staging halves)
+            with torch.cuda.stream(stream):
+                busy = torch.randn(1 << 20, device="cuda").square_().sum()  # compute sharing the GPU
+                y = comm.all_reduce(x, out=out, algo=spec)
+            # keep x alive until the end: freed now, the caching allocator would hand its block to the next
+            # iteration (main stream) while this call may still read it on the side stream
+            pending.append((it, spec, n, in_place, use_side, y, allx.sum(0), (x, busy)))
+        torch.cuda.synchronize()
+        for it, spec, n, in_place, use_side, y, want, _ in pending:
+            if not torch.equal(y.cpu(), want):
+                bad.append((it, spec, n, in_place, use_side))
+        comm.check()
+        comm.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, bad, None))
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ipc_randomized_call_sequence(cuda, world):
+    """Processes on one GPU run the same random sequence of algorithms, sizes, in/out-of-place and streams
+    (with compute kernels sharing the GPU) with no host synchronisation between calls; every result is
+    checked exactly (integer-valued fp32)."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stress_worker, args=(r, world, port, 60, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, bad, tb in res:
+        assert tb is None, tb
+        assert not bad, (rank, bad[:5])
