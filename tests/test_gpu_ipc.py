@@ -268,19 +268,47 @@ def _stress_worker(rank, world, port, calls, q):
             use_side = rnd.random() < 0.5
             # small integers in fp32: every summation order gives the exact same result
             gen = torch.Generator().manual_seed(it)
-            allx = torch.randint(-8, 9, (world, n), generator=gen).float()
-            x = allx[rank].to("cuda")
+            allx = torch.randint(-8, 9, (world, max(n, world)), generator=gen).float()[:, :max(n, world)]
+            x = allx[rank][:n].to("cuda")
             out = None if in_place else torch.empty_like(x)
+            coll = rnd.choice(["allreduce"] * 4 + ["broadcast", "all_to_all", "reduce_scatter", "all_gather"])
+            m = max(1, n // world)
             stream = side if use_side else main
+            if coll == "allreduce":
+                want = allx[:, :n].sum(0)
+            elif coll == "broadcast":
+                root = it % world
+                want = allx[root][:n]
+            elif coll == "all_to_all":
+                x = allx[rank][:m * world].to("cuda")
+                out = torch.empty_like(x)
+                want = torch.cat([allx[r][rank * m:(rank + 1) * m] for r in range(world)])
+            elif coll == "reduce_scatter":
+                x = allx[rank][:m * world].to("cuda")
+                out = torch.empty(m, device="cuda")
+                want = allx[:, rank * m:(rank + 1) * m].sum(0)
+            else:  # all_gather
+                x = allx[rank][:m].to("cuda")
+                out = torch.empty(m * world, device="cuda")
+                want = allx[:, :m].reshape(-1)
             stream.wait_stream(main)  # x and out were made on the main stream
             # NO host synchronisation between calls: consecutive calls on different streams must still be
-            # serialised by the communicator (they share epochs and staging halves)
+            # serialised by the communicator (every collective shares the epochs and staging halves)
             with torch.cuda.stream(stream):
                 busy = torch.randn(1 << 20, device="cuda").square_().sum()  # compute sharing the GPU
-                y = comm.all_reduce(x, out=out, algo=spec)
+                if coll == "allreduce":
+                    y = comm.all_reduce(x, out=out, algo=spec)
+                elif coll == "broadcast":
+                    y = comm.broadcast(x, root=root, out=out)
+                elif coll == "all_to_all":
+                    y = comm.all_to_all(x, out)
+                elif coll == "reduce_scatter":
+                    y = comm.reduce_scatter(x, out, algo="ring" if "ring" in spec else None)
+                else:
+                    y = comm.all_gather(x, out, algo="ring" if "ring" in spec else None)
             # keep x alive until the end: freed now, the caching allocator would hand its block to the next
             # iteration (main stream) while this call may still read it on the side stream
-            pending.append((it, spec, n, in_place, use_side, y, allx.sum(0), (x, busy)))
+            pending.append((it, coll + ":" + spec, n, in_place, use_side, y, want, (x, busy)))
         torch.cuda.synchronize()
         for it, spec, n, in_place, use_side, y, want, _ in pending:
             if not torch.equal(y.cpu(), want):
@@ -298,7 +326,8 @@ def _stress_worker(rank, world, port, calls, q):
 
 @pytest.mark.parametrize("world", [2, 4])
 def test_ipc_randomized_call_sequence(cuda, world):
-    """Processes on one GPU run the same random sequence of algorithms, sizes, in/out-of-place and streams
+    """Processes on one GPU run the same random sequence of collectives (allreduce with every algorithm,
+    broadcast, all-to-all, reduce-scatter, all-gather), sizes, in/out-of-place and streams
     (with compute kernels sharing the GPU) with no host synchronisation between calls; every result is
     checked exactly (integer-valued fp32)."""
     import torch.multiprocessing as mp
@@ -306,7 +335,7 @@ def test_ipc_randomized_call_sequence(cuda, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_stress_worker, args=(r, world, port, 60, q)) for r in range(world)]
+    procs = [ctx.Process(target=_stress_worker, args=(r, world, port, 80, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
