@@ -242,10 +242,12 @@ def test_autotune_installs_measured_table(cuda):
     assert tables[0] == tables[1]  # every rank installed the same table
 
 
-def _stress_worker(rank, world, port, calls, q):
+def _stress_worker(rank, world, port, calls, q, fault=""):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
                           FLEXAR_TIMEOUT_MS="20000")
+        if fault:
+            os.environ["FLEXAR_FAULT_INJECT"] = fault
         import random
 
         import torch.distributed as dist
@@ -324,8 +326,8 @@ def _stress_worker(rank, world, port, calls, q):
         q.put((rank, None, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_ipc_randomized_call_sequence(cuda, world):
+@pytest.mark.parametrize("world,fault", [(2, ""), (4, ""), (4, "delay:1:0:200")])
+def test_ipc_randomized_call_sequence(cuda, world, fault):
     """Processes on one GPU run the same random sequence of collectives (allreduce with every algorithm,
     broadcast, all-to-all, reduce-scatter, all-gather), sizes, in/out-of-place and streams
     (with compute kernels sharing the GPU) with no host synchronisation between calls; every result is
@@ -335,7 +337,7 @@ def test_ipc_randomized_call_sequence(cuda, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_stress_worker, args=(r, world, port, 80, q)) for r in range(world)]
+    procs = [ctx.Process(target=_stress_worker, args=(r, world, port, 80, q, fault)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
