@@ -43,11 +43,43 @@ def _deps():
     return (glob.glob(os.path.join(INCLUDE, "flexar", "*")) + glob.glob(os.path.join(CSRC, "src", "*")))
 
 
+def _fastcall_paths():
+    import sysconfig
+
+    src = os.path.join(CSRC, "python", "fastcall.c")
+    out = os.path.join(LIB_DIR, "_fastcall" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+    return src, out
+
+
+FASTCALL_PATH = _fastcall_paths()[1]
+
+
+def _fastcall_stale() -> bool:
+    src, out = _fastcall_paths()
+    return not os.path.exists(out) or os.path.getmtime(src) > os.path.getmtime(out)
+
+
 def needs_build() -> bool:
-    if not os.path.exists(LIB_PATH):
+    if not os.path.exists(LIB_PATH) or _fastcall_stale():
         return True
     t = os.path.getmtime(LIB_PATH)
     return any(os.path.getmtime(d) > t for d in _deps())
+
+
+def build_fastcall(verbose: bool = False) -> str:
+    """The CPython fast-call module (csrc/python/fastcall.c): plain C against the Python headers, no
+    link against libflexar.so (it receives the entry points' addresses at import)."""
+    import sysconfig
+
+    src, out = _fastcall_paths()
+    os.makedirs(LIB_DIR, exist_ok=True)
+    tmp = out + ".tmp"
+    _run([os.environ.get("CC", "gcc"), "-O2", "-shared", "-fPIC", "-Wall", "-I" + sysconfig.get_paths()["include"],
+          src, "-o", tmp])
+    os.replace(tmp, out)
+    if verbose:
+        print("built", out)
+    return out
 
 
 def _run(cmd):
@@ -58,7 +90,9 @@ def _run(cmd):
 
 
 def build(verbose: bool = False, force: bool = False) -> str:
-    """Compile libflexar.so in-tree; returns its path."""
+    """Compile libflexar.so (and the fast-call module) in-tree; returns the library's path."""
+    if force or _fastcall_stale():
+        build_fastcall(verbose)
     if not force and not needs_build():
         return LIB_PATH
     os.makedirs(BUILD_DIR, exist_ok=True)

@@ -104,8 +104,32 @@ def lib():
                 raise FlexarError(5, f"native library missing: {path} (run __graft_entry__.build())")
             l = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
             _sig(l)
+            _load_fastcall(l)
             _lib = l
     return _lib
+
+
+# Fast-call path (csrc/python/fastcall.c): the per-step collectives bypass ctypes' argument conversion.
+# FAST is the module (None if it was not built) and AR/RS/AG the C entry points' addresses.
+FAST = None
+AR = RS = AG = 0
+
+
+def _load_fastcall(l):
+    global FAST, AR, RS, AG
+    import importlib.machinery
+    import importlib.util
+
+    p = _build.FASTCALL_PATH
+    if not os.path.exists(p):
+        return
+    loader = importlib.machinery.ExtensionFileLoader("_fastcall", p)
+    spec = importlib.util.spec_from_file_location("_fastcall", p, loader=loader)
+    m = importlib.util.module_from_spec(spec)
+    loader.exec_module(m)
+    addr = lambda f: ctypes.cast(f, ctypes.c_void_p).value  # noqa: E731
+    AR, RS, AG = addr(l.flexar_allreduce_ex), addr(l.flexar_reduce_scatter), addr(l.flexar_all_gather)
+    FAST = m
 
 
 def last_error() -> str:

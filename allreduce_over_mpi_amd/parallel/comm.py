@@ -20,11 +20,60 @@ from typing import Optional, Sequence
 from .. import _native as nv
 
 
-def _stream_handle(stream=None) -> int:
+def _raw_stream_fn():
     import torch
 
-    s = stream if stream is not None else torch.cuda.current_stream()
-    return int(s.cuda_stream)
+    f = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+    return f if f is not None else (lambda dev: torch.cuda.current_stream(dev).cuda_stream)
+
+
+_RAW_STREAM = None
+
+
+def _stream_handle(stream=None, device: Optional[int] = None) -> int:
+    """hipStream_t of ``stream``, else of the current stream of ``device`` (default: current device)."""
+    global _RAW_STREAM
+    if stream is not None:
+        return int(stream.cuda_stream)
+    if _RAW_STREAM is None:
+        _RAW_STREAM = _raw_stream_fn()
+    if device is None:
+        import torch
+
+        device = torch.cuda.current_device()
+    return int(_RAW_STREAM(device))
+
+
+# per-call enum lookups, memoised by the (hashable) dtype / op objects the callers pass
+_DT_CODES: dict = {}
+_OP_CODES: dict = {}
+
+
+def _dt(dtype) -> int:
+    c = _DT_CODES.get(dtype)
+    if c is None:
+        c = _DT_CODES[dtype] = nv.dtype_code(dtype)
+    return c
+
+
+def _op(op) -> int:
+    try:
+        c = _OP_CODES.get(op)
+    except TypeError:  # unhashable op object
+        return nv.op_code(op)
+    if c is None:
+        c = _OP_CODES[op] = nv.op_code(op)
+    return c
+
+
+_ALGO_BYTES: dict = {None: None}
+
+
+def _algo(algo: Optional[str]):
+    b = _ALGO_BYTES.get(algo)
+    if b is None and algo is not None:
+        b = _ALGO_BYTES[algo] = algo.encode() if algo else None
+    return b
 
 
 def _require_cuda(t, what="tensor"):
@@ -60,6 +109,7 @@ class Communicator:
             nv.check(self._lib.flexar_comm_create(self.rank, self.world_size, self.device, int(workspace_bytes),
                                                   ctypes.byref(h)), "comm_create")
         self._h = h
+        self._hi = int(h.value or 0)  # the handle as an int, for the fast-call path
         if self.world_size > 1:
             hs = int(self._lib.flexar_handle_size())
             buf = ctypes.create_string_buffer(hs)
@@ -157,10 +207,14 @@ class Communicator:
             _require_cuda(out, "out")
             if out.numel() != tensor.numel() or out.dtype != tensor.dtype:
                 raise nv.FlexarError(1, "out must match tensor in size and dtype")
-        rc = self._lib.flexar_allreduce_ex(self._h, tensor.data_ptr(), dst.data_ptr(), tensor.numel(),
-                                           nv.dtype_code(tensor.dtype), nv.op_code(op), _stream_handle(stream),
-                                           algo.encode() if algo else None, float(scale))
-        nv.check(rc, "allreduce")
+        args = (tensor.data_ptr(), dst.data_ptr(), tensor.numel(), _dt(tensor.dtype), _op(op),
+                _stream_handle(stream, self.device), _algo(algo))
+        if nv.FAST is not None:
+            rc = nv.FAST.ar(nv.AR, self._hi, *args, float(scale))
+        else:
+            rc = self._lib.flexar_allreduce_ex(self._h, *args, float(scale))
+        if rc:
+            nv.check(rc, "allreduce")
         return dst
 
     def reduce_scatter(self, input, output, op="sum", algo: Optional[str] = None, stream=None):
@@ -169,9 +223,12 @@ class Communicator:
         _require_cuda(output, "output")
         if input.numel() != output.numel() * self.world_size or input.dtype != output.dtype:
             raise nv.FlexarError(1, "input must hold world_size * output.numel() elements of output's dtype")
-        nv.check(self._lib.flexar_reduce_scatter(self._h, input.data_ptr(), output.data_ptr(), output.numel(),
-                                                 nv.dtype_code(output.dtype), nv.op_code(op), _stream_handle(stream),
-                                                 algo.encode() if algo else None), "reduce_scatter")
+        args = (input.data_ptr(), output.data_ptr(), output.numel(), _dt(output.dtype), _op(op),
+                _stream_handle(stream, self.device), _algo(algo))
+        rc = nv.FAST.rs(nv.RS, self._hi, *args) if nv.FAST is not None else \
+            self._lib.flexar_reduce_scatter(self._h, *args)
+        if rc:
+            nv.check(rc, "reduce_scatter")
         return output
 
     def all_gather(self, input, output, algo: Optional[str] = None, stream=None):
@@ -180,9 +237,12 @@ class Communicator:
         _require_cuda(output, "output")
         if output.numel() != input.numel() * self.world_size or input.dtype != output.dtype:
             raise nv.FlexarError(1, "output must hold world_size * input.numel() elements of input's dtype")
-        nv.check(self._lib.flexar_all_gather(self._h, input.data_ptr(), output.data_ptr(), input.numel(),
-                                             nv.dtype_code(input.dtype), _stream_handle(stream),
-                                             algo.encode() if algo else None), "all_gather")
+        args = (input.data_ptr(), output.data_ptr(), input.numel(), _dt(input.dtype),
+                _stream_handle(stream, self.device), _algo(algo))
+        rc = nv.FAST.ag(nv.AG, self._hi, *args) if nv.FAST is not None else \
+            self._lib.flexar_all_gather(self._h, *args)
+        if rc:
+            nv.check(rc, "all_gather")
         return output
 
     def all_to_all(self, input, output, stream=None):
@@ -212,6 +272,7 @@ class Communicator:
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
+            self._hi = 0
             self._lib.flexar_comm_destroy(self._h)
             self._h = ctypes.c_void_p()
 

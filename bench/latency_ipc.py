@@ -7,6 +7,7 @@ All ranks sharing device 0 exercises the real launch + flag/granule protocol
 these numbers are the protocol + launch floor, not 8-GPU latencies.
 
     python bench/latency_ipc.py --nranks 2 --out gpurun_out/latency_ipc.jsonl
+    python bench/latency_ipc.py --nranks 2 --graph      # the same calls captured in one hipGraph
 """
 from __future__ import annotations
 
@@ -15,6 +16,7 @@ import json
 import os
 import socket
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -27,7 +29,7 @@ def _port():
     return p
 
 
-def worker(rank, world, port, sizes, algos, iters, q):
+def worker(rank, world, port, sizes, algos, iters, q, graph=False):
     import torch
     import torch.distributed as dist
 
@@ -49,17 +51,56 @@ def worker(rank, world, port, sizes, algos, iters, q):
             torch.cuda.synchronize()
             dist.barrier()
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record()
-            for _ in range(iters):
-                comm.all_reduce(x, out=y, algo=algo)
-            b.record()
+            if graph:
+                # launch-bound loop as one hipGraph: `iters` allreduces captured once, replayed; per-call
+                # cost is the protocol without the host launch path
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    for _ in range(iters):
+                        comm.all_reduce(x, out=y, algo=algo)
+                torch.cuda.current_stream().wait_stream(s)
+                for _ in range(2):
+                    g.replay()
+                torch.cuda.synchronize()
+                dist.barrier()
+                a.record()
+                h0 = time.perf_counter()
+                g.replay()
+                h1 = time.perf_counter()
+                b.record()
+            else:
+                a.record()
+                h0 = time.perf_counter()
+                for _ in range(iters):
+                    comm.all_reduce(x, out=y, algo=algo)
+                h1 = time.perf_counter()
+                b.record()
             torch.cuda.synchronize()
             us = a.elapsed_time(b) / iters * 1e3
+            host_us = (h1 - h0) / iters * 1e6  # CPU time to issue one call (eager) / 1/iters of a replay
             ok = bool(torch.all(y == world).item())
-            t = torch.tensor([us])
+            t = torch.tensor([us, host_us])
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            rows.append({"nranks": world, "bytes": n * 4, "algo": algo, "us_per_call": round(float(t.item()), 2),
-                         "correct": ok})
+            rows.append({"nranks": world, "bytes": n * 4, "algo": algo, "us_per_call": round(float(t[0]), 2),
+                         "host_us_per_call": round(float(t[1]), 2), "correct": ok, "graph": graph})
+        # floor: the same number of back-to-back single-kernel torch launches (a device copy)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(5):
+            y.copy_(x)
+        torch.cuda.synchronize()
+        a.record()
+        h0 = time.perf_counter()
+        for _ in range(iters):
+            y.copy_(x)
+        h1 = time.perf_counter()
+        b.record()
+        torch.cuda.synchronize()
+        t = torch.tensor([a.elapsed_time(b) / iters * 1e3, (h1 - h0) / iters * 1e6])
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        rows.append({"nranks": world, "bytes": n * 4, "algo": "torch_copy_floor", "us_per_call": round(float(t[0]), 2),
+                     "host_us_per_call": round(float(t[1]), 2), "correct": True, "graph": False})
     comm.check()
     comm.close()
     dist.barrier()
@@ -73,14 +114,16 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--algos", default="ll,oneshot,flat,ring")
     ap.add_argument("--out", default="")
+    ap.add_argument("--sizes", default="4,256,4096,65536,262144,1048576", help="buffer bytes")
+    ap.add_argument("--graph", action="store_true", help="capture the timed calls in one hipGraph and replay it")
     args = ap.parse_args()
     import torch.multiprocessing as mp
 
-    sizes = [4, 256, 4096, 65536, 262144, 1 << 20]
+    sizes = [int(v) for v in args.sizes.split(",")]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=worker, args=(r, args.nranks, port, sizes, args.algos.split(","), args.iters, q))
+    ps = [ctx.Process(target=worker, args=(r, args.nranks, port, sizes, args.algos.split(","), args.iters, q, args.graph))
           for r in range(args.nranks)]
     for p in ps:
         p.start()

@@ -150,6 +150,22 @@ struct flexar_comm {
   bool have_last = false;
   hipEvent_t order_ev = nullptr;
   bool unordered = false;  // FLEXAR_UNORDERED_CALLS=1: test-only, shows the race the ordering prevents
+  // Plan memo of the allreduce hot path: what a (algo, count, dtype, op, scale) call resolved to last
+  // time — spec, piece size, program, grid — so a repeated call skips spec parsing, key formatting and
+  // the program-cache lookup. Every setter that changes what a call resolves to bumps memo_gen.
+  struct CallMemo {
+    uint64_t gen = 0;  // == memo_gen when valid
+    uint64_t count = 0;
+    int dtype = -1, op = -1;
+    uint32_t fsb = 0;  // scale bits
+    std::string algo;
+    AlgoSpec s;
+    uint64_t piece = 0;
+    DevProgram* dp = nullptr;  // program of a one-piece call
+    int grid = 0;
+  };
+  CallMemo memo[16];
+  uint64_t memo_gen = 1;
 };
 
 namespace flexar {
@@ -770,6 +786,7 @@ int flexar_comm_set_tune_table(flexar_comm_t c, const char* text) {
   }
   c->tune = t;
   c->have_tune = !t.rows.empty();
+  c->memo_gen++;
   return 0;
 }
 
@@ -778,14 +795,18 @@ int flexar_comm_set_algo(flexar_comm_t c, const char* spec) {
   std::string err;
   AlgoSpec s;
   if (!parse_algo(spec ? spec : "auto", c->nranks, &s, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  std::lock_guard<std::mutex> lk(c->mu);
   c->spec = s;
+  c->memo_gen++;
   return 0;
 }
 
 int flexar_comm_set_grid(flexar_comm_t c, int grid_blocks, int block_threads) {
   if (!c) return FLEXAR_ERR_INVALID;
   (void)block_threads;
+  std::lock_guard<std::mutex> lk(c->mu);
   c->grid_override = grid_blocks < 0 ? 0 : grid_blocks;
+  c->memo_gen++;
   return 0;
 }
 
@@ -842,10 +863,35 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
   float fs = scale * (op == FLEXAR_AVG ? 1.0f / (float)c->nranks : 1.0f);
   std::lock_guard<std::mutex> lk(c->mu);
   if ((rc = order_call(c, st))) return rc;
+  uint32_t fsb;
+  memcpy(&fsb, &fs, 4);
+  const char* akey = algo ? algo : "";
+  flexar_comm::CallMemo& m = c->memo[((uint64_t)count * 0x9E3779B97F4A7C15ull + (uint64_t)dtype * 31u + (uint64_t)op) >> 60];
+  const bool hit = m.gen == c->memo_gen && m.count == count && m.dtype == dtype && m.op == op && m.fsb == fsb &&
+                   m.algo == akey;
   AlgoSpec s;
-  if ((rc = resolve_spec(c, algo, (double)count * es, &s))) return rc;
-  if (s.kind == AlgoKind::LL && !ll_usable(c, count, es)) s.kind = AlgoKind::ONESHOT;
-  if (s.kind == AlgoKind::DMA && c->nranks > 1) {
+  if (hit) {
+    s = m.s;
+  } else {
+    if ((rc = resolve_spec(c, algo, (double)count * es, &s))) return rc;
+    if (s.kind == AlgoKind::LL && !ll_usable(c, count, es)) s.kind = AlgoKind::ONESHOT;
+    if (s.kind == AlgoKind::DMA && c->nranks == 1) s.kind = AlgoKind::ONESHOT;  // one rank: the executor's copy
+  }
+  auto remember = [&](uint64_t piece, DevProgram* dp, int grid) {
+    if (hit) return;
+    m.gen = c->memo_gen;
+    m.count = count;
+    m.dtype = dtype;
+    m.op = op;
+    m.fsb = fsb;
+    m.algo = akey;
+    m.s = s;
+    m.piece = piece;
+    m.dp = dp;
+    m.grid = grid;
+  };
+  if (s.kind == AlgoKind::DMA) {
+    remember(0, nullptr, 0);
     if (roctx().push) roctx().push(("flexar allreduce dma " + std::to_string(count * es) + "B").c_str());
     c->calls++;
     c->bytes += count * es;
@@ -855,29 +901,61 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     if (roctx().pop) roctx().pop();
     return rc;
   }
-  if (s.kind == AlgoKind::DMA) s.kind = AlgoKind::ONESHOT;  // one rank: the executor's copy
   if (s.kind == AlgoKind::LL) {
-    DevCtx x;
-    fill_ctx(c, nullptr, in, out, &x);
-    x.count = count;
-    x.scale = fs;
     LaunchArgs la;
     la.kind = LAUNCH_LL;
-    la.ctx = x;
-    la.grid = ll_grid(c, count, es);
+    fill_ctx(c, nullptr, in, out, &la.ctx);
+    la.ctx.count = count;
+    la.ctx.scale = fs;
+    la.grid = hit ? m.grid : ll_grid(c, count, es);
     la.stream = st;
     if (roctx().push) roctx().push(("flexar allreduce ll " + std::to_string(count * es) + "B").c_str());
     c->calls++;
     c->bytes += count * es;
     rc = launch_dtype(dtype, op, la);
-    if (!rc) c->launches++;
+    if (!rc) {
+      c->launches++;
+      remember(0, nullptr, la.grid);
+    }
     if (roctx().pop) roctx().pop();
     return rc;
   }
   uint64_t piece = count;
-  if (c->nranks > 1 && (rc = plan_pieces(c, s, count, es, fs, &piece))) return rc;
-  const std::string sdesc = s.str();
+  if (hit) piece = m.piece;
+  else if (c->nranks > 1 && (rc = plan_pieces(c, s, count, es, fs, &piece))) return rc;
+  const bool described = roctx().push || c->profile;
+  const std::string sdesc = described ? s.str() : std::string();
   if (roctx().push) roctx().push(("flexar allreduce " + sdesc + " " + std::to_string(count * es) + "B").c_str());
+  if (piece >= count) {  // one launch: the memoised program and grid
+    DevProgram* dp = hit ? m.dp : nullptr;
+    if (!dp && (rc = get_program(c, s, count, es, fs, &dp))) return rc;
+    LaunchArgs la;
+    la.kind = LAUNCH_EXEC;
+    fill_ctx(c, dp, in, out, &la.ctx);
+    la.grid = hit ? m.grid : choose_grid(c, count * es, dp->prog.nchan);
+    la.stream = st;
+    la.proto = proto_of(s);
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    if (c->profile) {
+      FX_HIP(hipEventCreate(&ev0));
+      FX_HIP(hipEventCreate(&ev1));
+      FX_HIP(hipEventRecord(ev0, st));
+    }
+    c->calls++;
+    c->bytes += count * es;
+    rc = launch_dtype(dtype, op, la);
+    if (!rc) {
+      c->launches++;
+      remember(piece, dp, la.grid);
+    }
+    if (c->profile) {
+      (void)hipEventRecord(ev1, st);
+      c->prof_pending.push_back(ProfRec{sdesc, (uint64_t)count * es, ev0, ev1});
+    }
+    if (roctx().pop) roctx().pop();
+    return rc;
+  }
+  remember(piece, nullptr, 0);
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   if (c->profile) {
     FX_HIP(hipEventCreate(&ev0));
