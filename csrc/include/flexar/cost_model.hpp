@@ -39,7 +39,7 @@ constexpr double kLLMaxBytes = 1 << 20;  // LL protocol only for latency-bound s
 
 struct XgmiModel {
   double alpha_launch_us = 6.0;  // kernel launch + first-touch
-  double alpha_sync_us = 2.0;    // one cross-GPU signal->wait hop
+  double alpha_sync_us = 4.0;    // one signal->wait hand-off incl. release/acquire (measured ~4-5 us, BASELINE §5.8)
   double link_gbps = 64.0;       // usable per-direction bandwidth of one xGMI link (GB/s)
   double hbm_gbps = 4000.0;      // effective local HBM bandwidth of the fused reduce
   int links = 7;                 // point-to-point links per GPU (fully connected 8-GPU node)
