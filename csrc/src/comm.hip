@@ -215,7 +215,7 @@ static bool ll_usable(flexar_comm* c, uint64_t count, uint32_t es) {
 static int ll_grid(flexar_comm* c, uint64_t count, uint32_t es) {
   uint64_t words = (count * es + 3) / 4;
   uint64_t g = (words + 2 * kExecThreads - 1) / (2 * kExecThreads);  // ~2 words per lane
-  g = std::max<uint64_t>(1, std::min<uint64_t>(g, (uint64_t)std::min(c->max_grid, 64)));
+  g = std::max<uint64_t>(1, std::min<uint64_t>(g, (uint64_t)c->max_grid));
   return (int)g;
 }
 
