@@ -242,6 +242,76 @@ def test_autotune_installs_measured_table(cuda):
     assert tables[0] == tables[1]  # every rank installed the same table
 
 
+def _memo_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
+                          FLEXAR_TIMEOUT_MS="20000", FLEXAR_PROFILE="1")
+        import torch.distributed as dist
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from allreduce_over_mpi_amd.parallel import Communicator
+
+        comm = Communicator(workspace_bytes=64 << 20)
+        torch.manual_seed(9)  # same input on every rank
+        x = torch.randn(1 << 18, device="cuda")
+        ref = x.double().cpu() * world
+        errs, seen = [], []
+
+        def call(**kw):
+            y = comm.all_reduce(x.clone(), **kw)
+            torch.cuda.synchronize()
+            errs.append((y.double().cpu() - ref).abs().max().item())
+            seen.append(set(comm.stats()["profile"]))
+
+        call()                           # auto: the cost model's choice
+        call()                           # memo hit
+        comm.set_algo("ring")
+        call()                           # the default changed: must not reuse the memoised plan
+        comm.set_tune_table(f"{world} 0 flat+push")
+        comm.set_algo("auto")
+        call()                           # auto again, now from the installed table
+        call(algo="oneshot")             # same size, explicit algorithm
+        call(algo="ring")
+        comm.set_grid(4)
+        call(algo="ring")                # grid override bumps the memo too
+        comm.check()
+        comm.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, (errs, [sorted(k) for k in seen]), None))
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_plan_memo_follows_configuration_changes(cuda):
+    """The per-communicator plan memo of flexar_allreduce_ex (a repeated call skips spec parsing and the
+    program lookup) must be invalidated by set_algo / set_tune_table / set_grid: every call lands under
+    the algorithm the current configuration selects (FLEXAR_PROFILE records per-algorithm device time)."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_memo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, out, tb in res:
+        assert tb is None, tb
+        errs, seen = out
+        assert max(errs) < 1e-4, errs
+        # new algorithm names appear exactly where the configuration changed
+        assert len(seen[0]) == 1 and seen[1] == seen[0], seen
+        assert len(seen[2]) == 2 and any(k.startswith("ring") for k in seen[2]), seen
+        assert len(seen[3]) == 3 and any("push" in k for k in seen[3]), seen
+        assert len(seen[4]) == 3 + (0 if any(k.startswith("oneshot") for k in seen[3]) else 1), seen
+
+
 def _stress_worker(rank, world, port, calls, q, fault=""):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
