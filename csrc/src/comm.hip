@@ -150,6 +150,10 @@ struct flexar_comm {
   bool have_last = false;
   hipEvent_t order_ev = nullptr;
   bool unordered = false;  // FLEXAR_UNORDERED_CALLS=1: test-only, shows the race the ordering prevents
+  // A call of this communicator was captured into a graph. Replays advance the device epochs without the
+  // host seeing them, and the copy-engine path (dma) bakes the host mirror of the epoch into its copies
+  // and flag writes, so from then on a dma request runs the executor's flat exchange instead.
+  bool captured = false;
   // Plan memo of the allreduce hot path: what a (algo, count, dtype, op, scale) call resolved to last
   // time — spec, piece size, program, grid — so a repeated call skips spec parsing, key formatting and
   // the program-cache lookup. Every setter that changes what a call resolves to bumps memo_gen.
@@ -176,6 +180,7 @@ namespace flexar {
 static int order_call(flexar_comm* c, hipStream_t st) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess) { (void)hipGetLastError(); cs = hipStreamCaptureStatusNone; }
+  if (cs != hipStreamCaptureStatusNone) c->captured = true;
   if (cs != hipStreamCaptureStatusNone || c->unordered) return 0;
   if (c->have_last && c->last_st != st) {
     if (!c->order_ev) FX_HIP(hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming));
@@ -876,6 +881,12 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     if ((rc = resolve_spec(c, algo, (double)count * es, &s))) return rc;
     if (s.kind == AlgoKind::LL && !ll_usable(c, count, es)) s.kind = AlgoKind::ONESHOT;
     if (s.kind == AlgoKind::DMA && c->nranks == 1) s.kind = AlgoKind::ONESHOT;  // one rank: the executor's copy
+  }
+  if (s.kind == AlgoKind::DMA && c->captured) {  // not replay-safe (see flexar_comm::captured)
+    AlgoSpec f;
+    std::string err;
+    if (!parse_algo("flat+pull", c->nranks, &f, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+    s = f;
   }
   auto remember = [&](uint64_t piece, DevProgram* dp, int grid) {
     if (hit) return;

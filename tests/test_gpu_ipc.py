@@ -312,6 +312,68 @@ def test_plan_memo_follows_configuration_changes(cuda):
         assert len(seen[4]) == 3 + (0 if any(k.startswith("oneshot") for k in seen[3]) else 1), seen
 
 
+def _captured_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
+                          FLEXAR_TIMEOUT_MS="20000")
+        import torch.distributed as dist
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from allreduce_over_mpi_amd.parallel import CapturedAllReduce, Communicator
+
+        comm = Communicator(workspace_bytes=64 << 20)
+        sizes = [64, 16384, 1 << 18]
+        bufs = [torch.empty(n, device="cuda") for n in sizes]
+        outs = [None, torch.empty(sizes[1], device="cuda"), None]
+        cap = CapturedAllReduce(comm, bufs, outs=outs, algo=[None, "oneshot", "dma"])
+        errs = []
+        for it in range(5):
+            xs = [[torch.randn(n, generator=torch.Generator().manual_seed(1000 * it + 10 * r + k))
+                   for r in range(world)] for k, n in enumerate(sizes)]
+            for k, b in enumerate(bufs):
+                b.copy_(xs[k][rank])
+            cap.replay()
+            torch.cuda.synchronize()
+            for k, res in enumerate(cap.results):
+                ref = torch.stack(xs[k]).double().sum(0)
+                errs.append((res.double().cpu() - ref).abs().max().item())
+        # eager calls after replays, dma included: the host never saw the replays' epochs
+        x = torch.full((1 << 18,), float(rank + 1), device="cuda")
+        for spec in ("dma", "flat", "ll"):
+            y = comm.all_reduce(x.clone(), algo=spec)
+            torch.cuda.synchronize()
+            errs.append((y - world * (world + 1) / 2).abs().max().item())
+        comm.check()
+        comm.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, errs, None))
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_captured_allreduce_replays(cuda):
+    """CapturedAllReduce: LL / oneshot / dma-requested calls captured in one graph, replayed with new inputs;
+    eager calls (dma included) stay correct afterwards."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_captured_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, errs, tb in res:
+        assert tb is None, tb
+        assert len(errs) == 18 and max(errs) < 1e-4, errs
+
+
 def _stress_worker(rank, world, port, calls, q, fault=""):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
