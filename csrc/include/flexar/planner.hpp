@@ -709,6 +709,60 @@ class Planner {
   }
 };
 
+// Element extents of the caller's IN / OUT buffers that a (coll, count, stride) program may touch.
+inline void io_extent(Coll coll, uint32_t N, uint64_t count, uint64_t stride, uint64_t* in, uint64_t* out) {
+  const uint64_t wide = N > 1 ? (uint64_t)(N - 1) * stride + count : count;
+  switch (coll) {
+    case Coll::REDUCE_SCATTER: *in = wide; *out = count; break;
+    case Coll::ALL_GATHER: *in = count; *out = wide; break;
+    case Coll::ALL_TO_ALL: *in = wide; *out = wide; break;
+    default: *in = count; *out = count; break;  // allreduce, broadcast (stride = root)
+  }
+}
+
+// Host-side bounds check of a compiled program before it is uploaded or launched: every XFER operand
+// stays inside its buffer (IN/OUT: this rank's, within the call's extent; STG: any rank's, within the
+// program's staging), fan-in/fan-out and peer lists within the kernel's fixed arrays, flag slots within
+// the program range, channel table well formed. The executor trusts the program (no per-access
+// checks in the hot loop), so a planner bug must stop here instead of faulting the GPU.
+inline bool validate_program(const Program& P, uint32_t N, uint32_t rank, uint64_t in_elems, uint64_t out_elems,
+                             std::string* err) {
+  auto fail = [&](const std::string& m) {
+    if (err) *err = "internal: invalid program '" + P.desc + "': " + m;
+    return false;
+  };
+  if (P.chan_start.size() != (size_t)P.nchan + 1 || P.chan_start.front() != 0 || P.chan_start.back() != P.ops.size())
+    return fail("channel table");
+  for (size_t c = 0; c + 1 < P.chan_start.size(); ++c)
+    if (P.chan_start[c] > P.chan_start[c + 1]) return fail("channel table not monotonic");
+  auto loc_ok = [&](const Loc& l, uint64_t len) {
+    if (l.rank >= N || l.buf >= BUF_COUNT) return false;
+    if (l.buf == BUF_STG) return l.off + len <= P.stg_elems;
+    if (l.rank != rank) return false;  // a caller buffer is never addressed on a peer
+    return l.off + len <= (l.buf == BUF_IN ? in_elems : out_elems);
+  };
+  for (size_t i = 0; i < P.ops.size(); ++i) {
+    const Op& o = P.ops[i];
+    const std::string at = "op " + std::to_string(i);
+    if (o.kind == OP_XFER) {
+      if (o.nsrc < 1 || o.nsrc > kMaxSrc || o.ndst < 1 || o.ndst > kMaxDst) return fail(at + ": operand count");
+      for (int k = 0; k < o.nsrc; ++k)
+        if (!loc_ok(o.src[k], o.len)) return fail(at + ": source " + std::to_string(k) + " out of bounds");
+      for (int k = 0; k < o.ndst; ++k)
+        if (!loc_ok(o.dst[k], o.len)) return fail(at + ": destination " + std::to_string(k) + " out of bounds");
+      if (o.run > 1 && i + o.run > P.ops.size()) return fail(at + ": run past the end");
+    } else if (o.kind == OP_SIGNAL || o.kind == OP_WAIT) {
+      if (o.npeers > kMaxPeersPerOp) return fail(at + ": peer count");
+      if (o.slot >= kProgSlots) return fail(at + ": flag slot");
+      for (int k = 0; k < o.npeers; ++k)
+        if (o.peers[k] >= N || o.peers[k] == rank) return fail(at + ": peer");
+    } else if (o.kind != OP_NOP) {
+      return fail(at + ": kind");
+    }
+  }
+  return true;
+}
+
 // Human-readable program dump (the reference's Operations::print_ops, mpi_mod.hpp:107-144).
 inline std::string dump_program(const Program& P, uint32_t rank) {
   static const char* bn[] = {"IN", "OUT", "STG"};

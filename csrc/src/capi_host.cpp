@@ -204,6 +204,7 @@ int flexar_simulate(const char* spec, int nranks, size_t count, int dtype, int o
   for (int r = 0; r < nranks; ++r) {
     Planner pl(nranks, r, count, (uint32_t)es, fs);
     if (!pl.build(s, &progs[r], &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+    if (!validate_program(progs[r], nranks, r, count, count, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
     if (progs[r].nchan > (uint32_t)grid) { set_error("grid must be >= number of channels"); return FLEXAR_ERR_INVALID; }
   }
   if (grid % progs[0].nchan) { set_error("grid must be a multiple of the channel count"); return FLEXAR_ERR_INVALID; }
@@ -227,6 +228,9 @@ int flexar_simulate_coll(int coll, const char* spec, int nranks, size_t count, i
   for (int r = 0; r < nranks; ++r) {
     Planner pl(nranks, r, count, (uint32_t)es, fs);
     if (!pl.build_coll((Coll)coll, s, count, &progs[r], &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+    uint64_t in_el, out_el;
+    io_extent((Coll)coll, nranks, count, count, &in_el, &out_el);
+    if (!validate_program(progs[r], nranks, r, in_el, out_el, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
   }
   if (grid % progs[0].nchan) { set_error("grid must be a multiple of the channel count"); return FLEXAR_ERR_INVALID; }
   return dispatch_dtype_op<SimRun>(dtype, (coll == 2 || coll == 4) ? FLEXAR_SUM : op, progs, nranks, grid, ncalls, 0, inputs,
@@ -249,6 +253,7 @@ int flexar_simulate_bcast(const char* spec, int nranks, size_t count, int dtype,
   for (int r = 0; r < nranks; ++r) {
     Planner pl(nranks, r, count, (uint32_t)es, 1.0f);
     if (!pl.build_coll(Coll::BROADCAST, s, (uint64_t)root, &progs[r], &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+    if (!validate_program(progs[r], nranks, r, count, count, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
   }
   return dispatch_dtype_op<SimRun>(dtype, FLEXAR_SUM, progs, nranks, grid, ncalls, 0, inputs, outputs, count);
 }

@@ -265,6 +265,12 @@ static int get_program(flexar_comm* c, const AlgoSpec& s, uint64_t count, uint32
   std::string err;
   Planner pl(c->nranks, c->rank, count, esize, fscale);
   if (!pl.build_coll(coll, s, stride, &dp->prog, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  uint64_t in_el, out_el;
+  io_extent(coll, c->nranks, count, stride, &in_el, &out_el);
+  if (!validate_program(dp->prog, c->nranks, c->rank, in_el, out_el, &err)) {
+    set_error(err);
+    return FLEXAR_ERR_INVALID;
+  }
   mark_barriers(dp->prog, c->rank);
   logf(LOG_INFO, c->rank, "plan %s: count=%llu esize=%u ops=%zu channels=%u staging=%llu B", s.str().c_str(),
        (unsigned long long)count, esize, dp->prog.ops.size(), dp->prog.nchan,
