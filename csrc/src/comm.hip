@@ -601,6 +601,13 @@ static int run_dma(flexar_comm* const* cs, int ncomm, const char* const* ins, ch
 
 static int check_err(flexar_comm* c) {
   uint32_t e = __atomic_load_n(c->err_host, __ATOMIC_ACQUIRE);
+  if (e & 0x40000000u) {
+    char buf[200];
+    snprintf(buf, sizeof(buf), "rank %d: protocol violation — peer %u is more than one call ahead (slot %u): "
+             "two calls of this communicator overlapped", c->rank, e & 0xffu, (e >> 8) & 0xffffu);
+    set_error(buf);
+    return FLEXAR_ERR_STATE;
+  }
   if (e) {
     char buf[160];
     snprintf(buf, sizeof(buf), "rank %d: device wait timed out (slot %u, peer %u) — a peer stopped participating",

@@ -360,7 +360,8 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
         if (tid < o->npeers) {
           uint64_t* f = c.peer_flags[c.rank] + flag_index(o->slot, o->peers[tid], b);
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-          while (ld_flag(f) < epoch) {
+          uint64_t v;
+          while ((v = ld_flag(f)) < epoch) {
             __builtin_amdgcn_s_sleep(2);
             if (__builtin_amdgcn_s_memrealtime() - t0 > c.timeout_ticks) {
               __hip_atomic_store(c.err, (uint32_t)(0x80000000u | (o->slot << 8) | o->peers[tid]), __ATOMIC_RELAXED,
@@ -369,6 +370,13 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
               break;
             }
           }
+          // Protocol invariant (docs/DESIGN.md §2): a peer can be at most one call ahead, because its
+          // call e+2 needs this rank's contribution to e+1. A flag beyond epoch+1 means two calls of one
+          // communicator overlapped (broken stream ordering) and staging may have been overwritten:
+          // report it instead of returning a silently wrong sum.
+          if (v > epoch + 1)
+            __hip_atomic_store(c.err, (uint32_t)(0x40000000u | (o->slot << 8) | o->peers[tid]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
         }
         if constexpr (PM != PM_WT) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // WT: loads are sc0 sc1
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
