@@ -50,17 +50,16 @@ _OP_CODES: dict = {}
 
 
 def _dt(dtype) -> int:
-    c = _DT_CODES.get(dtype)
+    c = _DT_CODES.get(dtype)  # torch dtypes are singletons: the memo holds at most one entry per dtype
     if c is None:
         c = _DT_CODES[dtype] = nv.dtype_code(dtype)
     return c
 
 
 def _op(op) -> int:
-    try:
-        c = _OP_CODES.get(op)
-    except TypeError:  # unhashable op object
+    if type(op) is not str:  # ints pass through; other op objects are not memoised (unbounded identities)
         return nv.op_code(op)
+    c = _OP_CODES.get(op)
     if c is None:
         c = _OP_CODES[op] = nv.op_code(op)
     return c
@@ -71,8 +70,10 @@ _ALGO_BYTES: dict = {None: None}
 
 def _algo(algo: Optional[str]):
     b = _ALGO_BYTES.get(algo)
-    if b is None and algo is not None:
-        b = _ALGO_BYTES[algo] = algo.encode() if algo else None
+    if b is None and algo:
+        b = algo.encode()
+        if len(_ALGO_BYTES) < 256:  # specs are a small fixed vocabulary; never grow without bound
+            _ALGO_BYTES[algo] = b
     return b
 
 
