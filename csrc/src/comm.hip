@@ -1110,6 +1110,31 @@ int flexar_group_create(int nranks, int device, size_t workspace_bytes, flexar_c
   return 0;
 }
 
+// The in-process group paths (LocalGroup: tests, calibration) stage their per-rank contexts in one
+// device buffer per host thread. A call on another stream must not overwrite it while the previous
+// call's kernel still reads it: the copy waits on an event recorded after that kernel's launch.
+struct GroupCtxStage {
+  DevCtx* d = nullptr;
+  hipEvent_t done = nullptr;
+  bool used = false;
+};
+static thread_local GroupCtxStage g_group_ctx;
+
+static int stage_group_ctx(const std::vector<DevCtx>& h, int nranks, hipStream_t st, DevCtx** out) {
+  GroupCtxStage& g = g_group_ctx;
+  if (!g.d) FX_HIP(hipMalloc(&g.d, sizeof(DevCtx) * kMaxRanks));
+  if (!g.done) FX_HIP(hipEventCreateWithFlags(&g.done, hipEventDisableTiming));
+  if (g.used) FX_HIP(hipStreamWaitEvent(st, g.done, 0));
+  FX_HIP(hipMemcpyAsync(g.d, h.data(), sizeof(DevCtx) * nranks, hipMemcpyHostToDevice, st));
+  *out = g.d;
+  return 0;
+}
+static int group_ctx_launched(hipStream_t st) {
+  FX_HIP(hipEventRecord(g_group_ctx.done, st));
+  g_group_ctx.used = true;
+  return 0;
+}
+
 // One launch runs every rank of the group: ins/outs are nranks device pointers.
 int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* ins, void* const* outs, size_t count,
                            int dtype, int op, void* stream, const char* algo, float scale) {
@@ -1128,8 +1153,7 @@ int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
     int rc = resolve_spec(comms[r], algo, (double)count * es, &specs[r]);
     if (rc) return rc;
   }
-  static thread_local DevCtx* d_ctx = nullptr;
-  if (!d_ctx) FX_HIP(hipMalloc(&d_ctx, sizeof(DevCtx) * kMaxRanks));
+  DevCtx* d_ctx = nullptr;
   if (specs[0].kind == AlgoKind::LL && !ll_usable(comms[0], count, es))
     for (auto& sp : specs) sp.kind = AlgoKind::ONESHOT;
   if (specs[0].kind == AlgoKind::DMA && nranks > 1) {
@@ -1154,7 +1178,7 @@ int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
       h[r].scale = fs;
     }
     int grid = std::max(1, std::min(ll_grid(comms[0], count, es), (int)kGroupMaxBlocks / nranks));
-    FX_HIP(hipMemcpyAsync(d_ctx, h.data(), sizeof(DevCtx) * nranks, hipMemcpyHostToDevice, st));
+    if (int e = stage_group_ctx(h, nranks, st, &d_ctx)) return e;
     LaunchArgs la;
     la.kind = LAUNCH_LL_GROUP;
     la.d_ctxs = d_ctx;
@@ -1162,6 +1186,7 @@ int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
     la.grid = grid;
     la.stream = st;
     int rc = launch_dtype(dtype, op, la);
+    if (!rc) (void)group_ctx_launched(st);
     if (rc) return rc;
     for (int r = 0; r < nranks; ++r) comms[r]->launches++;
     FX_HIP(hipStreamSynchronize(st));
@@ -1190,7 +1215,7 @@ int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
       set_error("group grid too large: ranks x grid must stay <= 256 co-resident workgroups");
       return FLEXAR_ERR_INVALID;
     }
-    FX_HIP(hipMemcpyAsync(d_ctx, h.data(), sizeof(DevCtx) * nranks, hipMemcpyHostToDevice, st));
+    if (int e = stage_group_ctx(h, nranks, st, &d_ctx)) return e;
     LaunchArgs la;
     la.kind = LAUNCH_GROUP;
     la.d_ctxs = d_ctx;
@@ -1199,6 +1224,7 @@ int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
     la.stream = st;
     la.proto = proto_of(specs[0]);
     int rc = launch_dtype(dtype, op, la);
+    if (!rc) (void)group_ctx_launched(st);
     if (rc) return rc;
     for (int r = 0; r < nranks; ++r) comms[r]->launches++;
     FX_HIP(hipStreamSynchronize(st));  // d_ctx is reused by the next piece
@@ -1219,8 +1245,7 @@ int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const vo
   hipStream_t st = (hipStream_t)stream;
   const uint32_t es = (uint32_t)dtype_size(dtype);
   float fs = coll == 1 && op == FLEXAR_AVG ? 1.0f / (float)nranks : 1.0f;
-  static thread_local DevCtx* d_ctx = nullptr;
-  if (!d_ctx) FX_HIP(hipMalloc(&d_ctx, sizeof(DevCtx) * kMaxRanks));
+  DevCtx* d_ctx = nullptr;
   std::vector<DevCtx> h(nranks);
   int grid = 0;
   int proto = PM_FENCE;
@@ -1237,7 +1262,7 @@ int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const vo
     int g = choose_grid(comms[r], count * es * nranks, dp->prog.nchan);
     grid = r == 0 ? g : grid;
   }
-  FX_HIP(hipMemcpyAsync(d_ctx, h.data(), sizeof(DevCtx) * nranks, hipMemcpyHostToDevice, st));
+  if (int e = stage_group_ctx(h, nranks, st, &d_ctx)) return e;
   LaunchArgs la;
   la.kind = LAUNCH_GROUP;
   la.d_ctxs = d_ctx;
@@ -1246,6 +1271,7 @@ int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const vo
   la.stream = st;
   la.proto = proto;
   int rc = launch_dtype(dtype, op, la);
+  if (!rc) (void)group_ctx_launched(st);
   if (rc) return rc;
   for (int r = 0; r < nranks; ++r) comms[r]->launches++;
   FX_HIP(hipStreamSynchronize(st));
@@ -1263,8 +1289,7 @@ int flexar_group_broadcast(flexar_comm_t* comms, int nranks, int root, const voi
   if (count == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   const uint32_t es = (uint32_t)dtype_size(dtype);
-  static thread_local DevCtx* d_ctx = nullptr;
-  if (!d_ctx) FX_HIP(hipMalloc(&d_ctx, sizeof(DevCtx) * kMaxRanks));
+  DevCtx* d_ctx = nullptr;
   std::vector<DevCtx> h(nranks);
   int grid = 0, proto = PM_FENCE;
   for (int r = 0; r < nranks; ++r) {
@@ -1280,7 +1305,7 @@ int flexar_group_broadcast(flexar_comm_t* comms, int nranks, int root, const voi
     int g = choose_grid(comms[r], count * es, dp->prog.nchan);
     grid = r == 0 ? g : grid;
   }
-  FX_HIP(hipMemcpyAsync(d_ctx, h.data(), sizeof(DevCtx) * nranks, hipMemcpyHostToDevice, st));
+  if (int e = stage_group_ctx(h, nranks, st, &d_ctx)) return e;
   LaunchArgs la;
   la.kind = LAUNCH_GROUP;
   la.d_ctxs = d_ctx;
@@ -1289,6 +1314,7 @@ int flexar_group_broadcast(flexar_comm_t* comms, int nranks, int root, const voi
   la.stream = st;
   la.proto = proto;
   int rc = launch_dtype(dtype, FLEXAR_SUM, la);
+  if (!rc) (void)group_ctx_launched(st);
   if (rc) return rc;
   for (int r = 0; r < nranks; ++r) comms[r]->launches++;
   FX_HIP(hipStreamSynchronize(st));
