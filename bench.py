@@ -85,6 +85,7 @@ def main():
     ap.add_argument("--tune-out", default="", help="append the tuner's choice as a FLEXAR_TUNE_FILE line")
     ap.add_argument("--algo", default="auto", help="flexar algorithm spec or 'auto' (tuned at start-up)")
     ap.add_argument("--no-rccl", action="store_true", help="skip the RCCL comparison run")
+    ap.add_argument("--no-small", action="store_true", help="skip the 8 KiB latency companion figure")
     ap.add_argument("--no-tune", action="store_true", help="use the cost model instead of the start-up tuner")
     args = ap.parse_args()
 
@@ -321,6 +322,28 @@ def main():
         rt = max_over_ranks(time.perf_counter() - t1) / max(1, args.steps)
         rccl_busbw = round(busbw_gbps(nbytes, rt, world), 2)
 
+    # latency-bound companion figure (outside the timed region): an 8 KiB fp32 allreduce, eager, the
+    # selector's choice (LL), against RCCL's on the same buffer
+    small = None
+    if world > 1 and not args.no_small:
+        xs = torch.randn(2048, device=dev)
+        ys = torch.empty_like(xs)
+
+        def per_call(fn, iters=200):
+            for _ in range(20):
+                fn()
+            torch.cuda.synchronize()
+            dist.barrier()
+            t2 = time.perf_counter()
+            for _ in range(iters):
+                fn()
+            torch.cuda.synchronize()
+            return round(max_over_ranks(time.perf_counter() - t2) / iters * 1e6, 2)
+
+        small = {"flexar": per_call(lambda: comm.all_reduce(xs, out=ys))}
+        if not args.no_rccl and not shared:
+            small["rccl"] = per_call(lambda: dist.all_reduce(xs))
+
     algbw = algbw_gbps(nbytes, t_step)
     busbw = busbw_gbps(nbytes, t_step, world)
     value = busbw * world if world > 1 else algbw
@@ -355,6 +378,7 @@ def main():
         "rccl_busbw_GBps": rccl_busbw,
         "fallback": fallback,
         "tuner": tune_log or None,
+        "small_msg_8KiB_us_per_call": small,
     }
     if args.sweep:
         out["sweep"] = run_sweep(args, comm, world, rank, dev, dtype, op, dist, max_over_ranks)
