@@ -35,7 +35,7 @@ class FlexarError(RuntimeError):
 def _sig(lib):
     c = ctypes
     vp, sz, i, f, d, cp = c.c_void_p, c.c_size_t, c.c_int, c.c_float, c.c_double, c.c_char_p
-    u64 = c.c_uint64
+    u64, u32 = c.c_uint64, c.c_uint32
     table = {
         "flexar_version": (cp, []),
         "flexar_last_error": (cp, []),
@@ -79,6 +79,14 @@ def _sig(lib):
         "flexar_dequantize_fp8": (i, [vp, vp, i, sz, vp, f, vp]),
         "flexar_group_broadcast": (i, [c.POINTER(vp), i, i, c.POINTER(vp), c.POINTER(vp), sz, i, vp, cp]),
         "flexar_simulate_bcast": (i, [cp, i, sz, i, i, c.POINTER(vp), c.POINTER(vp), i, i]),
+        "flexar_comm_selftest": (i, [vp, u32, c.POINTER(u32)]),
+        "flexar_comm_set_disabled": (i, [vp, u32]),
+        "flexar_comm_disabled": (u32, [vp]),
+        "flexar_comm_topology": (i, [vp, cp, sz]),
+        "flexar_comm_predict_us": (d, [vp, cp, d]),
+        "flexar_kernel_info": (i, [i, i, i, i, c.POINTER(i), c.POINTER(i)]),
+        "flexar_downgrade_spec": (i, [cp, i, u32, i, cp, sz]),
+        "flexar_direct_links": (i, [c.POINTER(c.c_int32), c.POINTER(c.c_int32), i, i]),
     }
     for name, (res, args) in table.items():
         fn = getattr(lib, name)
@@ -209,6 +217,42 @@ def plan_dump(spec: str, rank: int, nranks: int, count: int, dtype="float32") ->
     b = _strbuf(1 << 22)
     check(lib().flexar_plan_dump(spec.encode(), rank, nranks, count, dtype_code(dtype), b, 1 << 22), "plan_dump")
     return b.value.decode()
+
+
+# protocol families (csrc/include/flexar/readiness.hpp)
+FAMILIES = {"fence": 1, "wt": 2, "ll": 4, "dma": 8}
+
+
+def family_names(mask: int) -> list[str]:
+    return [k for k, v in FAMILIES.items() if mask & v]
+
+
+def downgrade_spec(spec: str, nranks: int, disabled, allow_dma: bool = True) -> str:
+    """The spec a call runs when the families in ``disabled`` (mask or names) failed the self-test."""
+    if not isinstance(disabled, int):
+        disabled = sum(FAMILIES[n] for n in disabled)
+    b = _strbuf(256)
+    check(lib().flexar_downgrade_spec(spec.encode(), nranks, disabled, int(allow_dma), b, 256), "downgrade_spec")
+    return b.value.decode()
+
+
+LINK_CLASSES = {"unknown": 0, "same-device": 1, "xgmi": 2, "pcie": 3, "other": 4}
+
+
+def direct_links(classes, hops, self_rank: int) -> int:
+    """Concurrent links the cost model assumes for probed per-peer link classes (names) and hop counts."""
+    n = len(classes)
+    a = (ctypes.c_int32 * n)(*[LINK_CLASSES[c] for c in classes])
+    h = (ctypes.c_int32 * n)(*hops)
+    return int(lib().flexar_direct_links(a, h, n, self_rank))
+
+
+def kernel_info(dtype="float32", op="sum", kind: int = 0, proto: int = 0) -> dict:
+    """Occupancy (512-thread workgroups per CU) and VGPRs of one kernel instantiation (needs a GPU)."""
+    occ, regs = ctypes.c_int(0), ctypes.c_int(0)
+    check(lib().flexar_kernel_info(dtype_code(dtype), op_code(op), kind, proto, ctypes.byref(occ), ctypes.byref(regs)),
+          "kernel_info")
+    return {"blocks_per_cu": occ.value, "vgprs": regs.value}
 
 
 def _ptr_array(ptrs):

@@ -111,6 +111,7 @@ class Communicator:
                                                   ctypes.byref(h)), "comm_create")
         self._h = h
         self._hi = int(h.value or 0)  # the handle as an int, for the fast-call path
+        self.selftest_failed = []
         if self.world_size > 1:
             hs = int(self._lib.flexar_handle_size())
             buf = ctypes.create_string_buffer(hs)
@@ -129,11 +130,56 @@ class Communicator:
             if bad:
                 self.close()
                 raise nv.FlexarError(rc or 5, "comm_connect: " + "; ".join(bad))
+            self._readiness(exchange)
         self._rccl_default = False
         self._rccl_group = None
         env_algo = os.environ.get("FLEXAR_ALGO", "")
         if algo or env_algo == "rccl":
             self.set_algo(algo or env_algo)
+
+    def _readiness(self, exchange):
+        """Connect-time self-test (flexar_comm_selftest): every protocol family runs exact integer
+        allreduces on the real links; a family that failed on ANY rank is disabled on every rank, and
+        calls move to a verified one (ll -> oneshot, fence -> +wt -> dma). FLEXAR_SELFTEST=0 skips it."""
+        self.selftest_failed: list[str] = []
+        if os.environ.get("FLEXAR_SELFTEST", "1") == "0":
+            return
+        fam = sum(nv.FAMILIES.values())
+        failed = ctypes.c_uint32(0)
+        rc = self._lib.flexar_comm_selftest(self._h, fam, ctypes.byref(failed))
+        msg = f"{rc}:{failed.value}:{nv.last_error() if rc else ''}".encode()
+        rows = [m.decode(errors="replace").split(":", 2) for m in exchange(msg)]  # also the barrier
+        errs = [f"rank {r}: {e}" for r, (c, _, e) in enumerate(rows) if c != "0"]
+        if errs:
+            self.close()
+            raise nv.FlexarError(3, "self-test: " + "; ".join(errs))
+        mask = 0
+        for _, f, _ in rows:
+            mask |= int(f)
+        if mask:
+            # every rank has finished every self-test call (the exchange above): forget the watchdog state
+            nv.check(self._lib.flexar_comm_clear_error(self._h), "clear_error")
+            nv.check(self._lib.flexar_comm_set_disabled(self._h, mask), "set_disabled")
+            self.selftest_failed = nv.family_names(mask)
+            exchange(b"")  # nobody issues a production call before every rank installed the mask
+            if mask == fam:
+                self.close()
+                raise nv.FlexarError(2, "no device protocol passed the connect-time self-test on this node")
+
+    def topology(self) -> dict:
+        """Connect-time probe: per-peer PCI bus id, device, link class and hop count; self-test state."""
+        import json
+
+        b = ctypes.create_string_buffer(1 << 14)
+        nv.check(self._lib.flexar_comm_topology(self._h, b, 1 << 14), "comm_topology")
+        return json.loads(b.value.decode())
+
+    def predict_us(self, spec: str, nbytes: float) -> float:
+        """Cost-model time of ``spec`` ("auto" = the model's choice) for ``nbytes`` on this node's probed links."""
+        v = self._lib.flexar_comm_predict_us(self._h, spec.encode(), float(nbytes))
+        if v < 0:
+            raise nv.FlexarError(1, nv.last_error())
+        return float(v)
 
     # ------------------------------------------------------------------ config
     def set_algo(self, spec: str):

@@ -11,11 +11,18 @@ the MAX over ranks is reported.
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
         --master-addr 127.0.0.1 --master-port 29500 bench.py --gpus 8
 
-Numbers (rccl-tests convention): algbw = bytes / t and per-rank busbw = algbw * 2 (N - 1) / N.
-`value` is the whole-job aggregate: the per-rank busbw summed over the N ranks; `busbw_GBps` is the
-per-rank figure rccl-tests prints and `vs_baseline` compares that per-rank figure with the reference's
-per-rank busbw. For N = 1 the busbw factor is 0 (no inter-GPU traffic), so the N = 1 line reports the
-algbw of the out-of-place allreduce (a device copy through the flexar kernel) and says so.
+Numbers (rccl-tests convention): algbw = bytes / t and busbw = algbw * 2 (N - 1) / N. `value` IS the
+busbw of BASELINE.json's metric, the figure rccl-tests prints (one number for the job: every rank moves
+the same bytes), so `value == busbw_GBps` for every N and the 1/2/4/8 series is one quantity;
+`vs_baseline` compares it with the reference's busbw. At N = 1 the busbw factor 2(N-1)/N is 0 (no
+inter-GPU traffic), so `value` is 0 there by definition; the device-copy algbw of that run is reported
+separately as `algbw_GBps` and is not comparable with busbw. `aggregate_busbw_GBps` (busbw x N) is kept
+as an extra key for whole-job accounting.
+
+At N >= 2 the line also carries the cost model's own choice for this size (no tune table: what
+`auto` runs in production), the model's predicted time for it and its measured time, next to the
+start-up tuner's choice (BASELINE config #4 "cost-model-selected"), and the connect-time readiness
+result (probed links, self-tested protocol families).
 
 Correctness: every tuner candidate and the final choice are checked against RCCL's result
 (torch.distributed "nccl") on three consecutive calls whose inputs are scaled by 1, 1/2 and 1/4 (exact
@@ -208,6 +215,22 @@ def main():
         torch.cuda.synchronize()
         return max_over_ranks(time.perf_counter() - t0) / iters
 
+    # ---------------------------------------------------------------- cost model (no tune table)
+    model = None
+    if world > 1 and not fallback:
+        try:
+            choice = comm.describe(count, dtype)
+            spec0 = choice.split(" ")[0]
+            ok0, err0 = check("auto")
+            t0_model = timed("auto", 5) if max_over_ranks(0.0 if ok0 else 1.0) == 0.0 else None
+            model = {"choice": choice, "predicted_us": round(comm.predict_us(spec0, nbytes), 1),
+                     "measured_us": round(t0_model * 1e6, 1) if t0_model else None,
+                     "busbw_GBps": round(busbw_gbps(nbytes, t0_model, world), 2) if t0_model else None,
+                     "correct": ok0}
+            log(rank, f"cost model: {choice} predicted {model['predicted_us']} us, measured {model['measured_us']} us")
+        except nv.FlexarError as e:
+            model = {"error": str(e)}
+
     # ---------------------------------------------------------------- start-up tuner
     algo = args.algo
     tune_log = {}
@@ -257,10 +280,14 @@ def main():
                 comm.close()
                 comm = RcclOnly(dist)
         else:
-            # workgroup count for the two fastest schedules (auto = one per 32 KiB, at most 256 = one per CU;
-            # the executor needs 141 VGPRs, so 512-thread workgroups are resident one per CU and larger grids
-            # would not be co-resident)
-            grids = [g for g in (32, 64, 128) if not shared or g <= int(os.environ["FLEXAR_MAX_GRID"])]
+            # workgroup count for the two fastest schedules (auto = one per 32 KiB, at most FLEXAR_MAX_GRID);
+            # up to every workgroup the GPU keeps resident (occupancy x CUs, measured at comm creation): a
+            # rank's workgroup b only ever waits for workgroup b of its peers, so one rank per GPU needs no
+            # co-residency, but more resident workgroups keep more xGMI loads in flight. Ranks sharing one GPU
+            # must stay co-resident with each other (FLEXAR_MAX_GRID caps them).
+            resident = int(comm.stats().get("resident_blocks") or 256)
+            grids = [g for g in (32, 64, 128, 256, 512, 1024) if g <= resident and
+                     (not shared or g <= int(os.environ["FLEXAR_MAX_GRID"]))]
             best, best_grid, best_t = None, 0, float("inf")
             for spec in sorted(timings, key=timings.get)[:2]:
                 if timings[spec] < best_t:
@@ -346,7 +373,12 @@ def main():
 
     algbw = algbw_gbps(nbytes, t_step)
     busbw = busbw_gbps(nbytes, t_step, world)
-    value = busbw * world if world > 1 else algbw
+    value = busbw  # rccl-tests busbw; 0 at N = 1 by definition (see the module docstring)
+    readiness = None
+    if world > 1 and not isinstance(comm, RcclOnly):
+        topo = comm.topology()
+        readiness = {"links": topo["links"], "selftested": topo["selftested"], "disabled": topo["disabled"],
+                     "peer_links": sorted({p["link"] for p in topo["peers"] if p["link"] != "self"})}
     out = {
         "metric": "allreduce bus bandwidth (GB/s)",
         "value": round(value, 2),
@@ -370,21 +402,22 @@ def main():
             "parallelism": f"dp{world}",
             "algorithm": desc,
         },
-        "value_definition": ("per-rank busbw (rccl-tests: algbw * 2(N-1)/N) summed over the N ranks" if world > 1
-                             else "algbw of the out-of-place allreduce (N=1: the busbw factor 2(N-1)/N is 0)"),
+        "value_definition": "busbw (rccl-tests: algbw * 2(N-1)/N); 0 at N=1 by definition",
         "busbw_GBps": round(busbw, 2),
         "algbw_GBps": round(algbw, 2),
         "aggregate_busbw_GBps": round(busbw * world, 2),
         "rccl_busbw_GBps": rccl_busbw,
         "fallback": fallback,
         "tuner": tune_log or None,
+        "cost_model": model,
+        "readiness": readiness,
         "small_msg_8KiB_us_per_call": small,
     }
     if args.sweep:
         out["sweep"] = run_sweep(args, comm, world, rank, dev, dtype, op, dist, max_over_ranks)
     if world == 1:
-        out["note"] = ("N=1: busbw factor 2(N-1)/N is 0; value = algbw of the out-of-place allreduce "
-                       "(device copy through the flexar executor kernel)")
+        out["note"] = ("N=1: no inter-GPU traffic, busbw = 0 by definition (value); algbw_GBps is the device copy "
+                       "through the flexar executor kernel and is not comparable with busbw")
     if rank == 0:
         print(json.dumps(out), flush=True)
     comm.close()

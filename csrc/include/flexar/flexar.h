@@ -135,6 +135,19 @@ int flexar_broadcast(flexar_comm_t comm, const void* sendbuf, void* recvbuf, siz
 int flexar_comm_check(flexar_comm_t comm);
 /* Clear a recorded timeout once every rank has synchronised (collective use: all ranks call it). */
 int flexar_comm_clear_error(flexar_comm_t comm);
+/* Readiness (collective, after connect): run three exact integer allreduces per protocol family in
+ * `families` (1 = fence executor, 2 = write-through executor, 4 = LL, 8 = copy engines) with a short
+ * watchdog; *failed_out = families that failed on THIS rank. OR the masks of all ranks and install
+ * them with flexar_comm_set_disabled: calls then move to a verified family (ll -> oneshot,
+ * fence -> +wt -> dma) or fail with FLEXAR_ERR_UNSUPPORTED when none is left. */
+int flexar_comm_selftest(flexar_comm_t comm, uint32_t families, uint32_t* failed_out);
+int flexar_comm_set_disabled(flexar_comm_t comm, uint32_t families);
+uint32_t flexar_comm_disabled(flexar_comm_t comm);
+/* JSON: per-peer PCI bus id, device ordinal, link class (same-device / xgmi / pcie / unknown) and hop
+ * count from the connect-time probe; links used by the cost model; self-test state. */
+int flexar_comm_topology(flexar_comm_t comm, char* buf, size_t buflen);
+/* Cost-model estimate (us) of spec ("auto" = the model's own choice) on this communicator's model. */
+double flexar_comm_predict_us(flexar_comm_t comm, const char* spec, double bytes);
 /* JSON statistics (calls, bytes; per-algorithm device time when FLEXAR_PROFILE=1). */
 int flexar_comm_stats(flexar_comm_t comm, char* buf, size_t buflen);
 /* Describe the algorithm the communicator would run for (count, dtype). */
@@ -176,10 +189,20 @@ int flexar_dequantize_fp8(const void* q, void* x, int dtype, size_t n, const flo
 int flexar_pointer_is_device(const void* p); /* 1 if p is device memory */
 int flexar_current_device(void);
 int flexar_copy_device_host(void* dst, const void* src, size_t bytes); /* synchronous, any direction */
+int flexar_device_synchronize(void); /* hipDeviceSynchronize of the current device */
 void* flexar_device_alloc(size_t bytes);
 void flexar_device_free(void* p);
 
+/* Kernel facts for a (dtype, op) instantiation: kind 0 = executor (proto 0 fence, 1 +nts, 2 +wt),
+ * 1 = LL, 2 = standalone reduce. Writes workgroups resident per CU (512 threads) and VGPRs. */
+int flexar_kernel_info(int dtype, int op, int kind, int proto, int* blocks_per_cu, int* vgprs);
+
 /* ---- host-only planning utilities (no GPU needed) ------------------------ */
+/* Readiness downgrade chain (see flexar_comm_selftest) applied to `spec` for nranks with the given
+ * failed-family mask; writes the spec a call would run, or returns FLEXAR_ERR_UNSUPPORTED. */
+int flexar_downgrade_spec(const char* spec, int nranks, uint32_t disabled, int allow_dma, char* out, size_t outlen);
+/* Concurrent-link count the cost model uses for a peer list of link classes / hops (probe results). */
+int flexar_direct_links(const int32_t* link_classes, const int32_t* hops, int nranks, int self_rank);
 /* Parse an FT_TOPO string for nranks with the reference's rules (any 1 -> ring, unset -> flat,
  * product must equal nranks; trailing/duplicate separators tolerated). Writes a canonical spec
  * ("ring" or "tree:a,b,c") into out. Returns FLEXAR_ERR_INVALID on a bad topology. */

@@ -44,6 +44,7 @@
 #include "flexar/flexar.h"
 #include "flexar/host_exec.hpp"
 #include "flexar/planner.hpp"
+#include "flexar/readiness.hpp"
 
 extern "C" int flexar_pointer_is_device(const void* p);  // libflexar: hipPointerGetAttributes
 extern "C" int flexar_copy_device_host(void* dst, const void* src, size_t bytes);  // synchronous hipMemcpy
@@ -457,7 +458,26 @@ inline flexar_comm_t device_comm(MPI_Comm comm) {
   std::vector<char> mine(hs), all(hs * size);
   flexar_comm_export(d->c, mine.data());
   MPI_Allgather(mine.data(), (int)hs, MPI_BYTE, all.data(), (int)hs, MPI_BYTE, comm);
-  if (flexar_comm_connect(d->c, all.data())) { fprintf(stderr, "[flexar] connect: %s\n", flexar_last_error()); abort(); }
+  int ok = flexar_comm_connect(d->c, all.data()) == 0, all_ok = 0;
+  if (!ok) fprintf(stderr, "[flexar] rank %d connect: %s\n", rank, flexar_last_error());
+  MPI_Allreduce(&ok, &all_ok, 1, MPI_INT, MPI_MIN, comm);
+  if (!all_ok) abort();
+  // connect-time self-test (readiness.hpp): a protocol family that failed on any rank is disabled on all
+  if (size > 1 && !(getenv("FLEXAR_SELFTEST") && strcmp(getenv("FLEXAR_SELFTEST"), "0") == 0)) {
+    uint32_t failed = 0, any = 0;
+    if (flexar_comm_selftest(d->c, PF_ALL, &failed)) {
+      fprintf(stderr, "[flexar] rank %d self-test: %s\n", rank, flexar_last_error());
+      abort();
+    }
+    MPI_Allreduce(&failed, &any, 1, MPI_UINT32_T, MPI_BOR, comm);
+    if (any) {
+      flexar_comm_clear_error(d->c);  // every rank is past its self-test calls (the allreduce above)
+      flexar_comm_set_disabled(d->c, any);
+      fprintf(stderr, "[flexar] rank %d: protocol families failing the self-test disabled: %s\n", rank,
+              family_names(any).c_str());
+      if (any == PF_ALL) abort();
+    }
+  }
   MPI_Barrier(comm);
   MPI_Comm_set_attr(comm, dev_keyval(), d);
   return d->c;
@@ -521,15 +541,25 @@ inline int allreduce(const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
   MPI_Comm_size(comm, &size);
   const size_t es = dtype_size(dt);
   if (count == 0) return MPI_SUCCESS;
-  if (flexar_pointer_is_device(recvbuf)) {
+  const bool dev_out = flexar_pointer_is_device(recvbuf) != 0;
+  if (!in_place && in != recvbuf && (flexar_pointer_is_device(in) != 0) != dev_out) {
+    // mixed host/device pair: bring the input to recvbuf's side, then run in place there
+    if (flexar_copy_device_host(recvbuf, in, count * es)) return MPI_ERR_OTHER;
+    in = recvbuf;
+  }
+  if (dev_out) {
     HostComm* hc = host_comm(comm);
     if (hc->nodes > 1 && getenv("FLEXAR_MPI_FLAT_STAGING") == nullptr)
       return hierarchical_device_allreduce(*hc, in, recvbuf, count, datatype, mop, dt, op);
     if (hc->nodes == 1 || size <= 1) {  // one node: xGMI/IPC GPU engine
       flexar_comm_t c = device_comm(comm);
       int rc = flexar_allreduce(c, in, recvbuf, count, dt, op, nullptr);
+      // MPI semantics: recvbuf holds the result when the call returns (a NIC, MPI_Send or another stream
+      // may read it next), and a device watchdog timeout is this call's error, not the next one's
+      if (!rc) rc = flexar_device_synchronize();
+      if (!rc) rc = flexar_comm_check(c);
       if (rc) { fprintf(stderr, "[flexar] allreduce: %s\n", flexar_last_error()); return MPI_ERR_OTHER; }
-      return MPI_SUCCESS;  // stream-ordered on the default stream, like a CUDA-aware MPI
+      return MPI_SUCCESS;
     }
     // ranks on several nodes: IPC cannot span nodes -> stage through host memory and run the p2p engine
     hc->host_stage.resize(count * es);
@@ -562,11 +592,17 @@ inline int allreduce(const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
     uint64_t bytes = count * es;
     grid = h->threads;
     while (grid > 1 && bytes / grid < (1u << 20)) --grid;  // >= 1 MiB per host workgroup
+    // whole channels, and never more host workgroups than the flag layout has per rank
+    // (host_flag_index strides blocks by kHostMaxGrid: a larger grid would alias another rank's flags)
+    if (P.nchan > kHostMaxGrid) {
+      fprintf(stderr, "[flexar] %s needs %u channels; the host engine runs at most %u\n", s.str().c_str(), P.nchan,
+              kHostMaxGrid);
+      return MPI_ERR_ARG;
+    }
     grid = std::max<int>(grid, (int)P.nchan);
     grid = (grid + P.nchan - 1) / P.nchan * P.nchan;
-    if (grid > (int)kHostMaxGrid || (grid > 1 && (!h->pool || h->pool->size() < grid - 1))) {
-      if (grid > 1 && (!h->pool || h->pool->size() < grid - 1)) h->pool.reset(new Pool(grid - 1));
-    }
+    if (grid > (int)kHostMaxGrid) grid = (int)(kHostMaxGrid / P.nchan * P.nchan);
+    if (grid > 1 && (!h->pool || h->pool->size() < grid - 1)) h->pool.reset(new Pool(grid - 1));
   } else {
     auto jt = h->p2p.find(key);
     if (jt == h->p2p.end()) jt = h->p2p.emplace(key, build_p2p(*h, s, count, es, 1.0f)).first;

@@ -83,6 +83,15 @@ class Planner {
       for (int w : spec.widths)
         if (w < 2) { if (err) *err = "tree width < 2"; return false; }
       build_tree_lonely(spec.widths, (uint32_t)prod, spec.ag == AgMode::PULL, spec.fuse);
+      if (r >= (uint32_t)prod) {
+        // A lonely rank allocates only its fold slots, the tree ranks much more. Every rank sizes its
+        // pieces (and the MPI engine its shared window) from its own stg_elems, so all ranks must report
+        // the same figure: take the tree's (rank 0 is always a tree rank and a partner).
+        Program Q;
+        Planner twin(N, 0, count, esize, scale);
+        if (!twin.build(spec, &Q, err)) return false;
+        stg = std::max(stg, Q.stg_elems);
+      }
       P->desc = spec.str();
     } else if (spec.kind == AlgoKind::ONESHOT) {
       build_oneshot();

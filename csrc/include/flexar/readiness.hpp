@@ -1,0 +1,149 @@
+// Connect-time readiness of a communicator: which device protocol families passed the exact
+// self-test, how a requested algorithm is rewritten onto a verified family (the downgrade chain),
+// the per-peer link classes found by the topology probe, and the fingerprint of the settings every
+// rank must agree on.
+//
+// Reference counterpart: the per-communicator setup of FlexTree_Context (allreduce_over_mpi/
+// mpi_mod.hpp:216-243) reads the communicator shape and trusts the transport. MPI_Isend/Irecv never
+// fail silently; the device protocols here can (a cross-device visibility bug would corrupt sums
+// without hanging), so every protocol family is verified on the real links before a production call
+// may use it, and the machine shape (the reference's hostfile and fan-in penalty,
+// mpi_config_file:1-16, cost_model/CostModel.h:1-20) is probed instead of assumed.
+// Host-only: unit-tested on the CPU (tests/test_readiness.py).
+#pragma once
+
+#include <stdint.h>
+
+#include <cstdlib>
+#include <string>
+
+#include "flexar/topology.hpp"
+
+namespace flexar {
+
+// Protocol families. Every algorithm runs on exactly one of them.
+enum : uint32_t {
+  PF_FENCE = 1,  // executor, plain stores + system release/acquire (default, "+nts" included)
+  PF_WT = 2,     // executor, write-through payload ("+wt")
+  PF_LL = 4,     // flag-free {data, epoch} granules ("ll")
+  PF_DMA = 8,    // copy engines + stream-ordered flag writes ("dma")
+  PF_ALL = 15
+};
+
+inline uint32_t proto_family(const AlgoSpec& s) {
+  switch (s.kind) {
+    case AlgoKind::LL: return PF_LL;
+    case AlgoKind::DMA: return PF_DMA;
+    default: return s.wt ? PF_WT : PF_FENCE;
+  }
+}
+
+inline std::string family_names(uint32_t mask) {
+  static const char* n[] = {"fence", "wt", "ll", "dma"};
+  std::string s;
+  for (int i = 0; i < 4; ++i)
+    if (mask & (1u << i)) s += (s.empty() ? "" : ",") + std::string(n[i]);
+  return s.empty() ? "none" : s;
+}
+
+// Rewrite `s` onto a family that is not in `disabled`, keeping the schedule where possible:
+//   ll    -> oneshot (same single hop, flag hand-off instead of granules)
+//   fence -> the same schedule with "+wt"
+//   wt    -> dma (the flat exchange on the copy engines) when the spec is an allreduce schedule
+//   dma   -> flat+pull on the executor (fence, then wt)
+// Returns false (and says why) when no verified family is left for this call.
+inline bool downgrade_spec(AlgoSpec* s, int nranks, uint32_t disabled, bool allow_dma, std::string* why) {
+  disabled &= PF_ALL;
+  for (int hop = 0; hop < 6; ++hop) {
+    const uint32_t f = proto_family(*s);
+    if (!(disabled & f)) return true;
+    switch (f) {
+      case PF_LL: s->kind = AlgoKind::ONESHOT; break;
+      case PF_FENCE: s->wt = true; s->nts = false; break;
+      case PF_WT:
+        if (allow_dma && !(disabled & PF_DMA)) {
+          *s = AlgoSpec();
+          s->kind = AlgoKind::DMA;
+        } else {
+          if (why) *why = "no verified device protocol for " + s->str() + " (failed self-test: " +
+                          family_names(disabled) + ")";
+          return false;
+        }
+        break;
+      case PF_DMA:
+        *s = AlgoSpec();
+        s->kind = AlgoKind::TREE;
+        s->ag = AgMode::PULL;
+        s->widths = {nranks};
+        break;
+    }
+  }
+  if (why) *why = "no verified device protocol (failed self-test: " + family_names(disabled) + ")";
+  return false;
+}
+
+// ---- per-peer link classes (topology probe) ----------------------------------------------------
+enum : int32_t {
+  LINK_UNKNOWN = 0,  // peer device not visible in this process (e.g. HIP_VISIBLE_DEVICES): IPC only
+  LINK_SAME = 1,     // the same GPU (ranks sharing a device: one HBM, no link)
+  LINK_XGMI = 2,     // xGMI, hop count in `hops`
+  LINK_PCIE = 3,     // PCIe peer-to-peer
+  LINK_OTHER = 4
+};
+
+inline const char* link_name(int32_t k) {
+  switch (k) {
+    case LINK_SAME: return "same-device";
+    case LINK_XGMI: return "xgmi";
+    case LINK_PCIE: return "pcie";
+    case LINK_OTHER: return "other";
+    default: return "unknown";
+  }
+}
+
+// HSA link types (hsa_ext_amd.h HSA_AMD_LINK_INFO_TYPE_*) reported by hipExtGetLinkTypeAndHopCount.
+inline int32_t link_class_of_hsa(uint32_t hsa_type) {
+  switch (hsa_type) {
+    case 4: return LINK_XGMI;
+    case 2: return LINK_PCIE;
+    default: return LINK_OTHER;
+  }
+}
+
+// Direct xGMI links to drive concurrently for the cost model: the number of peers one xGMI hop away
+// (7 on a fully connected 8-GPU node), at least 1. Ranks on the same device count as one "link"
+// (the shared HBM); unknown peers count as direct links.
+inline int direct_links(const int32_t* cls, const int32_t* hops, int n, int self) {
+  int x = 0;
+  for (int p = 0; p < n; ++p) {
+    if (p == self) continue;
+    if ((cls[p] == LINK_XGMI && hops[p] <= 1) || cls[p] == LINK_UNKNOWN) ++x;
+  }
+  return x < 1 ? 1 : x;
+}
+
+// ---- settings fingerprint ----------------------------------------------------------------------
+// Every rank must resolve a call to the same schedule, pieces and grid. Those follow from these
+// settings (plus the loaded tune table, hashed by the caller as `extra`); a difference is rejected at
+// connect time instead of surfacing as a device timeout in the first collective (FNV-1a over
+// "name=value;").
+inline uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
+  for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
+  return h;
+}
+inline const char* const* fingerprint_vars() {
+  static const char* v[] = {"FLEXAR_ALGO",     "FT_TOPO",          "FLEXAR_CHUNK_BYTES", "FLEXAR_NCHANNELS",
+                            "FLEXAR_MAX_GRID", "FLEXAR_MIN_BLOCK_BYTES", "FLEXAR_MODEL",
+                            "FLEXAR_SELFTEST", nullptr};
+  return v;
+}
+inline uint64_t env_fingerprint(const std::string& extra) {
+  uint64_t h = fnv1a(extra);
+  for (const char* const* v = fingerprint_vars(); *v; ++v) {
+    const char* e = getenv(*v);
+    h = fnv1a(std::string(*v) + "=" + (e ? e : "") + ";", h);
+  }
+  return h;
+}
+
+}  // namespace flexar

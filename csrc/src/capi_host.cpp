@@ -14,6 +14,7 @@
 #include "flexar/flexar.h"
 #include "flexar/host_exec.hpp"
 #include "flexar/planner.hpp"
+#include "flexar/readiness.hpp"
 #include "internal.hpp"
 
 namespace flexar {
@@ -256,6 +257,20 @@ int flexar_simulate_bcast(const char* spec, int nranks, size_t count, int dtype,
     if (!validate_program(progs[r], nranks, r, count, count, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
   }
   return dispatch_dtype_op<SimRun>(dtype, FLEXAR_SUM, progs, nranks, grid, ncalls, 0, inputs, outputs, count);
+}
+
+int flexar_downgrade_spec(const char* spec, int nranks, uint32_t disabled, int allow_dma, char* out, size_t outlen) {
+  AlgoSpec s;
+  std::string err;
+  if (nranks < 1 || !parse_algo(spec ? spec : "auto", nranks, &s, &err)) { set_error(err.empty() ? "bad arguments" : err); return FLEXAR_ERR_INVALID; }
+  if (s.kind == AlgoKind::AUTO) { set_error("downgrade needs a concrete spec"); return FLEXAR_ERR_INVALID; }
+  if (!downgrade_spec(&s, nranks, disabled, allow_dma != 0, &err)) { set_error(err); return FLEXAR_ERR_UNSUPPORTED; }
+  return copy_out(s.str(), out, outlen);
+}
+
+int flexar_direct_links(const int32_t* cls, const int32_t* hops, int nranks, int self) {
+  if (!cls || !hops || nranks < 1 || self < 0 || self >= nranks) return -1;
+  return direct_links(cls, hops, nranks, self);
 }
 
 int flexar_reduce_host(void* dst, const void* const* srcs, int nsrc, size_t count, int dtype, int op, float scale) {

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -30,6 +31,7 @@
 #include "flexar/flexar.h"
 #include "flexar/log.hpp"
 #include "flexar/planner.hpp"
+#include "flexar/readiness.hpp"
 #include "internal.hpp"
 
 namespace flexar {
@@ -56,6 +58,8 @@ struct CommHandle {
   int32_t pid;
   int32_t device;
   char host[64];
+  char bus[32];          // PCI bus id of the rank's GPU (hipDeviceGetPCIBusId): resolves the peer device
+  uint64_t fingerprint;  // settings every rank must agree on (readiness.hpp env_fingerprint)
 };
 
 struct DevProgram {
@@ -170,6 +174,19 @@ struct flexar_comm {
   };
   CallMemo memo[16];
   uint64_t memo_gen = 1;
+  // readiness (readiness.hpp): protocol families that failed the connect-time self-test, per-peer
+  // link classes from the topology probe, residency of the executor kernel
+  uint32_t disabled = 0;
+  uint32_t selftested = 0;  // families the self-test ran
+  int32_t link_cls[kMaxRanks] = {};
+  int32_t link_hops[kMaxRanks] = {};
+  int32_t peer_dev[kMaxRanks] = {};  // peer's device ordinal in THIS process (-1 = not visible)
+  char peer_bus[kMaxRanks][32] = {};
+  bool links_from_env = false;  // FLEXAR_MODEL fixed the link count: the probe does not override it
+  int resident = 0;             // executor workgroups resident at once on this GPU (occupancy x CUs)
+  int* st_buf = nullptr;        // self-test buffers (device)
+  uint32_t* st_bad = nullptr;   // self-test mismatch counter (host-mapped)
+  uint32_t* st_bad_dev = nullptr;
 };
 
 namespace flexar {
@@ -209,7 +226,20 @@ static int resolve_spec(flexar_comm* c, const char* algo, double bytes, AlgoSpec
     }
   }
   if (s.kind == AlgoKind::TREE && s.ag == AgMode::AUTO) s.ag = AgMode::PULL;
+  if (c->disabled) {
+    std::string why;
+    if (!downgrade_spec(&s, c->nranks, c->disabled, true, &why)) { set_error(why); return FLEXAR_ERR_UNSUPPORTED; }
+  }
   *out = s;
+  return 0;
+}
+
+// An executor schedule chosen after resolve_spec (RS/AG/broadcast force their own shape, a captured
+// communicator replaces dma): move it onto a verified protocol family, never onto dma.
+static int executor_proto(flexar_comm* c, AlgoSpec* s) {
+  if (!c->disabled) return 0;
+  std::string why;
+  if (!downgrade_spec(s, c->nranks, c->disabled, false, &why)) { set_error(why); return FLEXAR_ERR_UNSUPPORTED; }
   return 0;
 }
 
@@ -363,6 +393,7 @@ static int run_rs_ag(flexar_comm* c, Coll coll, const void* in, void* out, size_
   int rc = resolve_spec(c, algo, (double)count * es * c->nranks, &s);
   if (rc) return rc;
   if (s.kind != AlgoKind::RING) s.kind = AlgoKind::TREE, s.widths = {c->nranks}, s.ag = AgMode::PUSH;
+  if ((rc = executor_proto(c, &s))) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
   if ((rc = order_call(c, st))) return rc;
   uint64_t piece = count;
@@ -401,7 +432,7 @@ static int bcast_spec(flexar_comm* c, const char* algo, uint64_t bytes, AlgoSpec
   if (s.kind == AlgoKind::LL) s.kind = AlgoKind::ONESHOT;
   if (s.kind != AlgoKind::ONESHOT) s.kind = AlgoKind::TREE, s.widths = {c->nranks};
   *out = s;
-  return 0;
+  return executor_proto(c, out);
 }
 
 // Broadcast of `count` elements from `root` (root reads `in`; every rank writes `out`), split into
@@ -599,6 +630,49 @@ static int run_dma(flexar_comm* const* cs, int ncomm, const char* const* ins, ch
   return 0;
 }
 
+// Settings fingerprint exchanged in the handle (readiness.hpp): environment knobs + workspace size +
+// the loaded tune table.
+static uint64_t comm_fingerprint(flexar_comm* c) {
+  std::string extra = "ws=" + std::to_string(c->ws_bytes) + ";";
+  for (auto& n : c->tune.rows)
+    for (auto& row : n.second) extra += std::to_string(n.first) + " " + std::to_string(row.first) + " " + row.second + ";";
+  return env_fingerprint(extra);
+}
+
+// Self-test pattern (flexar_comm_selftest): rank r contributes (r + 1) * p(i), p(i) in [1, 1000], so
+// the exact sum is N (N + 1) / 2 * p(i); OUT is poisoned so an element nobody wrote is caught too.
+__device__ FX_INLINE int selftest_pattern(uint64_t i, uint32_t salt) { return (int)((i * 7 + salt) % 1000) + 1; }
+static __global__ void selftest_fill(int* in, int* out, uint64_t n, int rank, uint32_t salt) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    in[i] = (rank + 1) * selftest_pattern(i, salt);
+    out[i] = -1;
+  }
+}
+static __global__ void selftest_check(const int* out, uint64_t n, int nranks, uint32_t salt, uint32_t* bad) {
+  uint32_t mine = 0;
+  const int tri = nranks * (nranks + 1) / 2;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    mine += out[i] != tri * selftest_pattern(i, salt);
+  if (mine) __hip_atomic_fetch_add(bad, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Executor workgroups resident at once on this device: occupancy of the fp32 fence executor (the
+// largest register footprint among the hot instantiations is within one workgroup of it) x CUs.
+static int resident_blocks(int device) {
+  LaunchArgs la;
+  la.kind = LAUNCH_QUERY;
+  int occ = 0, regs = 0;
+  la.occ_out = &occ;
+  la.regs_out = &regs;
+  if (launch_dtype(FLEXAR_FLOAT32, FLEXAR_SUM, la) != 0 || occ < 1) return 0;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return occ * cus;
+}
+
 static int check_err(flexar_comm* c) {
   uint32_t e = __atomic_load_n(c->err_host, __ATOMIC_ACQUIRE);
   if (e & 0x40000000u) {
@@ -654,6 +728,7 @@ static int alloc_workspace(flexar_comm* c, size_t ws) {
 
 static void init_defaults(flexar_comm* c) {
   c->model = XgmiModel::from_env();
+  if (const char* m = getenv("FLEXAR_MODEL")) c->links_from_env = std::count(m, m + strlen(m), ',') >= 4;
   c->have_tune = c->tune.load(getenv("FLEXAR_TUNE_FILE"));
   c->timeout_ticks = env_u64("FLEXAR_TIMEOUT_MS", 20000) * 100000ull;  // 100 MHz s_memrealtime
   c->max_grid = (int)env_u64("FLEXAR_MAX_GRID", 256);
@@ -705,6 +780,7 @@ int flexar_comm_create(int rank, int nranks, int device, size_t workspace_bytes,
   size_t ws = workspace_bytes ? workspace_bytes : env_u64("FLEXAR_WORKSPACE_BYTES", 512ull << 20);
   int rc = alloc_workspace(c.get(), ws);
   if (rc) return rc;
+  c->resident = resident_blocks(device);
   c->peer_stg[rank] = c->stg;
   c->peer_flags[rank] = c->flags;
   if (nranks == 1) c->connected = true;
@@ -729,34 +805,231 @@ int flexar_comm_export(flexar_comm_t c, void* handle_out) {
   h.pid = (int32_t)getpid();
   h.device = c->device;
   gethostname(h.host, sizeof(h.host) - 1);
+  if (hipDeviceGetPCIBusId(h.bus, sizeof(h.bus) - 1, c->device) != hipSuccess) {
+    (void)hipGetLastError();
+    snprintf(h.bus, sizeof(h.bus), "dev%d", c->device);
+  }
+  h.fingerprint = comm_fingerprint(c);
   memcpy(handle_out, &h, sizeof(h));
   return 0;
 }
 
+// Readiness gate (readiness.hpp), before any peer memory is mapped: every handle comes from this host,
+// the same library version and the same settings; every peer GPU that this process can see is
+// reachable peer-to-peer (hipDeviceCanAccessPeer) and its link class / hop count is recorded
+// (hipExtGetLinkTypeAndHopCount) and feeds the cost model's concurrent-link count. A failure names
+// the rank and the reason instead of surfacing as a raw hipIpcOpenMemHandle error or a device hang.
 int flexar_comm_connect(flexar_comm_t c, const void* all) {
   if (!c || !all) { set_error("null argument"); return FLEXAR_ERR_INVALID; }
   FX_HIP(hipSetDevice(c->device));
   const CommHandle* hs = (const CommHandle*)all;
+  const CommHandle& me = hs[c->rank];
   for (int r = 0; r < c->nranks; ++r) {
     const CommHandle& h = hs[r];
+    const std::string who = "rank " + std::to_string(r);
     if (h.magic != kHandleMagic || h.rank != r || h.nranks != c->nranks) {
-      set_error("bad handle from rank " + std::to_string(r) + " (mismatched ranks or version)");
+      set_error("bad handle from " + who + " (mismatched ranks or version)");
+      return FLEXAR_ERR_INVALID;
+    }
+    if (h.version != me.version) {
+      set_error(who + " runs another flexar version (" + std::to_string(h.version) + " vs " +
+                std::to_string(me.version) + ")");
       return FLEXAR_ERR_INVALID;
     }
     if (h.ws_bytes != c->ws_bytes) {
-      set_error("workspace size differs across ranks");
+      set_error("workspace size differs across ranks (" + who + ": " + std::to_string(h.ws_bytes) + " B, rank " +
+                std::to_string(c->rank) + ": " + std::to_string(c->ws_bytes) + " B)");
       return FLEXAR_ERR_INVALID;
     }
+    if (strncmp(h.host, me.host, sizeof(h.host)) != 0) {
+      set_error(who + " is on host '" + std::string(h.host) + "', rank " + std::to_string(c->rank) + " on '" +
+                std::string(me.host) + "': the device transport is intra-node (IPC over xGMI); use the "
+                "hierarchical allreduce or RCCL across nodes");
+      return FLEXAR_ERR_UNSUPPORTED;
+    }
+    if (h.fingerprint != me.fingerprint) {
+      std::string vars;
+      for (const char* const* v = fingerprint_vars(); *v; ++v) vars += std::string(vars.empty() ? "" : ", ") + *v;
+      set_error(who + " resolves calls with different settings than rank " + std::to_string(c->rank) +
+                " (one of " + vars + " or the tune table differs): every rank must pick the same schedule");
+      return FLEXAR_ERR_INVALID;
+    }
+    memcpy(c->peer_bus[r], h.bus, sizeof(c->peer_bus[r]));
+    c->peer_bus[r][sizeof(c->peer_bus[r]) - 1] = 0;
+    c->peer_dev[r] = -1;
+    if (r == c->rank) {
+      c->peer_dev[r] = c->device;
+      c->link_cls[r] = LINK_SAME;
+      continue;
+    }
+    int pd = -1;
+    if (hipDeviceGetByPCIBusId(&pd, c->peer_bus[r]) != hipSuccess) {
+      (void)hipGetLastError();
+      pd = -1;
+    }
+    c->peer_dev[r] = pd;
+    if (pd < 0) {
+      c->link_cls[r] = LINK_UNKNOWN;  // not visible here (HIP_VISIBLE_DEVICES): IPC still maps it
+    } else if (pd == c->device) {
+      c->link_cls[r] = LINK_SAME;
+    } else {
+      int can = 0;
+      FX_HIP(hipDeviceCanAccessPeer(&can, c->device, pd));
+      if (!can) {
+        set_error("GPU " + std::to_string(c->device) + " (" + me.bus + ") cannot access GPU " + std::to_string(pd) +
+                  " (" + c->peer_bus[r] + ") of " + who + " peer-to-peer: no xGMI/PCIe P2P path");
+        return FLEXAR_ERR_UNSUPPORTED;
+      }
+      uint32_t lt = 0, hops = 0;
+      if (hipExtGetLinkTypeAndHopCount(c->device, pd, &lt, &hops) == hipSuccess) {
+        c->link_cls[r] = link_class_of_hsa(lt);
+        c->link_hops[r] = (int32_t)hops;
+      } else {
+        (void)hipGetLastError();
+        c->link_cls[r] = LINK_OTHER;
+      }
+    }
+  }
+  for (int r = 0; r < c->nranks; ++r) {
     if (r == c->rank) continue;
+    const CommHandle& h = hs[r];
     void* p = nullptr;
-    FX_HIP(hipIpcOpenMemHandle(&p, h.stg, hipIpcMemLazyEnablePeerAccess));
-    c->peer_stg[r] = (char*)p;
-    FX_HIP(hipIpcOpenMemHandle(&p, h.flags, hipIpcMemLazyEnablePeerAccess));
+    hipError_t e = hipIpcOpenMemHandle(&p, h.stg, hipIpcMemLazyEnablePeerAccess);
+    if (e == hipSuccess) {
+      c->peer_stg[r] = (char*)p;
+      e = hipIpcOpenMemHandle(&p, h.flags, hipIpcMemLazyEnablePeerAccess);
+      if (e != hipSuccess) (void)hipIpcCloseMemHandle(c->peer_stg[r]);
+    }
+    if (e != hipSuccess) {
+      set_error("mapping the workspace of rank " + std::to_string(r) + " (" + link_name(c->link_cls[r]) + " peer " +
+                c->peer_bus[r] + ") failed: hipIpcOpenMemHandle: " + hipGetErrorString(e) +
+                " (HSA_ENABLE_IPC_MODE_LEGACY=0 is needed on dmabuf-only drivers)");
+      return FLEXAR_ERR_HIP;
+    }
     c->peer_flags[r] = (uint64_t*)p;
     c->opened[r] = true;
   }
+  if (!c->links_from_env) c->model.links = direct_links(c->link_cls, c->link_hops, c->nranks, c->rank);
+  c->memo_gen++;
   c->connected = true;
   return 0;
+}
+
+// Connect-time exact self-test (collective: every rank calls it after connect, in the same order).
+// Each protocol family runs three allreduces of an integer pattern whose sum every rank can compute
+// locally; the patterns change per call, so a read of a staging line left over from either of the two
+// previous calls (the parity halves) is a mismatch. Waits use a short watchdog, so a family whose
+// hand-off never becomes visible fails in seconds instead of hanging. Returns the mask of families
+// that failed ON THIS RANK; the caller ORs the masks of all ranks and installs the result with
+// flexar_comm_set_disabled (a family is usable only if it passed everywhere).
+int flexar_comm_selftest(flexar_comm_t c, uint32_t families, uint32_t* failed_out) {
+  if (!c || !failed_out) { set_error("null argument"); return FLEXAR_ERR_INVALID; }
+  if (!c->connected) { set_error("communicator not connected"); return FLEXAR_ERR_STATE; }
+  *failed_out = 0;
+  if (c->nranks == 1) return 0;
+  FX_HIP(hipSetDevice(c->device));
+  const uint64_t n = 65536 + 77;  // 256 KiB + an odd tail: several workgroups, a scalar tail, LL-sized
+  if (!c->st_buf) {
+    FX_HIP(hipMalloc(&c->st_buf, 2 * n * sizeof(int)));
+    FX_HIP(hipHostMalloc((void**)&c->st_bad, 64, hipHostMallocMapped));
+    FX_HIP(hipHostGetDevicePointer((void**)&c->st_bad_dev, c->st_bad, 0));
+  }
+  hipStream_t st = nullptr;
+  FX_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  const uint64_t saved_timeout = c->timeout_ticks, saved_gen = c->memo_gen;
+  const uint32_t saved_disabled = c->disabled;
+  const bool saved_profile = c->profile;
+  const uint64_t saved_calls = c->calls, saved_bytes = c->bytes;
+  c->disabled = 0;  // the self-test drives each family explicitly
+  c->profile = false;  // and stays out of the application's statistics
+  c->timeout_ticks = env_u64("FLEXAR_SELFTEST_TIMEOUT_MS", 2000) * 100000ull;
+  struct Case { uint32_t fam; const char* spec; };
+  const Case cases[] = {{PF_FENCE, "flat+pull"}, {PF_FENCE, "ring"}, {PF_WT, "flat+pull+wt"}, {PF_LL, "ll"},
+                        {PF_DMA, "dma"}};
+  int* in = c->st_buf;
+  int* out = c->st_buf + n;
+  const int N = c->nranks;
+  int rc = 0;
+  for (const Case& k : cases) {
+    if (!(families & k.fam)) continue;
+    if (k.fam == PF_LL && !ll_usable(c, n, 4)) continue;
+    c->selftested |= k.fam;
+    logf(LOG_INFO, c->rank, "self-test: %s", k.spec);
+    for (int call = 0; call < 3 && !rc; ++call) {
+      const uint32_t salt = (uint32_t)(call * 131 + k.fam * 17);
+      hipLaunchKernelGGL(selftest_fill, dim3(64), dim3(256), 0, st, in, out, n, c->rank, salt);
+      if ((rc = hipGetLastError() != hipSuccess ? FLEXAR_ERR_HIP : 0)) break;
+      int e = flexar_allreduce_ex(c, in, out, n, FLEXAR_INT32, FLEXAR_SUM, st, k.spec, 1.0f);
+      if (e == FLEXAR_ERR_TIMEOUT || e == FLEXAR_ERR_STATE) {
+        *failed_out |= k.fam;  // a previous call of this family timed out
+      } else if (e) {
+        rc = e;
+        break;
+      }
+      *c->st_bad = 0;
+      hipLaunchKernelGGL(selftest_check, dim3(64), dim3(256), 0, st, out, n, N, salt, c->st_bad_dev);
+      if (hipStreamSynchronize(st) != hipSuccess) { rc = FLEXAR_ERR_HIP; break; }
+      if (__atomic_load_n(c->st_bad, __ATOMIC_ACQUIRE) != 0) *failed_out |= k.fam;
+      if (__atomic_load_n(c->err_host, __ATOMIC_ACQUIRE) != 0) {
+        *failed_out |= k.fam;
+        __atomic_store_n(c->err_host, 0u, __ATOMIC_RELEASE);  // every rank still makes every call
+      }
+    }
+    if (rc) break;
+  }
+  (void)hipStreamSynchronize(st);
+  (void)hipStreamDestroy(st);
+  c->have_last = false;  // `st` is gone (and synchronised): the next call must not order behind it
+  c->timeout_ticks = saved_timeout;
+  c->disabled = saved_disabled;
+  c->profile = saved_profile;
+  c->calls = saved_calls;
+  c->bytes = saved_bytes;
+  c->memo_gen = saved_gen + 1;
+  if (rc == FLEXAR_ERR_HIP && std::string(flexar_last_error()).empty()) set_error("self-test: HIP error");
+  logf(*failed_out ? LOG_WARN : LOG_INFO, c->rank, "self-test: ran %s, failed on this rank: %s",
+       family_names(c->selftested).c_str(), family_names(*failed_out).c_str());
+  return rc;
+}
+
+// Cost-model time (us) of `spec` on this communicator's model (links from the connect-time probe).
+double flexar_comm_predict_us(flexar_comm_t c, const char* spec, double bytes) {
+  if (!c) return -1.0;
+  AlgoSpec s;
+  std::string err;
+  if (!parse_algo(spec ? spec : "auto", c->nranks, &s, &err)) { set_error(err); return -1.0; }
+  if (s.kind == AlgoKind::AUTO) s = select_plan(c->model, c->nranks, bytes);
+  return c->model.cost_us(s, c->nranks, bytes);
+}
+
+int flexar_comm_set_disabled(flexar_comm_t c, uint32_t families) {
+  if (!c) return FLEXAR_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->disabled = families & PF_ALL;
+  c->memo_gen++;
+  return 0;
+}
+
+uint32_t flexar_comm_disabled(flexar_comm_t c) { return c ? c->disabled : 0; }
+
+// JSON: the topology probe's view of every peer and the readiness state.
+int flexar_comm_topology(flexar_comm_t c, char* buf, size_t buflen) {
+  if (!c || !buf) return FLEXAR_ERR_INVALID;
+  std::string j = "{\"rank\": " + std::to_string(c->rank) + ", \"device\": " + std::to_string(c->device) +
+                  ", \"links\": " + std::to_string(c->model.links) + ", \"resident_blocks\": " +
+                  std::to_string(c->resident) + ", \"selftested\": \"" + family_names(c->selftested) +
+                  "\", \"disabled\": \"" + (c->disabled ? family_names(c->disabled) : std::string()) +
+                  "\", \"peers\": [";
+  for (int r = 0; r < c->nranks; ++r) {
+    char t[256];
+    snprintf(t, sizeof(t), "%s{\"rank\": %d, \"bus\": \"%s\", \"device\": %d, \"link\": \"%s\", \"hops\": %d}",
+             r ? ", " : "", r, c->peer_bus[r], c->peer_dev[r], r == c->rank ? "self" : link_name(c->link_cls[r]),
+             c->link_hops[r]);
+    j += t;
+  }
+  j += "]}";
+  snprintf(buf, buflen, "%s", j.c_str());
+  return j.size() < buflen ? 0 : FLEXAR_ERR_NOMEM;
 }
 
 int flexar_comm_destroy(flexar_comm_t c) {
@@ -778,6 +1051,8 @@ int flexar_comm_destroy(flexar_comm_t c) {
   }
   if (c->dma_fork) (void)hipEventDestroy(c->dma_fork);
   if (c->order_ev) (void)hipEventDestroy(c->order_ev);
+  if (c->st_buf) (void)hipFree(c->st_buf);
+  if (c->st_bad) (void)hipHostFree(c->st_bad);
   (void)hipFree(c->stg);
   (void)hipFree(c->flags);
   (void)hipFree(c->epochs);
@@ -894,12 +1169,14 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     if ((rc = resolve_spec(c, algo, (double)count * es, &s))) return rc;
     if (s.kind == AlgoKind::LL && !ll_usable(c, count, es)) s.kind = AlgoKind::ONESHOT;
     if (s.kind == AlgoKind::DMA && c->nranks == 1) s.kind = AlgoKind::ONESHOT;  // one rank: the executor's copy
+    if ((rc = executor_proto(c, &s))) return rc;  // the LL -> oneshot rewrite above may land on a failed family
   }
   if (s.kind == AlgoKind::DMA && c->captured) {  // not replay-safe (see flexar_comm::captured)
     AlgoSpec f;
     std::string err;
     if (!parse_algo("flat+pull", c->nranks, &f, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
     s = f;
+    if ((rc = executor_proto(c, &s))) return rc;
   }
   auto remember = [&](uint64_t piece, DevProgram* dp, int grid) {
     if (hit) return;
@@ -1030,7 +1307,10 @@ int flexar_comm_stats(flexar_comm_t c, char* buf, size_t buflen) {
   }
   c->prof_pending.clear();
   std::string j = "{\"calls\": " + std::to_string(c->calls) + ", \"bytes\": " + std::to_string(c->bytes) +
-                  ", \"plans_cached\": " + std::to_string(c->cache.size()) + ", \"profile\": {";
+                  ", \"plans_cached\": " + std::to_string(c->cache.size()) + ", \"links\": " +
+                  std::to_string(c->model.links) + ", \"resident_blocks\": " + std::to_string(c->resident) +
+                  ", \"selftested\": \"" + family_names(c->selftested) + "\", \"disabled\": \"" +
+                  (c->disabled ? family_names(c->disabled) : std::string()) + "\", \"profile\": {";
   bool first = true;
   for (auto& kv : c->prof) {
     char t[256];
@@ -1332,6 +1612,11 @@ int flexar_pointer_is_device(const void* p) {
   return a.type == hipMemoryTypeDevice ? 1 : 0;
 }
 
+int flexar_device_synchronize(void) {
+  FX_HIP(hipDeviceSynchronize());
+  return 0;
+}
+
 int flexar_copy_device_host(void* dst, const void* src, size_t bytes) {
   FX_HIP(hipDeviceSynchronize());  // the device buffer may still be written by queued work
   FX_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
@@ -1344,6 +1629,17 @@ void* flexar_device_alloc(size_t bytes) {
   return p;
 }
 void flexar_device_free(void* p) { (void)hipFree(p); }
+
+int flexar_kernel_info(int dtype, int op, int kind, int proto, int* blocks_per_cu, int* vgprs) {
+  if (kind < 0 || kind > 2 || proto < 0 || proto > 2) { set_error("bad kernel_info arguments"); return FLEXAR_ERR_INVALID; }
+  LaunchArgs la;
+  la.kind = LAUNCH_QUERY;
+  la.query = kind;
+  la.proto = proto;
+  la.occ_out = blocks_per_cu;
+  la.regs_out = vgprs;
+  return launch_dtype(dtype, op, la);
+}
 
 int flexar_current_device(void) {
   int d = 0;

@@ -8,9 +8,36 @@
 
 namespace flexar {
 
+template <typename K>
+inline int query_kernel(K kern, const LaunchArgs& a) {
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kExecThreads, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("occupancy query failed");
+    return FLEXAR_ERR_HIP;
+  }
+  hipFuncAttributes fa;
+  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kern)) != hipSuccess) {
+    (void)hipGetLastError();
+    fa.numRegs = 0;
+  }
+  if (a.occ_out) *a.occ_out = occ;
+  if (a.regs_out) *a.regs_out = fa.numRegs;
+  return 0;
+}
+
 template <typename T, typename OP>
 inline int launch_one(const LaunchArgs& a) {
   switch (a.kind) {
+    case LAUNCH_QUERY:
+      if (a.query == 1) {
+        if (sizeof(T) > 4) return FLEXAR_ERR_UNSUPPORTED;
+        return query_kernel(ll_kernel<T, OP>, a);
+      }
+      if (a.query == 2) return query_kernel(a.proto == PM_WT ? reduce_kernel<T, OP, PM_WT> : reduce_kernel<T, OP, PM_FENCE>, a);
+      return query_kernel(a.proto == PM_WT ? exec_kernel<T, OP, PM_WT>
+                                           : a.proto == PM_FENCE_NTS ? exec_kernel<T, OP, PM_FENCE_NTS>
+                                                                     : exec_kernel<T, OP, PM_FENCE>, a);
     case LAUNCH_EXEC:
       if (a.proto == PM_WT)
         hipLaunchKernelGGL((exec_kernel<T, OP, PM_WT>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);

@@ -8,7 +8,10 @@
 
 namespace flexar {
 
-enum LaunchKind { LAUNCH_EXEC = 0, LAUNCH_GROUP = 1, LAUNCH_REDUCE = 2, LAUNCH_LL = 3, LAUNCH_LL_GROUP = 4 };
+// LAUNCH_QUERY launches nothing: it reports the occupancy (workgroups per CU) and the VGPR count of the
+// kernel that `proto` / `query` select (query 0 = executor, 1 = LL, 2 = standalone reduce).
+enum LaunchKind { LAUNCH_EXEC = 0, LAUNCH_GROUP = 1, LAUNCH_REDUCE = 2, LAUNCH_LL = 3, LAUNCH_LL_GROUP = 4,
+                  LAUNCH_QUERY = 5 };
 
 struct LaunchArgs {
   int kind = LAUNCH_EXEC;
@@ -25,6 +28,9 @@ struct LaunchArgs {
   float scale = 1.0f;
   int vec = 1;
   int proto = PM_FENCE;  // executor protocol mode (PM_*: "+nts", "+wt")
+  int query = 0;         // QUERY: which kernel
+  int* occ_out = nullptr;
+  int* regs_out = nullptr;
 };
 
 // Defined in k_<dtype>.hip; returns 0 or a FLEXAR_ERR_* code.

@@ -478,3 +478,71 @@ def test_ipc_randomized_call_sequence(cuda, world, fault):
     for rank, bad, tb in res:
         assert tb is None, tb
         assert not bad, (rank, bad[:5])
+
+
+def _readiness_worker(rank, world, port, q, fault):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
+                          FLEXAR_TIMEOUT_MS="20000", FLEXAR_SELFTEST_TIMEOUT_MS="300")
+        if fault:
+            os.environ["FLEXAR_FAULT_INJECT"] = fault
+        import torch.distributed as dist
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from allreduce_over_mpi_amd.parallel import Communicator
+
+        comm = Communicator(workspace_bytes=32 << 20)
+        topo = comm.topology()
+        stats = comm.stats()
+        # production calls after the gate: whatever family survived must give exact sums
+        errs = {}
+        for spec in ("flat+pull", "ring", "ll", "oneshot", None):
+            x = torch.full((100003,), float(rank + 1), device="cuda")
+            y = comm.all_reduce(x, algo=spec)
+            torch.cuda.synchronize()
+            errs[str(spec)] = (y - world * (world + 1) / 2).abs().max().item()
+        desc = comm.describe(1 << 20, torch.float32)
+        comm.check()
+        comm.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, (topo, stats, errs, list(comm.selftest_failed), desc), None))
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("fault", ["", "drop:1:0:0"])
+def test_ipc_connect_readiness_gate(cuda, fault):
+    """Connect-time probe + exact self-test (readiness.hpp). Healthy: every family verified, peers on the
+    same GPU. With rank 1 dropping its slot-0 SIGNAL (every executor schedule then breaks), the self-test
+    disables the fence and write-through families on BOTH ranks and calls run on a verified family
+    (copy engines / LL) with exact results instead of timing out."""
+    import torch.multiprocessing as mp
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_readiness_worker, args=(r, world, port, q, fault)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, out, tb in res:
+        assert tb is None, tb
+        topo, stats, errs, failed, desc = out
+        assert [p["link"] for p in topo["peers"]] == ["self" if r == rank else "same-device" for r in range(world)]
+        assert topo["peers"][rank]["bus"] and topo["links"] == 1
+        assert stats["selftested"] == "fence,wt,ll,dma"
+        assert stats["resident_blocks"] >= 256, stats
+        if fault:
+            assert failed == ["fence", "wt"], failed
+            assert stats["disabled"] == "fence,wt"
+            assert desc.startswith("dma"), desc
+        else:
+            assert failed == [] and stats["disabled"] == ""
+        assert all(e == 0 for e in errs.values()), errs

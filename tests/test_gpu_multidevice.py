@@ -59,6 +59,7 @@ def _worker(rank, world, port, specs, q):
                             worst = max(worst, err)
                         results[(spec, str(dtype), size, op)] = worst
         comm.check()
+        results["readiness"] = (comm.topology(), list(comm.selftest_failed))
         comm.close()
         dist.barrier()
         dist.destroy_process_group()
@@ -94,6 +95,17 @@ def test_allreduce_one_process_per_gpu(cuda):
         p.join(timeout=60)
         assert p.exitcode == 0
     for rank, res in out.items():
+        topo, failed = res.pop("readiness")
+        # connect-time probe: every peer is another GPU reachable peer-to-peer; the self-test verified
+        # every protocol family on the real links
+        assert failed == [], (rank, failed, topo)
+        assert topo["selftested"] == "fence,wt,ll,dma", topo
+        for p in topo["peers"]:
+            if p["rank"] != rank:
+                assert p["link"] in ("xgmi", "pcie"), topo
+                assert p["device"] == p["rank"], topo  # torch.cuda.set_device(rank) in _worker
+        if all(p["link"] == "xgmi" and p["hops"] <= 1 for p in topo["peers"] if p["rank"] != rank):
+            assert topo["links"] == world - 1, topo
         for key, err in res.items():
             tol = 1e-5 if "float32" in key[1] else 2e-2
             assert err < tol, (rank, key, err)
