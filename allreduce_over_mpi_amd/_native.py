@@ -79,6 +79,10 @@ def _sig(lib):
         "flexar_dequantize_fp8": (i, [vp, vp, i, sz, vp, f, vp]),
         "flexar_group_broadcast": (i, [c.POINTER(vp), i, i, c.POINTER(vp), c.POINTER(vp), sz, i, vp, cp]),
         "flexar_simulate_bcast": (i, [cp, i, sz, i, i, c.POINTER(vp), c.POINTER(vp), i, i]),
+        "flexar_simulate_typed": (i, [cp, i, sz, i, i, c.POINTER(vp), c.POINTER(vp), i, i, f, f]),
+        "flexar_allreduce_fp8": (i, [vp, vp, vp, sz, i, i, vp, i, vp, cp]),
+        "flexar_group_allreduce_fp8": (i, [c.POINTER(vp), i, c.POINTER(vp), c.POINTER(vp), sz, i, i, vp, i,
+                                            c.POINTER(vp)]),
         "flexar_comm_selftest": (i, [vp, u32, c.POINTER(u32)]),
         "flexar_comm_set_disabled": (i, [vp, u32]),
         "flexar_comm_disabled": (u32, [vp]),
@@ -298,6 +302,22 @@ def simulate_typed(spec: str, inputs, dtype: str, op="sum", grid=2, ncalls=2, in
     import numpy as np
 
     return _simulate_raw(spec, inputs, DTYPES[dtype], op, grid, ncalls, in_place, scale, np)
+
+
+def simulate_mx(spec: str, inputs, dtype: str, op="sum", grid=2, ncalls=2, scale=1.0, pre=1.0):
+    """Typed-staging programs ("+f32" / "+e4m3" / "+e5m2" suffix) on host arrays. ``inputs`` hold raw bits for
+    16/8-bit dtypes (uint16 / uint8 arrays). ``pre`` is the fp8 pre-scale s (the device derives
+    fp8_max / (N * amax))."""
+    import numpy as np
+
+    n = len(inputs)
+    ins = [np.ascontiguousarray(x) for x in inputs]
+    outs = [np.empty_like(x) for x in ins]
+    rc = lib().flexar_simulate_typed(spec.encode(), n, ins[0].size, DTYPES[dtype], op_code(op),
+                                     _ptr_array([x.ctypes.data for x in ins]), _ptr_array([o.ctypes.data for o in outs]),
+                                     grid, ncalls, float(scale), float(pre))
+    check(rc, "simulate_typed")
+    return outs
 
 
 def reduce_host(srcs, op="sum", scale=1.0, dtype: str | None = None):

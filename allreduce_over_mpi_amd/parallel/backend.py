@@ -413,31 +413,26 @@ def flexar_allreduce_hook(state, bucket):
 def flexar_fp8_compress_hook(state, bucket):
     """DDP comm hook: fp8 (OCP e4m3) compressed gradient allreduce — BASELINE config #5 in a training step.
 
-    1. a fused amax kernel writes 256 per-workgroup partial maxima; one 1 KiB MAX allreduce (flexar LL
-       protocol) of the partials agrees on the bucket's global amax;
-    2. every rank pre-scales its bucket by s = 448 / (N * amax) and casts to fp8 e4m3 (N * |x| * s <= 448,
-       so no partial sum can saturate);
-    3. the fp8 buffer is allreduced with the 1/N post-scale fused into the reduction kernel (fp32
-       accumulate, one rounding), i.e. the kernel produces fp8(mean * s);
-    4. the mean is decompressed as fp8 / s into the bucket.
+    Two launches per bucket (``Communicator.all_reduce_fp8``):
+    1. a fused amax kernel writes 256 per-workgroup partial maxima of the bucket (one HBM pass);
+    2. one executor launch: every rank publishes its amax to the others as a data-tagged granule, all
+       derive s = 448 / (N * global amax) (N * |x| * s <= 448: no partial sum can saturate), the first
+       transfer quantises each contribution to e4m3 with s on its way to the owner, the owner sums in fp32
+       with the 1/N post-scale, rounds once to e4m3 for the all-gather, and every rank writes mean = q / s
+       straight into the bucket in its dtype.
     Moves 1/4 of the fp32 bytes (1/2 of bf16) over xGMI; the error is e4m3's 2^-4 relative step of the
-    largest |gradient| per bucket. Use like ``flexar_allreduce_hook`` with a ``FlexarHookState``."""
-    from ..ops.quant import fp8_amax, fp8_dequantize, fp8_quantize
-
+    largest |gradient| per bucket. Round 1 ran this as 5 launches and 2 allreduces (amax, MAX allreduce,
+    quantize, fp8 allreduce, dequantize). Use like ``flexar_allreduce_hook`` with a ``FlexarHookState``."""
     buf = bucket.buffer()
-    if buf.dtype not in (torch.float32, torch.bfloat16, torch.float16) or buf.data_ptr() % 16:
+    if buf.dtype not in (torch.float32, torch.bfloat16, torch.float16) or buf.data_ptr() % 16 or \
+            state.comm.world_size > 8:
         return flexar_allreduce_hook(state, bucket)
     cur = torch.cuda.current_stream(buf.device)
     side = state.stream(buf.device)
     side.wait_stream(cur)
     with torch.cuda.stream(side):
         buf.record_stream(side)
-        num = 448.0 / state.comm.world_size
-        amax = fp8_amax(buf)                      # one HBM pass -> 256 per-workgroup partials, on device
-        state.comm.all_reduce(amax, op="max")     # 1 KiB: the LL protocol
-        q = fp8_quantize(buf, amax, num)          # one pass: x * s -> e4m3 (s = 448 / (N amax))
-        state.comm.all_reduce(q, op="avg", algo=state.algo)  # fp8 on the wire, 1/N fused
-        fp8_dequantize(q, amax, num, out=buf)     # one pass: q / s -> the bucket
+        state.comm.all_reduce_fp8(buf, op="avg", algo=state.algo if state.algo and "wt" in state.algo else None)
         fut = torch.futures.Future(devices=[buf.device])
         fut.set_result(buf)
     state.calls += 1

@@ -264,6 +264,31 @@ class Communicator:
             nv.check(rc, "allreduce")
         return dst
 
+    def all_reduce_fp8(self, tensor, op="avg", out=None, wire: str = "e4m3", algo: Optional[str] = None, stream=None,
+                       amax_parts=None):
+        """Compressed allreduce of an fp32 / bf16 / fp16 ``tensor`` with OCP fp8 on the links (BASELINE
+        config #5): one amax pass (``fp8_amax``, 256 per-workgroup partials, device-resident), then ONE
+        executor launch that derives the pre-scale s = fp8_max / (N * global amax) from every rank's amax,
+        quantises each contribution with it inside the first transfer, sums in fp32 and writes the result
+        / s in the tensor's dtype inside the last. All ranks get identical results. In place unless ``out``."""
+        from ..ops.quant import fp8_amax
+
+        _require_cuda(tensor)
+        dst = tensor if out is None else out
+        if out is not None:
+            _require_cuda(out, "out")
+            if out.numel() != tensor.numel() or out.dtype != tensor.dtype:
+                raise nv.FlexarError(1, "out must match tensor in size and dtype")
+        if amax_parts is None:
+            amax_parts = fp8_amax(tensor, stream=stream)
+        wd = {"e4m3": nv.DTYPES["fp8_e4m3"], "e5m2": nv.DTYPES["fp8_e5m2"]}[wire]
+        rc = self._lib.flexar_allreduce_fp8(self._h, tensor.data_ptr(), dst.data_ptr(), tensor.numel(),
+                                            _dt(tensor.dtype), _op(op), _stream_handle(stream, self.device), wd,
+                                            amax_parts.data_ptr(), _algo(algo))
+        if rc:
+            nv.check(rc, "allreduce_fp8")
+        return dst
+
     def reduce_scatter(self, input, output, op="sum", algo: Optional[str] = None, stream=None):
         """``output`` (m elements) = this rank's reduced block of ``input`` (world_size * m elements)."""
         _require_cuda(input)
@@ -410,6 +435,22 @@ class LocalGroup:
                                               nv.dtype_code(tensors[0].dtype), nv.op_code(op), _stream_handle(stream),
                                               algo.encode() if algo else None, float(scale))
         nv.check(rc, "group_allreduce")
+        return outs
+
+    def all_reduce_fp8(self, tensors: Sequence, op="avg", outs: Optional[Sequence] = None, wire: str = "e4m3",
+                       stream=None):
+        """fp8-wire allreduce of every rank of the group in one launch (see Communicator.all_reduce_fp8)."""
+        from ..ops.quant import fp8_amax
+
+        outs = list(tensors) if outs is None else list(outs)
+        parts = [fp8_amax(t, stream=stream) for t in tensors]
+        ins = (ctypes.c_void_p * self.nranks)(*[t.data_ptr() for t in tensors])
+        ous = (ctypes.c_void_p * self.nranks)(*[t.data_ptr() for t in outs])
+        amx = (ctypes.c_void_p * self.nranks)(*[p.data_ptr() for p in parts])
+        wd = {"e4m3": nv.DTYPES["fp8_e4m3"], "e5m2": nv.DTYPES["fp8_e5m2"]}[wire]
+        nv.check(self._lib.flexar_group_allreduce_fp8(self._comms, self.nranks, ins, ous, tensors[0].numel(),
+                                                      nv.dtype_code(tensors[0].dtype), nv.op_code(op),
+                                                      _stream_handle(stream), wd, amx), "group_allreduce_fp8")
         return outs
 
     def collective(self, coll: str, ins: Sequence, outs: Sequence, op="sum", algo: Optional[str] = None, stream=None):

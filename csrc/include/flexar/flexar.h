@@ -113,6 +113,13 @@ int flexar_allreduce(flexar_comm_t comm, const void* sendbuf, void* recvbuf, siz
  * post-scale applied to the reduced value (1.0f = none; AVG multiplies 1/N on top). */
 int flexar_allreduce_ex(flexar_comm_t comm, const void* sendbuf, void* recvbuf, size_t count, int dtype,
                         int op, void* hip_stream, const char* algo, float scale);
+/* Compressed allreduce: fp32 / bf16 / fp16 buffers, OCP fp8 (wire_dtype FLEXAR_FP8_E4M3 / _E5M2) on the
+ * links. amax_parts: FLEXAR_AMAX_PARTIALS device floats from flexar_amax(sendbuf) on the same stream; the
+ * pre-scale fp8_max / (N * global amax) and the post-scale are fused into the flat schedule's transfers
+ * (every contribution and every result is rounded to fp8 once; all ranks get identical results).
+ * op: SUM or AVG. algo: NULL = "flat+pull"; "+wt" selects the write-through protocol. */
+int flexar_allreduce_fp8(flexar_comm_t comm, const void* sendbuf, void* recvbuf, size_t count, int dtype, int op,
+                         void* hip_stream, int wire_dtype, const float* amax_parts, const char* algo);
 /* Reduce-scatter: sendbuf holds nranks blocks of `count` elements, recvbuf receives this rank's
  * reduced block (count elements). All-gather: sendbuf has `count` elements, recvbuf nranks*count.
  * algo: "ring" or the direct exchange ("flat", default). Used by FSDP/ZeRO-style sharded DP and by
@@ -160,6 +167,10 @@ int flexar_comm_describe(flexar_comm_t comm, size_t count, int dtype, char* buf,
 int flexar_group_create(int nranks, int device, size_t workspace_bytes, flexar_comm_t* comms_out);
 int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* ins, void* const* outs, size_t count,
                            int dtype, int op, void* hip_stream, const char* algo, float scale);
+/* fp8-wire allreduce for the group (amax_parts: nranks device pointers of FLEXAR_AMAX_PARTIALS floats). */
+int flexar_group_allreduce_fp8(flexar_comm_t* comms, int nranks, const void* const* ins, void* const* outs,
+                               size_t count, int dtype, int op, void* hip_stream, int wire_dtype,
+                               const float* const* amax_parts);
 /* coll: 1 = reduce-scatter, 2 = all-gather, 4 = all-to-all (count = elements per rank block). */
 int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const void* const* ins, void* const* outs,
                             size_t count, int dtype, int op, void* hip_stream, const char* algo);
@@ -228,6 +239,10 @@ int flexar_simulate_coll(int coll, const char* spec, int nranks, size_t count, i
                          const void* const* inputs, void* const* outputs, int grid, int ncalls, float scale);
 int flexar_simulate(const char* spec, int nranks, size_t count, int dtype, int op, const void* const* inputs,
                     void* const* outputs, int grid, int ncalls, int in_place, float scale);
+/* Typed-staging programs (spec suffix "+f32", "+e4m3", "+e5m2"; float dtype, SUM/AVG) with the fp8
+ * pre-scale `pre` given explicitly (the device derives it from the global amax). */
+int flexar_simulate_typed(const char* spec, int nranks, size_t count, int dtype, int op, const void* const* inputs,
+                          void* const* outputs, int grid, int ncalls, float scale, float pre);
 /* Broadcast programs from `root` (inputs: root's source; outputs: every rank's destination). */
 int flexar_simulate_bcast(const char* spec, int nranks, size_t count, int dtype, int root, const void* const* inputs,
                           void* const* outputs, int grid, int ncalls);

@@ -28,6 +28,7 @@ namespace flexar {
 
 struct HostExecCtx {
   uint32_t rank = 0;
+  float pre = 1.0f, post_inv = 1.0f;  // typed programs, fp8 wire: pre-scale s and 1/s
   char* local[BUF_COUNT] = {nullptr, nullptr, nullptr};  // IN, OUT, STG of this rank
   std::vector<char*> peer_stg;                          // per rank (self = local STG)
   std::vector<std::atomic<uint64_t>*> peer_flags;       // per rank flag arrays
@@ -65,6 +66,49 @@ inline void host_reduce_span(T* const* dsts, int ndst, const T* const* srcs, int
   }
 }
 
+// Wire-typed elements (Program::wire): 1 = fp32, 2 = OCP e4m3, 3 = OCP e5m2 (saturating).
+inline float wire_load(int wire, const char* p, uint64_t i) {
+  if (wire == 1) { float f; memcpy(&f, p + 4 * i, 4); return f; }
+  return wire == 2 ? e4m3_to_f32((uint8_t)p[i]) : e5m2_to_f32((uint8_t)p[i]);
+}
+inline void wire_store(int wire, char* p, uint64_t i, float v) {
+  if (wire == 1) { memcpy(p + 4 * i, &v, 4); return; }
+  p[i] = (char)(wire == 2 ? f32_to_e4m3(v) : f32_to_e5m2(v));
+}
+inline float wire_round(int wire, float v) {
+  if (wire == 1) return v;
+  return wire == 2 ? e4m3_to_f32(f32_to_e4m3(v)) : e5m2_to_f32(f32_to_e5m2(v));
+}
+
+// One typed XFER on host memory (the device kernel's xfer_mx semantics, element by element):
+//   source of the wire type: its value; source of the dtype: its value, or in fp8 wire modes the value
+//   quantised with the pre-scale (x * s -> fp8 -> float), so every contribution is rounded the same way;
+//   y = scale * sum; with an fp8 destination y is rounded to fp8 first, so dtype destinations (x 1/s)
+//   and the fp8 copies the peers receive hold the same value.
+template <typename T>
+inline void host_xfer_typed(int wire, const Op& o, char* const* src, char* const* dst, uint64_t n, float pre,
+                            float post_inv) {
+  const uint16_t sm = o.pad16[0], dm = o.pad16[1];
+  for (uint64_t i = 0; i < n; ++i) {
+    float acc = 0.0f;
+    for (int k = 0; k < o.nsrc; ++k) {
+      float v;
+      if (sm & (1u << k)) v = wire_load(wire, src[k], i);
+      else {
+        v = (float)Elem<T>::load(reinterpret_cast<const T*>(src[k])[i]);
+        if (wire >= 2) v = wire_round(wire, v * pre);
+      }
+      acc = k ? acc + v : v;
+    }
+    float y = acc * o.scale;
+    if (wire >= 2 && dm) y = wire_round(wire, y);
+    for (int k = 0; k < o.ndst; ++k) {
+      if (dm & (1u << k)) wire_store(wire, dst[k], i, y);
+      else reinterpret_cast<T*>(dst[k])[i] = Elem<T>::store((typename Elem<T>::acc)(wire >= 2 ? y * post_inv : y));
+    }
+  }
+}
+
 template <typename T, typename OP>
 struct HostExec {
   // Returns 0, or FLEXAR_ERR_TIMEOUT if a WAIT exceeded the timeout.
@@ -72,12 +116,15 @@ struct HostExec {
     const uint32_t nchan = P.nchan;
     const uint32_t ch = gblock % nchan, lb = gblock / nchan;
     const uint32_t nb = (grid - ch + nchan - 1) / nchan;
-    const uint32_t quantum = sizeof(T) >= 16 ? 1 : (uint32_t)(16 / sizeof(T));
+    const uint32_t unit = P.stg_unit();
+    // slice boundaries keep every operand 16-B aligned: 16 bytes of the narrowest operand type
+    const uint32_t quantum = unit >= 16 ? 1 : (uint32_t)(16 / (P.wire ? unit : sizeof(T)));
     const uint64_t par = (epoch & 1) ? c.stg_half_bytes : 0;
     auto addr = [&](const Loc& l) -> char* {
-      if (l.buf == BUF_STG) return c.peer_stg[l.rank] + par + l.off * sizeof(T);
+      if (l.buf == BUF_STG) return c.peer_stg[l.rank] + par + l.off * unit;
       return c.local[l.buf] + l.off * sizeof(T);
     };
+    auto esz = [&](const Loc& l) -> uint64_t { return (l.pad & 1) ? P.wsize : sizeof(T); };
     for (uint32_t i = P.chan_start[ch]; i < P.chan_start[ch + 1]; ++i) {
       const Op& o0 = P.ops[i];
       if (o0.kind == OP_XFER) {
@@ -87,6 +134,14 @@ struct HostExec {
           uint64_t lo, hi;
           slice_range(o.len, lb, nb, quantum, &lo, &hi);
           if (hi <= lo) continue;
+          if (P.wire && (o.pad16[0] || o.pad16[1] || P.wire >= 2)) {
+            char* sp[kMaxSrc];
+            char* dp[kMaxDst];
+            for (int q = 0; q < o.nsrc; ++q) sp[q] = addr(o.src[q]) + lo * esz(o.src[q]);
+            for (int q = 0; q < o.ndst; ++q) dp[q] = addr(o.dst[q]) + lo * esz(o.dst[q]);
+            host_xfer_typed<T>(P.wire, o, sp, dp, hi - lo, c.pre, c.post_inv);
+            continue;
+          }
           const T* srcs[kMaxSrc];
           T* dsts[kMaxDst];
           for (int q = 0; q < o.nsrc; ++q) srcs[q] = (const T*)addr(o.src[q]) + lo;

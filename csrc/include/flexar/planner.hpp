@@ -37,11 +37,25 @@ struct Program {
   std::vector<Op> ops;
   std::vector<uint32_t> chan_start;  // nchan + 1 entries into ops
   uint32_t nchan = 1;
-  uint64_t stg_elems = 0;            // staging elements needed per parity
+  uint64_t stg_elems = 0;            // staging units needed per parity (units of `unit` bytes)
   uint32_t nslots = 0;
   uint64_t count = 0;
   uint32_t esize = 0;
+  // Typed operands (AlgoSpec::wire): 0 = every operand has the call's dtype. Otherwise a STG operand
+  // whose Loc.pad bit 0 is set holds the wire type (wsize bytes: fp32 partials for wire 1, fp8 for
+  // wire 2/3), STG offsets count `unit` = min(esize, wsize) bytes, and every XFER carries its source /
+  // destination wire-type masks in pad16[0] / pad16[1] (bit k = operand k).
+  int wire = 0;
+  uint32_t wsize = 0;
+  uint32_t unit = 0;
   std::string desc;
+  uint32_t stg_unit() const { return unit ? unit : esize; }
+  uint64_t stg_bytes() const { return stg_elems * stg_unit(); }
+  // extent (in offset units) of `len` elements at location l
+  uint64_t extent(const Loc& l, uint64_t len) const {
+    if (!wire || l.buf != BUF_STG) return len;
+    return len * ((l.pad & 1) ? wsize : esize) / unit;
+  }
 };
 
 enum class Coll { ALLREDUCE = 0, REDUCE_SCATTER = 1, ALL_GATHER = 2, BROADCAST = 3, ALL_TO_ALL = 4 };
@@ -61,10 +75,17 @@ class Planner {
     P->esize = esize;
     P->chan_start.push_back(0);
     stg = 0;
+    if (!set_wire(spec, err)) return false;
     if (N == 1) {  // reference: memcpy unless in place (mpi_mod.hpp:1181-1188)
       if (count) xfer(count, {loc(BUF_IN, r, 0)}, {loc(BUF_OUT, r, 0)}, scale);
       finish_channel();
       P->desc = "copy";
+    } else if (wire >= 2 && !(spec.kind == AlgoKind::TREE && spec.widths.size() == 1 && spec.widths[0] == (int)N)) {
+      if (err) *err = "fp8 wire compression needs the flat schedule (one quantisation per contribution)";
+      return false;
+    } else if (wire >= 2 && N > kMaxSrc) {
+      if (err) *err = "fp8 wire compression supports up to 8 ranks (one reduction of every contribution)";
+      return false;
     } else if (spec.kind == AlgoKind::RING) {
       int C = std::max(1, std::min(spec.channels, max_ring_channels(N)));
       if (2ull * (N - 1) * C > kProgSlots) { if (err) *err = "too many ring channels"; return false; }
@@ -82,7 +103,9 @@ class Planner {
       if (2 * spec.widths.size() + 2 > kProgSlots) { if (err) *err = "too many stages"; return false; }
       for (int w : spec.widths)
         if (w < 2) { if (err) *err = "tree width < 2"; return false; }
-      build_tree_lonely(spec.widths, (uint32_t)prod, spec.ag == AgMode::PULL, spec.fuse);
+      // typed staging: fp32 partials need the fused forms (no partial sum passes through OUT); fp8 wire
+      // pulls (one quantised copy of each result instead of a re-quantised multicast)
+      build_tree_lonely(spec.widths, (uint32_t)prod, spec.ag == AgMode::PULL || wire >= 2, spec.fuse || wire == 1);
       if (r >= (uint32_t)prod) {
         // A lonely rank allocates only its fold slots, the tree ranks much more. Every rank sizes its
         // pieces (and the MPI engine its shared window) from its own stg_elems, so all ranks must report
@@ -93,6 +116,9 @@ class Planner {
         stg = std::max(stg, Q.stg_elems);
       }
       P->desc = spec.str();
+    } else if (wire && spec.kind != AlgoKind::TREE) {
+      if (err) *err = "typed staging (" + spec.str() + ") applies to ring / tree / flat schedules only";
+      return false;
     } else if (spec.kind == AlgoKind::ONESHOT) {
       build_oneshot();
       P->desc = spec.str();
@@ -112,6 +138,7 @@ class Planner {
     }
     P->stg_elems = stg;
     P->nchan = (uint32_t)P->chan_start.size() - 1;
+    finish_types(*P);
     mark_runs(*P, r);
     return true;
   }
@@ -184,7 +211,7 @@ class Planner {
     };
     // any rank: a run may not read what another op of the run writes, locally or in a peer's staging
     auto ovl = [&](const Loc& a, uint64_t la, const Loc& b, uint64_t lb) {
-      return a.rank == b.rank && a.buf == b.buf && a.off < b.off + lb && b.off < a.off + la;
+      return a.rank == b.rank && a.buf == b.buf && a.off < b.off + P.extent(b, lb) && b.off < a.off + P.extent(a, la);
     };
     auto indep = [&](const Op& a, const Op& b) {
       for (int i = 0; i < a.ndst; ++i) {
@@ -219,6 +246,25 @@ class Planner {
   uint64_t align;
   uint64_t stg = 0;
   Program* prog = nullptr;
+  int wire = 0;        // AlgoSpec::wire of the program being built
+  uint32_t wsize = 0;  // bytes of a wire-typed element
+  uint32_t unit = 0;   // bytes per staging offset unit
+
+  // Typed staging setup (see Program::wire). Offsets of STG operands count `unit` bytes, IN/OUT
+  // operands stay in elements of the call's dtype.
+  bool set_wire(const AlgoSpec& spec, std::string* err) {
+    wire = spec.wire;
+    if (wire < 0 || wire > 3) { if (err) *err = "bad wire type"; return false; }
+    if (wire == 1 && esize >= 4) wire = 0;  // fp32 (or wider) partials already: nothing to widen
+    wsize = wire == 1 ? 4u : (wire >= 2 ? 1u : esize);
+    if (wire >= 2 && esize < 2) { if (err) *err = "fp8 wire compression needs a 16/32-bit float input"; return false; }
+    unit = wire ? std::min(esize, wsize) : esize;
+    align = std::max<uint64_t>(1, kStageAlignBytes / unit);
+    prog->wire = wire;
+    prog->wsize = wire ? wsize : 0;
+    prog->unit = wire ? unit : 0;
+    return true;
+  }
 
   static Loc loc(uint16_t buf, uint32_t rank, uint64_t off) {
     Loc l;
@@ -228,11 +274,51 @@ class Planner {
     l.off = off;
     return l;
   }
+  // a staging location holding the wire type (fp32 partial sums in wire mode 1)
+  static Loc wloc(uint32_t rank, uint64_t off) {
+    Loc l = loc(BUF_STG, rank, off);
+    l.pad = 1;
+    return l;
+  }
   uint64_t round_up(uint64_t x) const { return (x + align - 1) / align * align; }
+  // staging for `elems` elements of the program's default staging type (in units): the call's dtype,
+  // or fp8 in wire modes 2/3 where every staging operand carries the wire type
   uint64_t alloc(uint64_t elems) {
     uint64_t o = stg;
-    stg += round_up(elems);
+    stg += round_up(wire == 1 ? elems * esize / unit : elems);
     return o;
+  }
+  uint64_t talloc(uint64_t elems) {  // staging for `elems` elements of the call's dtype, any mode
+    uint64_t o = stg;
+    stg += round_up(wire ? elems * esize / unit : elems);
+    return o;
+  }
+  uint64_t walloc(uint64_t elems) {  // staging for `elems` wire-typed elements (in units)
+    uint64_t o = stg;
+    stg += round_up(wire ? elems * wsize / unit : elems);
+    return o;
+  }
+  // element span -> offset units, for a typed slot
+  uint64_t wunits(uint64_t elems) const { return wire ? elems * wsize / unit : elems; }
+  uint64_t tunits(uint64_t elems) const { return wire ? elems * esize / unit : elems; }
+
+  // Final typing pass: fp8 wire = every staging operand carries the wire type; per-XFER masks.
+  void finish_types(Program& P) const {
+    if (!wire) return;
+    for (Op& o : P.ops) {
+      if (o.kind != OP_XFER) continue;
+      uint16_t sm = 0, dm = 0;
+      for (int k = 0; k < o.nsrc; ++k) {
+        if (wire >= 2 && o.src[k].buf == BUF_STG && !(o.src[k].pad & 2)) o.src[k].pad = 1;
+        if (o.src[k].pad & 1) sm |= (uint16_t)(1u << k);
+      }
+      for (int k = 0; k < o.ndst; ++k) {
+        if (wire >= 2 && o.dst[k].buf == BUF_STG && !(o.dst[k].pad & 2)) o.dst[k].pad = 1;
+        if (o.dst[k].pad & 1) dm |= (uint16_t)(1u << k);
+      }
+      o.pad16[0] = sm;
+      o.pad16[1] = dm;
+    }
   }
   void finish_channel() { prog->chan_start.push_back((uint32_t)prog->ops.size()); }
 
@@ -265,7 +351,10 @@ class Planner {
   void xfer(uint64_t len, std::vector<Loc> srcs, std::vector<Loc> dsts, float sc) {
     if (len == 0 || srcs.empty() || dsts.empty()) return;
     if (srcs.size() > kMaxSrc) {
-      Loc tmp = loc(BUF_STG, r, alloc(len));
+      // partial-sum temp: fp32 in wire mode 1, the call's dtype otherwise (never fp8: pad bit 1 keeps
+      // finish_types from retyping it)
+      Loc tmp = wire == 1 ? wloc(r, walloc(len)) : loc(BUF_STG, r, talloc(len));
+      if (wire >= 2) tmp.pad = 2;
       std::vector<Loc> first(srcs.begin(), srcs.begin() + kMaxSrc);
       emit_xfer(len, first, {tmp}, 1.0f);
       size_t i = kMaxSrc;
@@ -332,22 +421,29 @@ class Planner {
         uint64_t s = (uint64_t)k * split;
         return s >= c_cnt ? 0 : std::min(split, c_cnt - s);
       };
-      // Every rank computes the same staging layout (same sequence of allocs).
-      uint64_t base = alloc(2ull * (N - 1) * split);
-      auto rs_off = [&](uint32_t i) { return base + (uint64_t)i * split; };
-      auto ag_off = [&](uint32_t i) { return base + (uint64_t)(N - 1 + i) * split; };
+      // Every rank computes the same staging layout (same sequence of allocs). Wire mode 1: the RS slots
+      // that receive partial sums (i >= 1) hold fp32; slot 0 (a raw input) and the AG slots the dtype.
+      const bool acc = wire == 1;
+      uint64_t base = alloc((uint64_t)N * split);            // rs slot 0 + N - 1 AG slots
+      uint64_t wbase = acc ? walloc((uint64_t)(N - 2) * split) : 0;  // rs slots 1 .. N - 2
+      if (!acc) base = (alloc((uint64_t)(N - 2) * split), base);     // same extent as before: 2 (N - 1) slots
+      auto rs_loc = [&](uint32_t rank, uint32_t i) {
+        if (acc && i >= 1) return wloc(rank, wbase + (uint64_t)(i - 1) * wunits(split));
+        return loc(BUF_STG, rank, i == 0 ? base : base + (uint64_t)(N + i - 1) * split);
+      };
+      auto ag_off = [&](uint32_t i) { return base + (uint64_t)(1 + i) * split; };
       uint32_t slot0 = c * slots_per;
       auto mod = [&](long x) { return (uint32_t)(((x % (long)N) + N) % N); };
 
       uint32_t b0 = v;
-      xfer(blen(b0), {loc(BUF_IN, r, boff(b0))}, {loc(BUF_STG, right, rs_off(0))}, 1.0f);
+      xfer(blen(b0), {loc(BUF_IN, r, boff(b0))}, {rs_loc(right, 0)}, 1.0f);
       signal({right}, slot0 + 0);
       for (uint32_t i = 0; i + 1 < N; ++i) {
         wait({left}, slot0 + i);
         uint32_t b = mod((long)v - 1 - (long)i);
-        std::vector<Loc> srcs{loc(BUF_IN, r, boff(b)), loc(BUF_STG, r, rs_off(i))};
+        std::vector<Loc> srcs{loc(BUF_IN, r, boff(b)), rs_loc(r, i)};
         if (i + 2 < N) {
-          xfer(blen(b), srcs, {loc(BUF_STG, right, rs_off(i + 1))}, 1.0f);
+          xfer(blen(b), srcs, {rs_loc(right, i + 1)}, 1.0f);
         } else {  // owned block (v + 1): final value -> OUT and start the all-gather
           xfer(blen(b), srcs, {loc(BUF_OUT, r, boff(b)), loc(BUF_STG, right, ag_off(0))}, scale);
         }
@@ -452,15 +548,29 @@ class Planner {
       for (uint32_t k = p % st[s].G; k < N; k += st[s].G) b.push_back(k);
       return b;
     };
-    // Staging layout (identical on every rank): rs[s], ag[s] (push) or pub (pull).
+    // Staging layout (identical on every rank): rs[s], ag[s] (push) or pub (pull). Wire mode 1: the RS
+    // slots of stages s >= 1 receive partial sums and hold fp32 (slot stride in units scales with it);
+    // a rank's own partial for stage s + 1 goes to its own (otherwise unused) slot of that stage.
+    const bool acc = wire == 1;
+    auto slot_units = [&](uint32_t s) { return acc && s > 0 ? wunits(split) : split; };
     std::vector<uint64_t> rs_base(S), ag_base(S);
-    for (uint32_t s = 0; s < S; ++s) rs_base[s] = alloc((uint64_t)st[s].w * (N / st[s].G) * split);
+    for (uint32_t s = 0; s < S; ++s)
+      rs_base[s] = acc && s > 0 ? walloc((uint64_t)st[s].w * (N / st[s].G) * split)
+                                : alloc((uint64_t)st[s].w * (N / st[s].G) * split);
     uint64_t pub_base = 0;
     if (pull) pub_base = alloc((uint64_t)N * split);
     else
       for (uint32_t s = 0; s < S; ++s) ag_base[s] = alloc((uint64_t)st[s].w * (N / st[s].G) * split);
     auto rs_off = [&](uint32_t s, uint32_t j, uint32_t k) {
-      return rs_base[s] + ((uint64_t)j * (N / st[s].G) + k / st[s].G) * split;
+      return rs_base[s] + ((uint64_t)j * (N / st[s].G) + k / st[s].G) * slot_units(s);
+    };
+    auto rs_loc = [&](uint32_t s, uint32_t rank, uint32_t j, uint32_t k) {
+      return acc && s > 0 ? wloc(rank, rs_off(s, j, k)) : loc(BUF_STG, rank, rs_off(s, j, k));
+    };
+    // this rank's running value of block k entering stage s
+    auto own_at = [&](uint32_t s, uint32_t k, uint16_t first_buf) {
+      if (s == 0) return loc(first_buf, r, boff(k));
+      return acc ? rs_loc(s, r, st[s].myj, k) : loc(BUF_OUT, r, boff(k));
     };
     auto ag_off = [&](uint32_t s, uint32_t j, uint32_t k) {
       return ag_base[s] + ((uint64_t)j * (N / st[s].G) + k / st[s].G) * split;
@@ -472,26 +582,25 @@ class Planner {
     // ---------------- reduce-scatter
     for (uint32_t s = 0; s < S; ++s) {
       const Stage& x = st[s];
-      uint16_t cur = (s == 0) ? first : BUF_OUT;
       bool sends_fused = fuse && s > 0;  // previous stage already wrote our sends into the receivers
       if (!sends_fused) {
         for (uint32_t p : x.others())
-          for (uint32_t k : blocks_of(p, s))
-            xfer(blen(k), {loc(cur, r, boff(k))}, {loc(BUF_STG, p, rs_off(s, x.myj, k))}, 1.0f);
+          for (uint32_t k : blocks_of(p, s)) xfer(blen(k), {own_at(s, k, first)}, {rs_loc(s, p, x.myj, k)}, 1.0f);
       }
       signal(x.others(), s);
       wait(x.others(), s);
       bool last = (s + 1 == S);
       for (uint32_t k : blocks_of(r, s)) {
-        std::vector<Loc> srcs{loc(cur, r, boff(k))};
+        std::vector<Loc> srcs{own_at(s, k, first)};
         for (uint32_t jj = 1; jj < x.w; ++jj) {
           uint32_t j = (x.myj + jj) % x.w;
-          srcs.push_back(loc(BUF_STG, r, rs_off(s, j, k)));
+          srcs.push_back(rs_loc(s, r, j, k));
         }
         std::vector<Loc> dsts;
         if (!last) {
           uint32_t p = owner_at(k, s + 1);
-          if (fuse && p != r) dsts.push_back(loc(BUF_STG, p, rs_off(s + 1, st[s + 1].myj, k)));
+          if (fuse && p != r) dsts.push_back(rs_loc(s + 1, p, st[s + 1].myj, k));
+          else if (acc) dsts.push_back(rs_loc(s + 1, r, st[s + 1].myj, k));
           else dsts.push_back(loc(BUF_OUT, r, boff(k)));
           xfer(blen(k), srcs, dsts, 1.0f);
         } else {
@@ -746,7 +855,8 @@ inline bool validate_program(const Program& P, uint32_t N, uint32_t rank, uint64
     if (P.chan_start[c] > P.chan_start[c + 1]) return fail("channel table not monotonic");
   auto loc_ok = [&](const Loc& l, uint64_t len) {
     if (l.rank >= N || l.buf >= BUF_COUNT) return false;
-    if (l.buf == BUF_STG) return l.off + len <= P.stg_elems;
+    if (l.pad > 2 || (l.pad && (!P.wire || l.buf != BUF_STG))) return false;
+    if (l.buf == BUF_STG) return l.off + P.extent(l, len) <= P.stg_elems;
     if (l.rank != rank) return false;  // a caller buffer is never addressed on a peer
     return l.off + len <= (l.buf == BUF_IN ? in_elems : out_elems);
   };
@@ -777,18 +887,23 @@ inline std::string dump_program(const Program& P, uint32_t rank) {
   static const char* bn[] = {"IN", "OUT", "STG"};
   std::ostringstream ss;
   ss << "rank " << rank << " program '" << P.desc << "': " << P.ops.size() << " ops, " << P.nchan
-     << " channel(s), staging " << P.stg_elems << " elems/parity, " << P.nslots << " flag slots\n";
+     << " channel(s), staging " << P.stg_elems << " elems/parity, " << P.nslots << " flag slots";
+  if (P.wire) ss << ", wire type " << (P.wire == 1 ? "fp32" : P.wire == 2 ? "e4m3" : "e5m2") << " ('~'), unit " << P.unit << " B";
+  ss << "\n";
   for (uint32_t c = 0; c < P.nchan; ++c) {
     ss << "channel " << c << ":\n";
     for (uint32_t i = P.chan_start[c]; i < P.chan_start[c + 1]; ++i) {
       const Op& o = P.ops[i];
       if (o.kind == OP_XFER) {
         ss << "  XFER len=" << o.len << (o.scale != 1.0f ? " scale" : "") << " [";
+        // a wire-typed staging operand is marked with '~'
         for (int k = 0; k < o.nsrc; ++k)
-          ss << (k ? " + " : "") << bn[o.src[k].buf] << "@" << o.src[k].rank << ":" << o.src[k].off;
+          ss << (k ? " + " : "") << bn[o.src[k].buf] << ((o.src[k].pad & 1) ? "~" : "") << "@" << o.src[k].rank << ":"
+             << o.src[k].off;
         ss << "] -> [";
         for (int k = 0; k < o.ndst; ++k)
-          ss << (k ? ", " : "") << bn[o.dst[k].buf] << "@" << o.dst[k].rank << ":" << o.dst[k].off;
+          ss << (k ? ", " : "") << bn[o.dst[k].buf] << ((o.dst[k].pad & 1) ? "~" : "") << "@" << o.dst[k].rank << ":"
+             << o.dst[k].off;
         ss << "]\n";
       } else {
         ss << (o.kind == OP_SIGNAL ? "  SIGNAL" : "  WAIT  ") << " slot=" << o.slot << " peers=";

@@ -37,6 +37,13 @@ struct AlgoSpec {
   bool fuse = true;         // fuse reduce->forward (tree RS / AG multicast)
   bool nts = false;         // executor stores with the streaming (nontemporal) policy
   bool wt = false;          // write-through protocol: sc0 sc1 payload, fence-free SIGNAL/WAIT
+  // Typed staging (planner.hpp "typed operands"): WIRE_ACC keeps the partial sums of multi-hop schedules
+  // (ring, multi-stage trees) in fp32 staging so a 16/8-bit allreduce rounds once, like flat; WIRE_E4M3 /
+  // WIRE_E5M2 carry a wider dtype over the links as fp8 with a per-call pre-scale from the global amax
+  // (flat schedule only: one quantisation per contribution, one per result). round_wire ("+rw") opts a
+  // multi-hop 16/8-bit schedule out of the fp32 staging default.
+  int wire = 0;
+  bool round_wire = false;
 
   std::string str() const {
     std::ostringstream ss;
@@ -56,6 +63,10 @@ struct AlgoSpec {
     if (!fuse) ss << "+nofuse";
     if (nts) ss << "+nts";
     if (wt) ss << "+wt";
+    if (wire == 1) ss << "+f32";
+    if (wire == 2) ss << "+e4m3";
+    if (wire == 3) ss << "+e5m2";
+    if (round_wire) ss << "+rw";
     return ss.str();
   }
 };
@@ -179,6 +190,10 @@ inline bool parse_algo(const std::string& raw, int nranks, AlgoSpec* spec, std::
     else if (mod == "fuse") spec->fuse = true;
     else if (mod == "nts") spec->nts = true;
     else if (mod == "wt") spec->wt = true;
+    else if (mod == "f32") spec->wire = 1;
+    else if (mod == "e4m3" || mod == "fp8") spec->wire = 2;
+    else if (mod == "e5m2") spec->wire = 3;
+    else if (mod == "rw") spec->round_wire = true;
     else { if (err) *err = "unknown algorithm modifier '+" + mod + "'"; return false; }
   }
   std::string head = s, arg;
@@ -223,9 +238,10 @@ inline bool parse_algo(const std::string& raw, int nranks, AlgoSpec* spec, std::
   }
   if (head == "ft") {
     const char* env = getenv("FT_TOPO");
-    AgMode ag = spec->ag; bool fuse = spec->fuse, nts = spec->nts, wt = spec->wt;
+    AgMode ag = spec->ag; bool fuse = spec->fuse, nts = spec->nts, wt = spec->wt, rw = spec->round_wire;
+    int wire = spec->wire;
     if (!parse_ft_topo(!arg.empty() ? arg.c_str() : env, nranks, spec, err)) return false;
-    spec->ag = ag; spec->fuse = fuse; spec->nts = nts; spec->wt = wt;
+    spec->ag = ag; spec->fuse = fuse; spec->nts = nts; spec->wt = wt; spec->wire = wire; spec->round_wire = rw;
     return true;
   }
   if (err) *err = "unknown algorithm '" + raw + "'";

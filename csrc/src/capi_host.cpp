@@ -50,15 +50,15 @@ struct RankBarrier {
 struct SimRun {
   template <typename T, typename OP>
   static int run(const std::vector<Program>& progs, int nranks, int grid, int ncalls, int in_place,
-                 const void* const* inputs, void* const* outputs, size_t count) {
+                 const void* const* inputs, void* const* outputs, size_t count, float pre = 1.0f) {
     const size_t es = sizeof(T);
-    uint64_t stg_elems = 0;
+    uint64_t stg_bytes = 0;
     uint32_t nslots = 1;
     for (auto& p : progs) {
-      stg_elems = std::max<uint64_t>(stg_elems, p.stg_elems);
+      stg_bytes = std::max<uint64_t>(stg_bytes, p.stg_bytes());
       nslots = std::max<uint32_t>(nslots, p.nslots);
     }
-    uint64_t half = (stg_elems * es + 255) / 256 * 256;
+    uint64_t half = (stg_bytes + 255) / 256 * 256;
     std::vector<std::vector<char>> stg(nranks, std::vector<char>(2 * half + 256, (char)0xA5));  // poison
     size_t nflags = (size_t)nslots * nranks * grid;
     std::vector<std::unique_ptr<std::atomic<uint64_t>[]>> flags(nranks);
@@ -81,6 +81,8 @@ struct SimRun {
       c.blocks_stride = grid;
       c.stg_half_bytes = half;
       c.timeout_s = 30.0;
+      c.pre = pre;
+      c.post_inv = 1.0f / pre;
     }
     std::vector<RankBarrier> bars(nranks);
     for (auto& b : bars) b.n = grid;
@@ -210,6 +212,33 @@ int flexar_simulate(const char* spec, int nranks, size_t count, int dtype, int o
   }
   if (grid % progs[0].nchan) { set_error("grid must be a multiple of the channel count"); return FLEXAR_ERR_INVALID; }
   return dispatch_dtype_op<SimRun>(dtype, op, progs, nranks, grid, ncalls, in_place, inputs, outputs, count);
+}
+
+// Typed programs ("+f32" fp32 partials, "+e4m3"/"+e5m2" fp8 wire) with an explicit fp8 pre-scale
+// (the device derives it from the global amax: s = fp8_max / (N * amax)).
+int flexar_simulate_typed(const char* spec, int nranks, size_t count, int dtype, int op, const void* const* inputs,
+                          void* const* outputs, int grid, int ncalls, float scale, float pre) {
+  size_t es = dtype_size(dtype);
+  if (!es || nranks < 1 || nranks > 64 || grid < 1 || grid > 64 || ncalls < 1 || !inputs || !outputs || !(pre > 0)) {
+    set_error("bad simulate arguments");
+    return FLEXAR_ERR_INVALID;
+  }
+  if (!dtype_is_float(dtype) || (op != FLEXAR_SUM && op != FLEXAR_AVG)) {
+    set_error("typed staging needs a float dtype with SUM/AVG");
+    return FLEXAR_ERR_UNSUPPORTED;
+  }
+  AlgoSpec s;
+  std::string err;
+  if (!spec_for(spec, nranks, (double)count * es, &s, &err, true)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  float fs = scale * (op == FLEXAR_AVG ? 1.0f / (float)nranks : 1.0f);
+  std::vector<Program> progs(nranks);
+  for (int r = 0; r < nranks; ++r) {
+    Planner pl(nranks, r, count, (uint32_t)es, fs);
+    if (!pl.build(s, &progs[r], &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+    if (!validate_program(progs[r], nranks, r, count, count, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  }
+  if (grid % progs[0].nchan) { set_error("grid must be a multiple of the channel count"); return FLEXAR_ERR_INVALID; }
+  return dispatch_dtype_op<SimRun>(dtype, op, progs, nranks, grid, ncalls, 0, inputs, outputs, count, pre);
 }
 
 int flexar_simulate_coll(int coll, const char* spec, int nranks, size_t count, int dtype, int op,

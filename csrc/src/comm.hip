@@ -236,6 +236,27 @@ static int resolve_spec(flexar_comm* c, const char* algo, double bytes, AlgoSpec
 
 // An executor schedule chosen after resolve_spec (RS/AG/broadcast force their own shape, a captured
 // communicator replaces dma): move it onto a verified protocol family, never onto dma.
+// Typed staging for an allreduce schedule (AlgoSpec::wire). Multi-hop schedules of 16/8-bit float
+// dtypes keep their partial sums in fp32 staging by default (one rounding, like flat) unless the spec
+// says "+rw"; fp8 wire modes need flexar_allreduce_fp8 (the amax partials). Other ops / schedules
+// run untyped.
+static int typed_spec(AlgoSpec* s, int dtype, int op, bool have_amax) {
+  const bool sumavg = op == FLEXAR_SUM || op == FLEXAR_AVG;
+  const bool narrow = dtype == FLEXAR_BFLOAT16 || dtype == FLEXAR_FLOAT16 || dtype == FLEXAR_FP8_E4M3 ||
+                      dtype == FLEXAR_FP8_E5M2;
+  const bool multihop = s->kind == AlgoKind::RING || (s->kind == AlgoKind::TREE && s->widths.size() > 1);
+  if (s->wire >= 2) {
+    if (!have_amax) {
+      set_error("fp8 wire compression (" + s->str() + ") needs the amax partials: use flexar_allreduce_fp8");
+      return FLEXAR_ERR_INVALID;
+    }
+    return 0;
+  }
+  if (s->wire == 1 && !(narrow && sumavg && multihop)) s->wire = 0;  // nothing to widen
+  if (s->wire == 0 && !s->round_wire && narrow && sumavg && multihop) s->wire = 1;
+  return 0;
+}
+
 static int executor_proto(flexar_comm* c, AlgoSpec* s) {
   if (!c->disabled) return 0;
   std::string why;
@@ -260,7 +281,7 @@ static void mark_barriers(Program& P, uint32_t rank) {
   (void)rank;
   auto overlap = [&](const Loc& a, uint64_t la, const Loc& b, uint64_t lb) {
     if (a.rank != b.rank || a.buf != b.buf) return false;
-    return a.off < b.off + lb && b.off < a.off + la;
+    return a.off < b.off + P.extent(b, lb) && b.off < a.off + P.extent(a, la);
   };
   for (uint32_t ch = 0; ch < P.nchan; ++ch) {
     for (uint32_t i = P.chan_start[ch]; i < P.chan_start[ch + 1]; ++i) {
@@ -304,7 +325,7 @@ static int get_program(flexar_comm* c, const AlgoSpec& s, uint64_t count, uint32
   mark_barriers(dp->prog, c->rank);
   logf(LOG_INFO, c->rank, "plan %s: count=%llu esize=%u ops=%zu channels=%u staging=%llu B", s.str().c_str(),
        (unsigned long long)count, esize, dp->prog.ops.size(), dp->prog.nchan,
-       (unsigned long long)(dp->prog.stg_elems * esize));
+       (unsigned long long)dp->prog.stg_bytes());
   if (log_level() >= LOG_DEBUG) logf(LOG_DEBUG, c->rank, "%s", dump_program(dp->prog, c->rank).c_str());
   size_t ob = dp->prog.ops.size() * sizeof(Op), cb = dp->prog.chan_start.size() * sizeof(uint32_t);
   FX_HIP(hipMalloc(&dp->d_ops, ob ? ob : sizeof(Op)));
@@ -338,7 +359,9 @@ static void fill_ctx(flexar_comm* c, DevProgram* dp, const void* in, void* out, 
     x->chan_start = dp->d_chan;
     x->nchan = dp->prog.nchan;
   }
-  x->ll_off = c->exec_half;
+  x->ll_off = c->exec_half + kAmaxRegion;
+  x->amax_off = c->exec_half;
+  x->stg_unit = dp ? dp->prog.stg_unit() : 0;
   x->nranks = c->nranks;
   x->rank = c->rank;
   x->local[BUF_IN] = (char*)in;
@@ -364,7 +387,7 @@ static int plan_pieces(flexar_comm* c, const AlgoSpec& s, uint64_t count, uint32
   DevProgram* dp = nullptr;
   int rc = get_program(c, s, count, esize, fs, &dp, coll, stride);
   if (rc) return rc;
-  uint64_t need = dp->prog.stg_elems * esize;
+  uint64_t need = dp->prog.stg_bytes();
   const uint64_t bytes = count * esize;
   const bool chunked = c->chunk_bytes && bytes > c->chunk_bytes;
   if (need <= c->exec_half && !chunked) { *piece = count; return 0; }
@@ -377,7 +400,7 @@ static int plan_pieces(flexar_comm* c, const AlgoSpec& s, uint64_t count, uint32
     if (p == 0) p = align;
     rc = get_program(c, s, p, esize, fs, &dp, coll, stride);
     if (rc) return rc;
-    if (dp->prog.stg_elems * esize <= c->exec_half) { *piece = p; return 0; }
+    if (dp->prog.stg_bytes() <= c->exec_half) { *piece = p; return 0; }
   }
   set_error("workspace too small for this algorithm");
   return FLEXAR_ERR_NOMEM;
@@ -714,7 +737,8 @@ static int alloc_workspace(flexar_comm* c, size_t ws) {
   FX_HIP(hipMemset(c->stg, 0, c->ws_bytes));  // LL granules: zero = epoch 0, never matches a live call
   c->ll_bytes = (size_t)(2 * kLLMaxBytes) * c->nranks;
   if (c->ll_bytes * 2 > c->half_bytes) c->ll_bytes = 0;
-  c->exec_half = c->half_bytes - c->ll_bytes;
+  // each parity half: [op-program staging | amax granules (fp8 wire) | LL granules]
+  c->exec_half = c->half_bytes - c->ll_bytes - kAmaxRegion;
   FX_HIP(hipExtMallocWithFlags((void**)&c->flags, kFlagWords * sizeof(uint64_t), hipDeviceMallocUncached));
   FX_HIP(hipMemset(c->flags, 0, kFlagWords * sizeof(uint64_t)));
   FX_HIP(hipMalloc(&c->epochs, kMaxGridBlocks * sizeof(uint64_t)));
@@ -1126,6 +1150,7 @@ int flexar_comm_describe(flexar_comm_t c, size_t count, int dtype, char* buf, si
   AlgoSpec s;
   int rc = resolve_spec(c, nullptr, (double)count * es, &s);
   if (rc) return rc;
+  if ((rc = typed_spec(&s, dtype, FLEXAR_SUM, false))) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
   uint64_t piece = count;
   if (c->nranks > 1 && count) {
@@ -1139,7 +1164,7 @@ int flexar_comm_describe(flexar_comm_t c, size_t count, int dtype, char* buf, si
   snprintf(buf, buflen, "%s grid=%d pieces=%llu stg_bytes=%llu ops=%zu",
            c->nranks == 1 ? "copy (1 rank)" : s.str().c_str(), grid,
            (unsigned long long)(piece ? (count + piece - 1) / piece : 0),
-           (unsigned long long)(dp->prog.stg_elems * es), dp->prog.ops.size());
+           (unsigned long long)dp->prog.stg_bytes(), dp->prog.ops.size());
   return 0;
 }
 
@@ -1167,6 +1192,7 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     s = m.s;
   } else {
     if ((rc = resolve_spec(c, algo, (double)count * es, &s))) return rc;
+    if ((rc = typed_spec(&s, dtype, op, false))) return rc;
     if (s.kind == AlgoKind::LL && !ll_usable(c, count, es)) s.kind = AlgoKind::ONESHOT;
     if (s.kind == AlgoKind::DMA && c->nranks == 1) s.kind = AlgoKind::ONESHOT;  // one rank: the executor's copy
     if ((rc = executor_proto(c, &s))) return rc;  // the LL -> oneshot rewrite above may land on a failed family
@@ -1236,6 +1262,7 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     la.grid = hit ? m.grid : choose_grid(c, count * es, dp->prog.nchan);
     la.stream = st;
     la.proto = proto_of(s);
+    la.wire = dp->prog.wire;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     if (c->profile) {
       FX_HIP(hipEventCreate(&ev0));
@@ -1278,6 +1305,7 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     la.grid = grid;
     la.stream = st;
     la.proto = proto_of(s);
+    la.wire = dp->prog.wire;
     rc = launch_dtype(dtype, op, la);
     if (rc) break;
     c->launches++;
@@ -1326,6 +1354,65 @@ int flexar_comm_stats(flexar_comm_t c, char* buf, size_t buflen) {
 
 int flexar_allreduce(flexar_comm_t c, const void* in, void* out, size_t count, int dtype, int op, void* stream) {
   return flexar_allreduce_ex(c, in, out, count, dtype, op, stream, nullptr, 1.0f);
+}
+
+// Compressed allreduce (BASELINE config #5): fp32 / bf16 / fp16 in and out, OCP fp8 on the links. The
+// pre-scale s = fp8_max / (N * global amax) is derived inside the executor from every rank's amax
+// partials (flexar_amax, one HBM pass) and fused into the first transfer; the post-scale 1/s (and AVG's
+// 1/N) into the last: two launches per bucket (amax + this), no separate quantize / dequantize pass.
+int flexar_allreduce_fp8(flexar_comm_t c, const void* in, void* out, size_t count, int dtype, int op, void* stream,
+                         int wire_dtype, const float* amax_parts, const char* algo) {
+  int rc = validate_call(c, dtype, op, 1.0f);
+  if (rc) return rc;
+  if (count == 0) return 0;
+  if (!out || !amax_parts) { set_error("null recvbuf / amax partials"); return FLEXAR_ERR_INVALID; }
+  if (dtype != FLEXAR_FLOAT32 && dtype != FLEXAR_BFLOAT16 && dtype != FLEXAR_FLOAT16) {
+    set_error("fp8 wire compression takes fp32 / bf16 / fp16 buffers");
+    return FLEXAR_ERR_UNSUPPORTED;
+  }
+  if ((op != FLEXAR_SUM && op != FLEXAR_AVG) || (wire_dtype != FLEXAR_FP8_E4M3 && wire_dtype != FLEXAR_FP8_E5M2)) {
+    set_error("fp8 wire compression: SUM/AVG over e4m3 or e5m2");
+    return FLEXAR_ERR_UNSUPPORTED;
+  }
+  if ((rc = check_err(c))) return rc;
+  if (!in) in = out;
+  if (c->nranks == 1) return flexar_allreduce_ex(c, in, out, count, dtype, op, stream, nullptr, 1.0f);
+  hipStream_t st = (hipStream_t)stream;
+  const uint32_t es = (uint32_t)dtype_size(dtype);
+  const float fs = op == FLEXAR_AVG ? 1.0f / (float)c->nranks : 1.0f;
+  AlgoSpec s;
+  std::string err;
+  if (!parse_algo(algo && *algo ? algo : "flat+pull", c->nranks, &s, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  const bool wt = s.wt;
+  s = AlgoSpec();
+  s.kind = AlgoKind::TREE;
+  s.widths = {c->nranks};
+  s.ag = AgMode::PULL;
+  s.wt = wt;
+  s.wire = wire_dtype == FLEXAR_FP8_E4M3 ? 2 : 3;
+  if ((rc = executor_proto(c, &s))) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = order_call(c, st))) return rc;
+  uint64_t piece = count;
+  if ((rc = plan_pieces(c, s, count, es, fs, &piece))) return rc;
+  c->calls++;
+  c->bytes += count * es;
+  for (uint64_t off = 0; off < count; off += piece) {
+    const uint64_t n = std::min<uint64_t>(piece, count - off);
+    DevProgram* dp = nullptr;
+    if ((rc = get_program(c, s, n, es, fs, &dp))) return rc;
+    LaunchArgs la;
+    la.kind = LAUNCH_EXEC;
+    fill_ctx(c, dp, (const char*)in + off * es, (char*)out + off * es, &la.ctx);
+    la.ctx.amax_parts = amax_parts;
+    la.grid = choose_grid(c, n * es, dp->prog.nchan);
+    la.stream = st;
+    la.proto = proto_of(s);
+    la.wire = dp->prog.wire;
+    if ((rc = launch_dtype(dtype, op, la))) return rc;
+    c->launches++;
+  }
+  return 0;
 }
 
 int flexar_reduce_scatter(flexar_comm_t c, const void* in, void* out, size_t count, int dtype, int op, void* stream,
@@ -1416,8 +1503,9 @@ static int group_ctx_launched(hipStream_t st) {
 }
 
 // One launch runs every rank of the group: ins/outs are nranks device pointers.
-int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* ins, void* const* outs, size_t count,
-                           int dtype, int op, void* stream, const char* algo, float scale) {
+static int group_allreduce(flexar_comm_t* comms, int nranks, const void* const* ins, void* const* outs, size_t count,
+                           int dtype, int op, void* stream, const char* algo, float scale,
+                           const float* const* amax_parts) {
   if (!comms || nranks < 1) return FLEXAR_ERR_INVALID;
   for (int r = 0; r < nranks; ++r) {
     int rc = validate_call(comms[r], dtype, op, scale);
@@ -1432,6 +1520,7 @@ int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
   for (int r = 0; r < nranks; ++r) {
     int rc = resolve_spec(comms[r], algo, (double)count * es, &specs[r]);
     if (rc) return rc;
+    if ((rc = typed_spec(&specs[r], dtype, op, amax_parts != nullptr))) return rc;
   }
   DevCtx* d_ctx = nullptr;
   if (specs[0].kind == AlgoKind::LL && !ll_usable(comms[0], count, es))
@@ -1480,13 +1569,15 @@ int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
   for (uint64_t off = 0; off < count; off += piece) {
     uint64_t n = std::min<uint64_t>(piece, count - off);
     std::vector<DevCtx> h(nranks);
-    int grid = 0;
+    int grid = 0, wire = 0;
     for (int r = 0; r < nranks; ++r) {
       DevProgram* dp = nullptr;
       int rc = get_program(comms[r], specs[r], n, es, fs, &dp);
       if (rc) return rc;
       const char* in = ins && ins[r] ? (const char*)ins[r] : (const char*)outs[r];
       fill_ctx(comms[r], dp, in + off * es, (char*)outs[r] + off * es, &h[r]);
+      if (amax_parts) h[r].amax_parts = amax_parts[r];
+      wire = dp->prog.wire;
       int g = choose_grid(comms[r], n * es, dp->prog.nchan);
       grid = r == 0 ? g : grid;
       if (g != grid) { set_error("group ranks disagree on grid"); return FLEXAR_ERR_STATE; }
@@ -1503,6 +1594,7 @@ int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
     la.grid = grid;
     la.stream = st;
     la.proto = proto_of(specs[0]);
+    la.wire = wire;
     int rc = launch_dtype(dtype, op, la);
     if (!rc) (void)group_ctx_launched(st);
     if (rc) return rc;
@@ -1510,6 +1602,21 @@ int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
     FX_HIP(hipStreamSynchronize(st));  // d_ctx is reused by the next piece
   }
   return 0;
+}
+
+int flexar_group_allreduce(flexar_comm_t* comms, int nranks, const void* const* ins, void* const* outs, size_t count,
+                           int dtype, int op, void* stream, const char* algo, float scale) {
+  return group_allreduce(comms, nranks, ins, outs, count, dtype, op, stream, algo, scale, nullptr);
+}
+
+// fp8-wire allreduce for an in-process group (tests): amax_parts = nranks device pointers of partials.
+int flexar_group_allreduce_fp8(flexar_comm_t* comms, int nranks, const void* const* ins, void* const* outs,
+                               size_t count, int dtype, int op, void* stream, int wire_dtype,
+                               const float* const* amax_parts) {
+  if (!amax_parts) { set_error("null amax partials"); return FLEXAR_ERR_INVALID; }
+  if (wire_dtype != FLEXAR_FP8_E4M3 && wire_dtype != FLEXAR_FP8_E5M2) { set_error("wire dtype must be fp8"); return FLEXAR_ERR_INVALID; }
+  return group_allreduce(comms, nranks, ins, outs, count, dtype, op, stream,
+                         wire_dtype == FLEXAR_FP8_E4M3 ? "flat+pull+e4m3" : "flat+pull+e5m2", 1.0f, amax_parts);
 }
 
 // Reduce-scatter / all-gather for an in-process group (tests): one launch, every rank of the group.
@@ -1537,7 +1644,7 @@ int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const vo
     proto = proto_of(s);
     DevProgram* dp = nullptr;
     if ((rc = get_program(comms[r], s, count, es, fs, &dp, (Coll)coll, count))) return rc;
-    if (dp->prog.stg_elems * es > comms[r]->exec_half) { set_error("group collective exceeds workspace"); return FLEXAR_ERR_NOMEM; }
+    if (dp->prog.stg_bytes() > comms[r]->exec_half) { set_error("group collective exceeds workspace"); return FLEXAR_ERR_NOMEM; }
     fill_ctx(comms[r], dp, ins[r], outs[r], &h[r]);
     int g = choose_grid(comms[r], count * es * nranks, dp->prog.nchan);
     grid = r == 0 ? g : grid;
@@ -1579,7 +1686,7 @@ int flexar_group_broadcast(flexar_comm_t* comms, int nranks, int root, const voi
     proto = proto_of(s);
     DevProgram* dp = nullptr;
     if ((rc = get_program(comms[r], s, count, es, 1.0f, &dp, Coll::BROADCAST, (uint64_t)root))) return rc;
-    if (dp->prog.stg_elems * es > comms[r]->exec_half) { set_error("group broadcast exceeds workspace"); return FLEXAR_ERR_NOMEM; }
+    if (dp->prog.stg_bytes() > comms[r]->exec_half) { set_error("group broadcast exceeds workspace"); return FLEXAR_ERR_NOMEM; }
     const void* in = ins && ins[r] ? ins[r] : outs[r];
     fill_ctx(comms[r], dp, in, outs[r], &h[r]);
     int g = choose_grid(comms[r], count * es, dp->prog.nchan);

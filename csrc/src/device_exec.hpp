@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "flexar/program.hpp"
 #include "flexar/types.hpp"
 
@@ -48,7 +50,14 @@ struct DevCtx {
   uint32_t nranks;
   uint64_t count;  // elements
   float scale;
+  // typed programs (Program::wire, planner.hpp): STG offsets count stg_unit bytes; fp8 wire modes
+  // derive the pre-scale from this rank's amax partials and the peers' amax granules
+  uint32_t stg_unit;
+  const float* amax_parts;  // FLEXAR_AMAX_PARTIALS per-workgroup max |x| of this rank's input
+  uint64_t amax_off;        // byte offset of the amax granule slots in each staging parity half
 };
+constexpr uint32_t kAmaxParts = 256;    // == FLEXAR_AMAX_PARTIALS
+constexpr uint64_t kAmaxRegion = 256;   // bytes reserved per parity half for the amax granules
 
 // 16-byte vector memory ops (global_load/store_dwordx4). Payload bytes are touched once, so loads use
 // the streaming (nontemporal) policy by default: measured on MI355X (bench/kernel_bench.py, profiles/)
@@ -311,21 +320,268 @@ __device__ FX_INLINE void xfer_op(const DevCtx& c, const Op* o, uint32_t lb, uin
   }
 }
 
-template <typename T, typename OP, int PM>
+// ---------------------------------------------------------------------------------------------
+// Typed XFER (Program::wire): operands of two storage types in one fused pass. Each lane handles G
+// elements per step, G = 16 bytes of the narrower type, so every operand moves in whole 16-B vectors
+// (VT / VW of them for a dtype / wire-typed operand) and all of a step's loads are issued before the
+// first is consumed (the operand type is workgroup-uniform: the per-operand branches are scalar).
+//   wire-typed source: its value;  dtype source: its value, or with an fp8 wire the value quantised with
+//   the pre-scale (x * s -> fp8 -> f32) so every contribution is rounded once and identically;
+//   y = scale * sum (fp32);  with an fp8 destination y is rounded to fp8 first, so the dtype destination
+//   (y / s) and the fp8 copies the peers receive carry the same value on every rank.
+template <typename W>
+__device__ FX_INLINE float wround(float x) {
+  return (float)Elem<W>::load(Elem<W>::store((typename Elem<W>::acc)x));
+}
+template <typename S, int G>
+__device__ FX_INLINE void decode_g(const uint4* raw, float (&x)[G]) {
+  S v[G];
+  __builtin_memcpy(v, raw, sizeof(S) * G);
+#pragma unroll
+  for (int e = 0; e < G; ++e) x[e] = (float)Elem<S>::load(v[e]);
+}
+template <typename S, int G>
+__device__ FX_INLINE void encode_g(const float (&x)[G], uint4* raw) {
+  S v[G];
+#pragma unroll
+  for (int e = 0; e < G; ++e) v[e] = Elem<S>::store((typename Elem<S>::acc)x[e]);
+  __builtin_memcpy(raw, v, sizeof(S) * G);
+}
+
+template <typename T, typename W, int K, int PM>
+__device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], uint32_t sm, char* const (&d)[kMaxDst], int nd,
+                                  uint32_t dm, uint64_t n, float scale, float pre, float post_inv, bool vec) {
+  constexpr int U = sizeof(T) < sizeof(W) ? (int)sizeof(T) : (int)sizeof(W);
+  constexpr int G = 16 / U;
+  constexpr int VT = (int)sizeof(T) * G / 16, VW = (int)sizeof(W) * G / 16;
+  constexpr int VM = VT > VW ? VT : VW;
+  constexpr bool FP8 = sizeof(W) == 1;
+  constexpr bool WT = PM == PM_WT;
+  constexpr bool NTS = PM == PM_FENCE_NTS;
+  const uint64_t nt = blockDim.x;
+  const uint64_t ng = vec ? n / G : 0;
+  __amdgpu_buffer_rsrc_t rs[K], rd[kMaxDst];
+  if constexpr (WT) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) rs[k] = rsrc_of(s[k], n * ((sm >> k) & 1 ? sizeof(W) : sizeof(T)));
+#pragma unroll
+    for (int dd = 0; dd < kMaxDst; ++dd)
+      if (dd < nd) rd[dd] = rsrc_of(d[dd], n * ((dm >> dd) & 1 ? sizeof(W) : sizeof(T)));
+  }
+  auto ld = [&](int k, uint64_t byte) -> uint4 {
+    if constexpr (WT) return ld16_sys(rs[k], (uint32_t)byte);
+    else return ld16(s[k] + byte);
+  };
+  auto st = [&](int dd, uint64_t byte, uint4 y) {
+    if constexpr (WT) st16_sys(rd[dd], (uint32_t)byte, y);
+    else st16<NTS>(d[dd] + byte, y);
+  };
+  for (uint64_t v = threadIdx.x; v < ng; v += nt) {
+    uint4 raw[K][VM];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const bool w = (sm >> k) & 1;
+      const uint64_t at = v * G * (w ? sizeof(W) : sizeof(T));
+#pragma unroll
+      for (int j = 0; j < VM; ++j)
+        if (j < (w ? VW : VT)) raw[k][j] = ld(k, at + 16 * j);
+    }
+    float acc[G];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      float x[G];
+      if ((sm >> k) & 1) {
+        decode_g<W, G>(raw[k], x);
+      } else {
+        decode_g<T, G>(raw[k], x);
+        if constexpr (FP8) {
+#pragma unroll
+          for (int e = 0; e < G; ++e) x[e] = wround<W>(x[e] * pre);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < G; ++e) acc[e] = k ? acc[e] + x[e] : x[e];
+    }
+#pragma unroll
+    for (int e = 0; e < G; ++e) acc[e] *= scale;
+    if (FP8 && dm) {
+#pragma unroll
+      for (int e = 0; e < G; ++e) acc[e] = wround<W>(acc[e]);
+    }
+#pragma unroll
+    for (int dd = 0; dd < kMaxDst; ++dd) {
+      if (dd >= nd) continue;
+      uint4 y[VM];
+      if ((dm >> dd) & 1) {
+        encode_g<W, G>(acc, y);
+#pragma unroll
+        for (int j = 0; j < VW; ++j) st(dd, v * G * sizeof(W) + 16 * j, y[j]);
+      } else {
+        float t[G];
+#pragma unroll
+        for (int e = 0; e < G; ++e) t[e] = FP8 ? acc[e] * post_inv : acc[e];
+        encode_g<T, G>(t, y);
+#pragma unroll
+        for (int j = 0; j < VT; ++j) st(dd, v * G * sizeof(T) + 16 * j, y[j]);
+      }
+    }
+  }
+  // scalar tail (or the whole span when a caller buffer is not 16-B aligned)
+  for (uint64_t i = ng * G + threadIdx.x; i < n; i += nt) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      float x;
+      if ((sm >> k) & 1) {
+        x = (float)Elem<W>::load(ld_elem<PM, W>(s[k], i));
+      } else {
+        x = (float)Elem<T>::load(ld_elem<PM, T>(s[k], i));
+        if constexpr (FP8) x = wround<W>(x * pre);
+      }
+      acc = k ? acc + x : x;
+    }
+    acc *= scale;
+    if (FP8 && dm) acc = wround<W>(acc);
+#pragma unroll
+    for (int dd = 0; dd < kMaxDst; ++dd) {
+      if (dd >= nd) continue;
+      if ((dm >> dd) & 1) st_elem<PM, W>(d[dd], i, Elem<W>::store((typename Elem<W>::acc)acc));
+      else st_elem<PM, T>(d[dd], i, Elem<T>::store((typename Elem<T>::acc)(FP8 ? acc * post_inv : acc)));
+    }
+  }
+}
+
+// Typed op: operand addresses (STG offsets in units, element slice [lo, hi) in each operand's own
+// type), then the all-dtype / all-wire fast paths or the mixed one.
+template <typename T, typename W, int PM>
+__device__ FX_INLINE void xfer_op_typed(const DevCtx& c, const Op* o, uint32_t lb, uint32_t nb, uint32_t quantum,
+                                        uint64_t par, float pre, float post_inv) {
+  uint64_t lo, hi;
+  slice_range(o->len, lb, nb, quantum, &lo, &hi);
+  if (hi <= lo) return;
+  constexpr bool FP8 = sizeof(W) == 1;
+  const int ns = o->nsrc, nd = o->ndst;
+  const uint32_t sm = o->pad16[0], dm = o->pad16[1];
+  const char* s[kMaxSrc];
+  char* d[kMaxDst];
+  bool vec = true;
+#pragma unroll
+  for (int k = 0; k < kMaxSrc; ++k) {
+    s[k] = nullptr;
+    if (k < ns) {
+      const Loc l = o->src[k];
+      const uint64_t es = (sm >> k) & 1 ? sizeof(W) : sizeof(T);
+      s[k] = (l.buf == BUF_STG) ? c.peer_stg[l.rank] + par + l.off * c.stg_unit + lo * es
+                                : c.local[l.buf] + (l.off + lo) * sizeof(T);
+      vec &= (l.buf == BUF_STG) || c.vec_ok;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kMaxDst; ++k) {
+    d[k] = nullptr;
+    if (k < nd) {
+      const Loc l = o->dst[k];
+      const uint64_t es = (dm >> k) & 1 ? sizeof(W) : sizeof(T);
+      d[k] = (l.buf == BUF_STG) ? c.peer_stg[l.rank] + par + l.off * c.stg_unit + lo * es
+                                : c.local[l.buf] + (l.off + lo) * sizeof(T);
+      vec &= (l.buf == BUF_STG) || c.vec_ok;
+    }
+  }
+  const uint64_t n = hi - lo;
+  const uint32_t all_s = (1u << ns) - 1, all_d = (1u << nd) - 1;
+  if (sm == all_s && dm == all_d) {  // wire type throughout (fp32 partial -> fp32 partial, fp8 copy)
+    xfer_dispatch<W, OpSum, PM>(ns, s, d, nd, n, o->scale, vec);
+    return;
+  }
+  if (!FP8 && sm == 0 && dm == 0) {  // dtype throughout (raw inputs, all-gather copies)
+    xfer_dispatch<T, OpSum, PM>(ns, s, d, nd, n, o->scale, vec);
+    return;
+  }
+  switch (ns) {
+    case 1: xfer_mx<T, W, 1, PM>(s, sm, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    case 2: xfer_mx<T, W, 2, PM>(s, sm, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    case 3: xfer_mx<T, W, 3, PM>(s, sm, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    case 4: xfer_mx<T, W, 4, PM>(s, sm, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    case 5: xfer_mx<T, W, 5, PM>(s, sm, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    case 6: xfer_mx<T, W, 6, PM>(s, sm, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    case 7: xfer_mx<T, W, 7, PM>(s, sm, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    default: xfer_mx<T, W, 8, PM>(s, sm, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+  }
+}
+
+// fp8 wire prologue: every workgroup derives the call's pre-scale s = fp8_max / (N * global amax).
+// Workgroup 0 publishes this rank's amax (max over its partials) to every rank as an {epoch, value}
+// granule (the LL protocol's data-tagged hand-off: no flag, no fence); every workgroup gathers all N
+// granules and takes the max, so all ranks use the same s. Returns false on a watchdog timeout.
+template <typename W>
+__device__ FX_INLINE bool fp8_scale(const DevCtx& c, uint32_t b, uint64_t epoch, uint64_t par, float* s_out) {
+  const uint32_t lane = threadIdx.x;
+  float m = 0.0f;
+  for (uint32_t i = lane; i < kAmaxParts; i += 64) m = __builtin_fmaxf(m, c.amax_parts[i]);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) m = __builtin_fmaxf(m, __shfl_xor(m, off, 64));
+  const uint64_t tag = epoch & 0xffffffffull;
+  if (b == 0 && lane < c.nranks)
+    st_flag(reinterpret_cast<uint64_t*>(c.peer_stg[lane] + par + c.amax_off) + c.rank, (tag << 32) | f2u(m));
+  float g = 0.0f;
+  bool ok = true;
+  if (lane < c.nranks) {
+    uint64_t* slot = reinterpret_cast<uint64_t*>(c.peer_stg[c.rank] + par + c.amax_off) + lane;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t v;
+    while (((v = ld_flag(slot)) >> 32) != tag) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > c.timeout_ticks) {
+        __hip_atomic_store(c.err, (uint32_t)(0x80000000u | (0xfeu << 8) | lane), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        ok = false;
+        break;
+      }
+    }
+    g = u2f((uint32_t)v);
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) g = __builtin_fmaxf(g, __shfl_xor(g, off, 64));
+  const float wmax = (float)Elem<W>::load(Elem<W>::store(1e30f));  // saturating encode: the type's max
+  *s_out = (g > 0.0f && g < 3.0e38f) ? wmax / ((float)c.nranks * g) : 1.0f;
+  return __all(ok) != 0;
+}
+
+template <typename T, typename OP, int PM, typename W = void>
 __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uint32_t grid) {
   __shared__ int s_abort;
+  __shared__ float s_pre;
   const uint32_t tid = threadIdx.x;
   const uint32_t nchan = c.nchan;
   const uint32_t ch = b % nchan, lb = b / nchan;
   const uint32_t nb = (grid - ch + nchan - 1) / nchan;
-  const uint32_t quantum = sizeof(T) >= 16 ? 1u : (uint32_t)(16 / sizeof(T));
+  constexpr bool TYPED = !std::is_void<W>::value;
+  using WT_ = typename std::conditional<TYPED, W, T>::type;
+  constexpr uint32_t U = sizeof(T) < sizeof(WT_) ? sizeof(T) : sizeof(WT_);
+  const uint32_t quantum = TYPED ? 16 / U : (sizeof(T) >= 16 ? 1u : (uint32_t)(16 / sizeof(T)));
   const uint64_t epoch = c.epochs[b] + 1;
   const uint64_t par = (epoch & 1) ? c.stg_half_bytes : 0;
   if (tid == 0) s_abort = 0;
-  __syncthreads();
+  float pre = 1.0f;
+  if constexpr (TYPED && sizeof(WT_) == 1) {
+    if (tid < 64) {
+      float sc;
+      const bool ok = fp8_scale<WT_>(c, b, epoch, par, &sc);
+      if (tid == 0) {
+        s_pre = sc;
+        if (!ok) s_abort = 1;
+      }
+    }
+    __syncthreads();
+    pre = s_pre;
+  } else {
+    __syncthreads();
+  }
+  const float post_inv = 1.0f / pre;
+  (void)post_inv;
 
   const uint32_t i0 = c.chan_start[ch], i1 = c.chan_start[ch + 1];
-  for (uint32_t i = i0; i < i1;) {
+  for (uint32_t i = s_abort ? i1 : i0; i < i1;) {
     const Op* o = c.ops + i;
     const uint16_t kind = o->kind;
     if (kind == OP_XFER) {
@@ -335,7 +591,8 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
       bool bar = false;
       for (uint32_t k = 0; k < n; ++k) {
         const Op* q = c.ops + i + (n > 1 ? (k + lb) % n : 0);
-        xfer_op<T, OP, PM>(c, q, lb, nb, quantum, par);
+        if constexpr (TYPED) xfer_op_typed<T, WT_, PM>(c, q, lb, nb, quantum, par, pre, post_inv);
+        else xfer_op<T, OP, PM>(c, q, lb, nb, quantum, par);
         bar |= (q->flags & kXferBarrierAfter) != 0;
       }
       if (bar) __syncthreads();
@@ -500,6 +757,17 @@ __global__ void __launch_bounds__(kExecThreads) ll_group_kernel(const DevCtx* ct
 template <typename T, typename OP, int PM>
 __global__ void __launch_bounds__(kExecThreads) exec_kernel(DevCtx c) {
   exec_body<T, OP, PM>(c, blockIdx.x, gridDim.x);
+}
+
+// Typed programs (Program::wire: fp32 partials or an fp8 wire), SUM/AVG only.
+template <typename T, typename W, int PM>
+__global__ void __launch_bounds__(kExecThreads) exec_mx_kernel(DevCtx c) {
+  exec_body<T, OpSum, PM, W>(c, blockIdx.x, gridDim.x);
+}
+template <typename T, typename W, int PM>
+__global__ void __launch_bounds__(kExecThreads) exec_mx_group_kernel(const DevCtx* ctxs, uint32_t grid_per_rank) {
+  const uint32_t r = blockIdx.x / grid_per_rank;
+  exec_body<T, OpSum, PM, W>(ctxs[r], blockIdx.x % grid_per_rank, grid_per_rank);
 }
 
 // In-process group launch: nranks ranks share one grid (rank = blockIdx / grid_per_rank) —

@@ -1,0 +1,9 @@
+// Typed executors, bf16 inputs over an fp8 wire ("+e4m3" / "+e5m2": flat schedule, the pre-scale from
+// the global amax fused into the first transfer, the post-scale into the last).
+#include "kernels_impl.hpp"
+
+namespace flexar {
+int launch_mx_wire_bf16(const LaunchArgs& a) {
+  return a.wire == 3 ? launch_typed<bf16_t, fp8e5m2_t>(a) : launch_typed<bf16_t, fp8e4m3_t>(a);
+}
+}  // namespace flexar

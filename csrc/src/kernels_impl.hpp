@@ -112,6 +112,40 @@ inline int launch_int(int op, const LaunchArgs& a) {
 
 }  // namespace flexar
 
+namespace flexar {
+
+// Typed-program executor launch (exec_mx_kernel<T, W, PM>); "+nts" runs the fence protocol.
+template <typename T, typename W>
+inline int launch_typed(const LaunchArgs& a) {
+  const bool wt = a.proto == PM_WT;
+  switch (a.kind) {
+    case LAUNCH_QUERY:
+      return query_kernel(wt ? exec_mx_kernel<T, W, PM_WT> : exec_mx_kernel<T, W, PM_FENCE>, a);
+    case LAUNCH_EXEC:
+      if (wt) hipLaunchKernelGGL((exec_mx_kernel<T, W, PM_WT>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
+      else hipLaunchKernelGGL((exec_mx_kernel<T, W, PM_FENCE>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
+      break;
+    case LAUNCH_GROUP:
+      if (wt)
+        hipLaunchKernelGGL((exec_mx_group_kernel<T, W, PM_WT>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
+                           a.stream, a.d_ctxs, (uint32_t)a.grid);
+      else
+        hipLaunchKernelGGL((exec_mx_group_kernel<T, W, PM_FENCE>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
+                           a.stream, a.d_ctxs, (uint32_t)a.grid);
+      break;
+    default:
+      return FLEXAR_ERR_INVALID;
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(std::string("kernel launch: ") + hipGetErrorString(e));
+    return FLEXAR_ERR_HIP;
+  }
+  return 0;
+}
+
+}  // namespace flexar
+
 #define FX_DEFINE_FLOAT_LAUNCH(T, NAME) \
   namespace flexar {                    \
   int launch_##NAME(int op, const LaunchArgs& a) { return launch_float<T>(op, a); } \

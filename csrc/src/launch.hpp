@@ -31,7 +31,30 @@ struct LaunchArgs {
   int query = 0;         // QUERY: which kernel
   int* occ_out = nullptr;
   int* regs_out = nullptr;
+  int wire = 0;          // EXEC / GROUP / QUERY of a typed program (Program::wire): 1 fp32, 2 e4m3, 3 e5m2
 };
+
+// Typed-program executors (exec_mx_kernel), SUM/AVG only: fp32 partials for 16/8-bit dtypes
+// (k_mx_acc*.hip) and an fp8 wire for 32/16-bit floats (k_mx_wire_*.hip), one translation unit per
+// input dtype so the gfx950 build parallelises.
+int launch_mx_acc16(int dtype, const LaunchArgs& a);  // bf16, fp16 -> fp32 partials
+int launch_mx_acc8(int dtype, const LaunchArgs& a);   // e4m3, e5m2 -> fp32 partials
+int launch_mx_wire_f32(const LaunchArgs& a);          // fp32 over e4m3 / e5m2 (a.wire)
+int launch_mx_wire_bf16(const LaunchArgs& a);
+int launch_mx_wire_f16(const LaunchArgs& a);
+inline int launch_mx(int dtype, const LaunchArgs& a) {
+  if (a.wire == 1) {
+    if (dtype == FLEXAR_BFLOAT16 || dtype == FLEXAR_FLOAT16) return launch_mx_acc16(dtype, a);
+    if (dtype == FLEXAR_FP8_E4M3 || dtype == FLEXAR_FP8_E5M2) return launch_mx_acc8(dtype, a);
+    return FLEXAR_ERR_UNSUPPORTED;
+  }
+  switch (dtype) {
+    case FLEXAR_FLOAT32: return launch_mx_wire_f32(a);
+    case FLEXAR_BFLOAT16: return launch_mx_wire_bf16(a);
+    case FLEXAR_FLOAT16: return launch_mx_wire_f16(a);
+    default: return FLEXAR_ERR_UNSUPPORTED;
+  }
+}
 
 // Defined in k_<dtype>.hip; returns 0 or a FLEXAR_ERR_* code.
 #define FX_DECLARE_LAUNCH(NAME) int launch_##NAME(int op, const LaunchArgs& a);
@@ -53,6 +76,10 @@ FX_DECLARE_LAUNCH(boolean)
 #undef FX_DECLARE_LAUNCH
 
 inline int launch_dtype(int dtype, int op, const LaunchArgs& a) {
+  if (a.wire && (a.kind == LAUNCH_EXEC || a.kind == LAUNCH_GROUP || a.kind == LAUNCH_QUERY)) {
+    if (op != FLEXAR_SUM && op != FLEXAR_AVG) return FLEXAR_ERR_UNSUPPORTED;
+    return launch_mx(dtype, a);
+  }
   switch (dtype) {
     case FLEXAR_FLOAT32: return launch_f32(op, a);
     case FLEXAR_FLOAT16: return launch_f16(op, a);
