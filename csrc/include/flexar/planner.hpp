@@ -838,6 +838,25 @@ inline void io_extent(Coll coll, uint32_t N, uint64_t count, uint64_t stride, ui
   }
 }
 
+// The typed XFER forms the device executor runs (device_exec.hpp xfer_mx_k): sources all dtype (SP_T),
+// own dtype + peers wire (SP_TW) or all wire (SP_W); fp8 wire: K = 1 pushes / all-gathers and K >= 2
+// reductions, fp32 partials: K >= 2 (SP_TW only as the ring's K = 2 step). Masks must match the operands.
+inline bool typed_pattern_ok(const Program& P, const Op& o) {
+  uint32_t sm = 0, dm = 0;
+  for (int k = 0; k < o.nsrc; ++k) sm |= (o.src[k].pad & 1u) << k;
+  for (int k = 0; k < o.ndst; ++k) dm |= (o.dst[k].pad & 1u) << k;
+  if (sm != o.pad16[0] || dm != o.pad16[1]) return false;
+  const uint32_t all_s = (1u << o.nsrc) - 1, all_d = (1u << o.ndst) - 1;
+  const bool fp8 = P.wire >= 2;
+  const int K = o.nsrc;
+  if (sm == all_s && dm == all_d) return true;  // wire type throughout
+  if (!fp8 && sm == 0 && dm == 0) return true;  // dtype throughout
+  if (sm == 0) return fp8 ? K == 1 : K >= 2;
+  if (sm == (all_s & ~1u)) return K >= 2 && (fp8 || K == 2);
+  if (sm == all_s) return fp8 ? K == 1 : K >= 2;
+  return false;
+}
+
 // Host-side bounds check of a compiled program before it is uploaded or launched: every XFER operand
 // stays inside its buffer (IN/OUT: this rank's, within the call's extent; STG: any rank's, within the
 // program's staging), fan-in/fan-out and peer lists within the kernel's fixed arrays, flag slots within
@@ -865,6 +884,7 @@ inline bool validate_program(const Program& P, uint32_t N, uint32_t rank, uint64
     const std::string at = "op " + std::to_string(i);
     if (o.kind == OP_XFER) {
       if (o.nsrc < 1 || o.nsrc > kMaxSrc || o.ndst < 1 || o.ndst > kMaxDst) return fail(at + ": operand count");
+      if (P.wire && !typed_pattern_ok(P, o)) return fail(at + ": typed operand pattern the executor does not run");
       for (int k = 0; k < o.nsrc; ++k)
         if (!loc_ok(o.src[k], o.len)) return fail(at + ": source " + std::to_string(k) + " out of bounds");
       for (int k = 0; k < o.ndst; ++k)

@@ -698,6 +698,11 @@ static int resident_blocks(int device) {
 
 static int check_err(flexar_comm* c) {
   uint32_t e = __atomic_load_n(c->err_host, __ATOMIC_ACQUIRE);
+  if ((e & 0x40000000u) && ((e >> 8) & 0xffffu) == 0xfdu) {
+    set_error("rank " + std::to_string(c->rank) + ": internal: a typed transfer with an operand pattern the "
+              "executor does not run (planner/executor mismatch)");
+    return FLEXAR_ERR_STATE;
+  }
   if (e & 0x40000000u) {
     char buf[200];
     snprintf(buf, sizeof(buf), "rank %d: protocol violation — peer %u is more than one call ahead (slot %u): "

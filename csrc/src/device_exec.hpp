@@ -333,37 +333,103 @@ template <typename W>
 __device__ FX_INLINE float wround(float x) {
   return (float)Elem<W>::load(Elem<W>::store((typename Elem<W>::acc)x));
 }
-template <typename S, int G>
-__device__ FX_INLINE void decode_g(const uint4* raw, float (&x)[G]) {
-  S v[G];
-  __builtin_memcpy(v, raw, sizeof(S) * G);
-#pragma unroll
-  for (int e = 0; e < G; ++e) x[e] = (float)Elem<S>::load(v[e]);
+template <typename S> struct IsFp8 { static constexpr bool value = false; static constexpr bool e4m3 = false; };
+template <> struct IsFp8<fp8e4m3_t> { static constexpr bool value = true; static constexpr bool e4m3 = true; };
+template <> struct IsFp8<fp8e5m2_t> { static constexpr bool value = true; static constexpr bool e4m3 = false; };
+
+// fp8 words through the packed gfx950 converters: v_cvt_pk_f32_fp8 / _bf8 turn two bytes of a word into
+// two floats, v_cvt_pk_fp8_f32 / _bf8_f32 two floats into two bytes (RNE) — 2 instructions per 4 elements.
+// No saturation: only for values the fp8 wire's pre-scale keeps in range (|x| <= fp8 max by construction).
+template <typename S>
+__device__ FX_INLINE void fp8_word_decode(uint32_t w, float* x) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 lo, hi;
+  if constexpr (IsFp8<S>::e4m3) {
+    lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)w, false);
+    hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)w, true);
+  } else {
+    lo = __builtin_amdgcn_cvt_pk_f32_bf8((int)w, false);
+    hi = __builtin_amdgcn_cvt_pk_f32_bf8((int)w, true);
+  }
+  x[0] = lo.x; x[1] = lo.y; x[2] = hi.x; x[3] = hi.y;
 }
-template <typename S, int G>
-__device__ FX_INLINE void encode_g(const float (&x)[G], uint4* raw) {
-  S v[G];
-#pragma unroll
-  for (int e = 0; e < G; ++e) v[e] = Elem<S>::store((typename Elem<S>::acc)x[e]);
-  __builtin_memcpy(raw, v, sizeof(S) * G);
+template <typename S>
+__device__ FX_INLINE uint32_t fp8_word_encode(const float* x) {
+  int w;
+  if constexpr (IsFp8<S>::e4m3) {
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(x[0], x[1], 0, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(x[2], x[3], w, true);
+  } else {
+    w = __builtin_amdgcn_cvt_pk_bf8_f32(x[0], x[1], 0, false);
+    w = __builtin_amdgcn_cvt_pk_bf8_f32(x[2], x[3], w, true);
+  }
+  return (uint32_t)w;
 }
 
-template <typename T, typename W, int K, int PM>
-__device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], uint32_t sm, char* const (&d)[kMaxDst], int nd,
-                                  uint32_t dm, uint64_t n, float scale, float pre, float post_inv, bool vec) {
+template <typename S, int G>
+__device__ FX_INLINE void decode_g(const uint4* raw, float (&x)[G]) {
+  if constexpr (IsFp8<S>::value && G % 4 == 0) {
+    uint32_t w[G / 4];
+    __builtin_memcpy(w, raw, G);
+#pragma unroll
+    for (int i = 0; i < G / 4; ++i) fp8_word_decode<S>(w[i], x + 4 * i);
+  } else {
+    S v[G];
+    __builtin_memcpy(v, raw, sizeof(S) * G);
+#pragma unroll
+    for (int e = 0; e < G; ++e) x[e] = (float)Elem<S>::load(v[e]);
+  }
+}
+// SAT = false: packed fp8 encode without saturation (fp8 wire values, in range by construction)
+template <typename S, int G, bool SAT = true>
+__device__ FX_INLINE void encode_g(const float (&x)[G], uint4* raw) {
+  if constexpr (!SAT && IsFp8<S>::value && G % 4 == 0) {
+    uint32_t w[G / 4];
+#pragma unroll
+    for (int i = 0; i < G / 4; ++i) w[i] = fp8_word_encode<S>(x + 4 * i);
+    __builtin_memcpy(raw, w, G);
+  } else {
+    S v[G];
+#pragma unroll
+    for (int e = 0; e < G; ++e) v[e] = Elem<S>::store((typename Elem<S>::acc)x[e]);
+    __builtin_memcpy(raw, v, sizeof(S) * G);
+  }
+}
+// x <- fp8(x) for G values in range (packed encode + decode)
+template <typename S, int G>
+__device__ FX_INLINE void fp8_round_g(float (&x)[G]) {
+#pragma unroll
+  for (int i = 0; i < G / 4; ++i) fp8_word_decode<S>(fp8_word_encode<S>(x + 4 * i), x + 4 * i);
+}
+
+// Source patterns of a typed XFER (bit k of the source mask = operand k has the wire type). The
+// planner only emits three (validate_typed_patterns): SP_T every source has the dtype (tree stage 0
+// into fp32 partials, fp8 quantising push), SP_TW the first source (the rank's own value) has the dtype
+// and the rest the wire type (ring step, fp8 reduction), SP_W every source has the wire type (final
+// stage out of fp32 partials, fp8 all-gather). The pattern is a template parameter, so every operand's
+// vector count is known at compile time and UU groups per lane are in flight per step (the same
+// ~4-8 outstanding 16-B loads per lane as the untyped path).
+enum : int { SP_T = 0, SP_TW = 1, SP_W = 2 };
+
+template <typename T, typename W, int K, int SP, int PM>
+__device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (&d)[kMaxDst], int nd, uint32_t dm,
+                                  uint64_t n, float scale, float pre, float post_inv, bool vec) {
   constexpr int U = sizeof(T) < sizeof(W) ? (int)sizeof(T) : (int)sizeof(W);
   constexpr int G = 16 / U;
   constexpr int VT = (int)sizeof(T) * G / 16, VW = (int)sizeof(W) * G / 16;
   constexpr int VM = VT > VW ? VT : VW;
+  constexpr int V = SP == SP_T ? K * VT : (SP == SP_TW ? VT + (K - 1) * VW : K * VW);
+  constexpr int UU = V <= 2 ? 4 : (V <= 4 ? 2 : 1);
   constexpr bool FP8 = sizeof(W) == 1;
   constexpr bool WT = PM == PM_WT;
   constexpr bool NTS = PM == PM_FENCE_NTS;
+  auto isw = [](int k) constexpr -> bool { return SP == SP_W || (SP == SP_TW && k > 0); };
   const uint64_t nt = blockDim.x;
   const uint64_t ng = vec ? n / G : 0;
   __amdgpu_buffer_rsrc_t rs[K], rd[kMaxDst];
   if constexpr (WT) {
 #pragma unroll
-    for (int k = 0; k < K; ++k) rs[k] = rsrc_of(s[k], n * ((sm >> k) & 1 ? sizeof(W) : sizeof(T)));
+    for (int k = 0; k < K; ++k) rs[k] = rsrc_of(s[k], n * (isw(k) ? sizeof(W) : sizeof(T)));
 #pragma unroll
     for (int dd = 0; dd < kMaxDst; ++dd)
       if (dd < nd) rd[dd] = rsrc_of(d[dd], n * ((dm >> dd) & 1 ? sizeof(W) : sizeof(T)));
@@ -376,55 +442,73 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], uint32_t sm, 
     if constexpr (WT) st16_sys(rd[dd], (uint32_t)byte, y);
     else st16<NTS>(d[dd] + byte, y);
   };
-  for (uint64_t v = threadIdx.x; v < ng; v += nt) {
-    uint4 raw[K][VM];
+  auto load_group = [&](uint64_t g, uint4 (&raw)[K][VM]) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const bool w = (sm >> k) & 1;
-      const uint64_t at = v * G * (w ? sizeof(W) : sizeof(T));
+      const uint64_t at = g * G * (isw(k) ? sizeof(W) : sizeof(T));
 #pragma unroll
-      for (int j = 0; j < VM; ++j)
-        if (j < (w ? VW : VT)) raw[k][j] = ld(k, at + 16 * j);
+      for (int j = 0; j < (isw(k) ? VW : VT); ++j) raw[k][j] = ld(k, at + 16 * j);
     }
+  };
+  // fp8 wire: a single dtype source quantised straight into fp8 destinations (the push) needs one
+  // rounding, done by the store's encode; any dtype destination needs the rounded value itself
+  const bool direct = FP8 && K == 1 && SP == SP_T && dm == (1u << nd) - 1 && scale == 1.0f;
+  const bool round_y = FP8 && dm && !direct;
+  auto finish_group = [&](uint64_t g, const uint4 (&raw)[K][VM]) {
     float acc[G];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       float x[G];
-      if ((sm >> k) & 1) {
+      if (isw(k)) {
         decode_g<W, G>(raw[k], x);
       } else {
         decode_g<T, G>(raw[k], x);
         if constexpr (FP8) {
 #pragma unroll
-          for (int e = 0; e < G; ++e) x[e] = wround<W>(x[e] * pre);
+          for (int e = 0; e < G; ++e) x[e] *= pre;
+          if (!direct) fp8_round_g<W, G>(x);
         }
       }
 #pragma unroll
       for (int e = 0; e < G; ++e) acc[e] = k ? acc[e] + x[e] : x[e];
     }
+    if (scale != 1.0f) {
 #pragma unroll
-    for (int e = 0; e < G; ++e) acc[e] *= scale;
-    if (FP8 && dm) {
-#pragma unroll
-      for (int e = 0; e < G; ++e) acc[e] = wround<W>(acc[e]);
+      for (int e = 0; e < G; ++e) acc[e] *= scale;
+    }
+    if constexpr (FP8) {
+      if (round_y) fp8_round_g<W, G>(acc);
     }
 #pragma unroll
     for (int dd = 0; dd < kMaxDst; ++dd) {
       if (dd >= nd) continue;
       uint4 y[VM];
       if ((dm >> dd) & 1) {
-        encode_g<W, G>(acc, y);
+        encode_g<W, G, !FP8>(acc, y);  // fp8 wire values are in range: packed encode, no clamp
 #pragma unroll
-        for (int j = 0; j < VW; ++j) st(dd, v * G * sizeof(W) + 16 * j, y[j]);
+        for (int j = 0; j < VW; ++j) st(dd, g * G * sizeof(W) + 16 * j, y[j]);
       } else {
         float t[G];
 #pragma unroll
         for (int e = 0; e < G; ++e) t[e] = FP8 ? acc[e] * post_inv : acc[e];
         encode_g<T, G>(t, y);
 #pragma unroll
-        for (int j = 0; j < VT; ++j) st(dd, v * G * sizeof(T) + 16 * j, y[j]);
+        for (int j = 0; j < VT; ++j) st(dd, g * G * sizeof(T) + 16 * j, y[j]);
       }
     }
+  };
+  uint64_t v = threadIdx.x;
+  for (; v + (UU - 1) * nt < ng; v += UU * nt) {
+    uint4 raw[UU][K][VM];
+#pragma unroll
+    for (int u = 0; u < UU; ++u) load_group(v + u * nt, raw[u]);
+#pragma unroll
+    for (int u = 0; u < UU; ++u) finish_group(v + u * nt, raw[u]);
+  }
+  for (; v < ng; v += nt) {
+    uint4 raw[K][VM];
+    load_group(v, raw);
+    finish_group(v, raw);
   }
   // scalar tail (or the whole span when a caller buffer is not 16-B aligned)
   for (uint64_t i = ng * G + threadIdx.x; i < n; i += nt) {
@@ -432,7 +516,7 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], uint32_t sm, 
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       float x;
-      if ((sm >> k) & 1) {
+      if (isw(k)) {
         x = (float)Elem<W>::load(ld_elem<PM, W>(s[k], i));
       } else {
         x = (float)Elem<T>::load(ld_elem<PM, T>(s[k], i));
@@ -449,6 +533,29 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], uint32_t sm, 
       else st_elem<PM, T>(d[dd], i, Elem<T>::store((typename Elem<T>::acc)(FP8 ? acc * post_inv : acc)));
     }
   }
+}
+
+// The (K, pattern) combinations the planner emits (validate_typed_patterns): fp8 wire = quantising push
+// (K 1, SP_T), reduction (K >= 2, SP_TW), dequantising all-gather (K 1, SP_W); fp32 partials = tree
+// stage 0 (SP_T), ring step (K 2, SP_TW), final stage / temp chains (SP_W). Anything else is reported
+// as a protocol error instead of being computed wrongly.
+template <typename T, typename W, int K, int PM>
+__device__ FX_INLINE bool xfer_mx_k(int sp, const char* const (&s)[kMaxSrc], char* const (&d)[kMaxDst], int nd,
+                                    uint32_t dm, uint64_t n, float scale, float pre, float post_inv, bool vec) {
+  constexpr bool FP8 = sizeof(W) == 1;
+  if (sp == SP_T && (FP8 ? K == 1 : K >= 2)) {
+    if constexpr (FP8 ? K == 1 : K >= 2) xfer_mx<T, W, K, SP_T, PM>(s, d, nd, dm, n, scale, pre, post_inv, vec);
+    return true;
+  }
+  if (sp == SP_TW && K >= 2 && (FP8 || K == 2)) {
+    if constexpr (K >= 2 && (FP8 || K == 2)) xfer_mx<T, W, K, SP_TW, PM>(s, d, nd, dm, n, scale, pre, post_inv, vec);
+    return true;
+  }
+  if (sp == SP_W && (FP8 ? K == 1 : K >= 2)) {
+    if constexpr (FP8 ? K == 1 : K >= 2) xfer_mx<T, W, K, SP_W, PM>(s, d, nd, dm, n, scale, pre, post_inv, vec);
+    return true;
+  }
+  return false;
 }
 
 // Typed op: operand addresses (STG offsets in units, element slice [lo, hi) in each operand's own
@@ -497,16 +604,20 @@ __device__ FX_INLINE void xfer_op_typed(const DevCtx& c, const Op* o, uint32_t l
     xfer_dispatch<T, OpSum, PM>(ns, s, d, nd, n, o->scale, vec);
     return;
   }
+  const int sp = sm == 0 ? SP_T : (sm == (all_s & ~1u) ? SP_TW : (sm == all_s ? SP_W : -1));
+  bool ok = false;
   switch (ns) {
-    case 1: xfer_mx<T, W, 1, PM>(s, sm, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-    case 2: xfer_mx<T, W, 2, PM>(s, sm, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-    case 3: xfer_mx<T, W, 3, PM>(s, sm, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-    case 4: xfer_mx<T, W, 4, PM>(s, sm, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-    case 5: xfer_mx<T, W, 5, PM>(s, sm, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-    case 6: xfer_mx<T, W, 6, PM>(s, sm, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-    case 7: xfer_mx<T, W, 7, PM>(s, sm, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-    default: xfer_mx<T, W, 8, PM>(s, sm, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    case 1: ok = xfer_mx_k<T, W, 1, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    case 2: ok = xfer_mx_k<T, W, 2, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    case 3: ok = xfer_mx_k<T, W, 3, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    case 4: ok = xfer_mx_k<T, W, 4, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    case 5: ok = xfer_mx_k<T, W, 5, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    case 6: ok = xfer_mx_k<T, W, 6, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    case 7: ok = xfer_mx_k<T, W, 7, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    default: ok = xfer_mx_k<T, W, 8, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
   }
+  if (!ok && threadIdx.x == 0)  // unreachable for validated programs: fail loudly, never compute wrongly
+    __hip_atomic_store(c.err, (uint32_t)(0x40000000u | (0xfdu << 8)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // fp8 wire prologue: every workgroup derives the call's pre-scale s = fp8_max / (N * global amax).
@@ -542,8 +653,12 @@ __device__ FX_INLINE bool fp8_scale(const DevCtx& c, uint32_t b, uint64_t epoch,
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) g = __builtin_fmaxf(g, __shfl_xor(g, off, 64));
+  // s = fp8_max / (N * amax * (1 + h)), h = the fp8 type's largest relative rounding step (2^-4 e4m3,
+  // 2^-3 e5m2): each quantised contribution is at most fp8_max / N * (1 + h) / (1 + h), so the N-term sum
+  // (and every rounding of it) stays within fp8_max and the packed converters need no saturation
   const float wmax = (float)Elem<W>::load(Elem<W>::store(1e30f));  // saturating encode: the type's max
-  *s_out = (g > 0.0f && g < 3.0e38f) ? wmax / ((float)c.nranks * g) : 1.0f;
+  const float head = IsFp8<W>::e4m3 ? 1.0625f : 1.125f;
+  *s_out = (g > 0.0f && g < 3.0e38f) ? wmax / ((float)c.nranks * g * head) : 1.0f;
   return __all(ok) != 0;
 }
 

@@ -1,0 +1,6 @@
+// Typed executors, fp32 partial sums for bf16 inputs ("+f32": ring / tree schedules round once).
+#include "kernels_impl.hpp"
+
+namespace flexar {
+int launch_mx_acc_bf16(const LaunchArgs& a) { return launch_typed<bf16_t, float>(a); }
+}  // namespace flexar

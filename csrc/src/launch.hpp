@@ -37,16 +37,22 @@ struct LaunchArgs {
 // Typed-program executors (exec_mx_kernel), SUM/AVG only: fp32 partials for 16/8-bit dtypes
 // (k_mx_acc*.hip) and an fp8 wire for 32/16-bit floats (k_mx_wire_*.hip), one translation unit per
 // input dtype so the gfx950 build parallelises.
-int launch_mx_acc16(int dtype, const LaunchArgs& a);  // bf16, fp16 -> fp32 partials
-int launch_mx_acc8(int dtype, const LaunchArgs& a);   // e4m3, e5m2 -> fp32 partials
+int launch_mx_acc_bf16(const LaunchArgs& a);  // 16/8-bit dtypes with fp32 partials
+int launch_mx_acc_f16(const LaunchArgs& a);
+int launch_mx_acc_e4m3(const LaunchArgs& a);
+int launch_mx_acc_e5m2(const LaunchArgs& a);
 int launch_mx_wire_f32(const LaunchArgs& a);          // fp32 over e4m3 / e5m2 (a.wire)
 int launch_mx_wire_bf16(const LaunchArgs& a);
 int launch_mx_wire_f16(const LaunchArgs& a);
 inline int launch_mx(int dtype, const LaunchArgs& a) {
   if (a.wire == 1) {
-    if (dtype == FLEXAR_BFLOAT16 || dtype == FLEXAR_FLOAT16) return launch_mx_acc16(dtype, a);
-    if (dtype == FLEXAR_FP8_E4M3 || dtype == FLEXAR_FP8_E5M2) return launch_mx_acc8(dtype, a);
-    return FLEXAR_ERR_UNSUPPORTED;
+    switch (dtype) {
+      case FLEXAR_BFLOAT16: return launch_mx_acc_bf16(a);
+      case FLEXAR_FLOAT16: return launch_mx_acc_f16(a);
+      case FLEXAR_FP8_E4M3: return launch_mx_acc_e4m3(a);
+      case FLEXAR_FP8_E5M2: return launch_mx_acc_e5m2(a);
+      default: return FLEXAR_ERR_UNSUPPORTED;
+    }
   }
   switch (dtype) {
     case FLEXAR_FLOAT32: return launch_mx_wire_f32(a);

@@ -206,7 +206,7 @@ def test_group_fp8_wire_fused_scale(cuda, groups, n, dtype, op):
     g = torch.Generator(device=cuda).manual_seed(31 + n)
     xs = [(torch.randn(1000003, device=cuda, generator=g) * (r + 1)).to(dtype) for r in range(n)]
     amax = max(float(x.float().abs().max()) for x in xs)
-    s = 448.0 / (n * amax)
+    s = 448.0 / (n * amax * 1.0625)  # e4m3 headroom (device_exec.hpp fp8_scale): the sum never saturates
     want = _emulate_fp8_flat(xs, s, op)
     ref = torch.stack([x.double() for x in xs]).sum(0) / (n if op == "avg" else 1)
     for _ in range(3):  # parities; the amax granules are epoch-tagged
@@ -218,7 +218,7 @@ def test_group_fp8_wire_fused_scale(cuda, groups, n, dtype, op):
         mism = (~torch.isclose(outs[0].float(), want.float(), rtol=1e-5, atol=0)).float().mean().item()
         assert mism < 2e-3, mism
         rel = ((outs[0].double() - ref).abs().max() / ref.abs().max()).item()
-        assert rel < 0.07, rel
+        assert rel < 0.1, rel  # e4m3: half-ulp 2^-4 of the result + the quantised contributions
     grp.check()
 
 
