@@ -205,7 +205,8 @@ void* flexar_device_alloc(size_t bytes);
 void flexar_device_free(void* p);
 
 /* Kernel facts for a (dtype, op) instantiation: kind 0 = executor (proto 0 fence, 1 +nts, 2 +wt),
- * 1 = LL, 2 = standalone reduce. Writes workgroups resident per CU (512 threads) and VGPRs. */
+ * 1 = LL, 2 = standalone reduce, 3/4/5 = typed executor with fp32 partials / e4m3 wire / e5m2 wire.
+ * Writes workgroups resident per CU (512 threads) and VGPRs. */
 int flexar_kernel_info(int dtype, int op, int kind, int proto, int* blocks_per_cu, int* vgprs);
 
 /* ---- host-only planning utilities (no GPU needed) ------------------------ */

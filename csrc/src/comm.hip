@@ -1743,10 +1743,11 @@ void* flexar_device_alloc(size_t bytes) {
 void flexar_device_free(void* p) { (void)hipFree(p); }
 
 int flexar_kernel_info(int dtype, int op, int kind, int proto, int* blocks_per_cu, int* vgprs) {
-  if (kind < 0 || kind > 2 || proto < 0 || proto > 2) { set_error("bad kernel_info arguments"); return FLEXAR_ERR_INVALID; }
+  if (kind < 0 || kind > 5 || proto < 0 || proto > 2) { set_error("bad kernel_info arguments"); return FLEXAR_ERR_INVALID; }
   LaunchArgs la;
   la.kind = LAUNCH_QUERY;
-  la.query = kind;
+  la.query = kind > 2 ? 0 : kind;
+  la.wire = kind > 2 ? kind - 2 : 0;  // typed executors: 3 = fp32 partials, 4 = e4m3 wire, 5 = e5m2 wire
   la.proto = proto;
   la.occ_out = blocks_per_cu;
   la.regs_out = vgprs;
