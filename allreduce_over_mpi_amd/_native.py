@@ -88,6 +88,8 @@ def _sig(lib):
         "flexar_comm_disabled": (u32, [vp]),
         "flexar_comm_topology": (i, [vp, cp, sz]),
         "flexar_comm_predict_us": (d, [vp, cp, d]),
+        "flexar_comm_set_model": (i, [vp, d, d, d, d, i]),
+        "flexar_model_features": (i, [cp, i, d, i, c.POINTER(d)]),
         "flexar_kernel_info": (i, [i, i, i, i, c.POINTER(i), c.POINTER(i)]),
         "flexar_downgrade_spec": (i, [cp, i, u32, i, cp, sz]),
         "flexar_direct_links": (i, [c.POINTER(c.c_int32), c.POINTER(c.c_int32), i, i]),
@@ -204,6 +206,17 @@ def model_cost_us(spec: str, nranks: int, nbytes: float) -> float:
     if v < 0:
         raise FlexarError(1, last_error())
     return v
+
+
+def model_features(spec: str, nranks: int, nbytes: float, links: int = 0):
+    """Linear cost features of ``spec``: cost_us = f . (alpha_launch, alpha_sync, 1/link_gbps, 1/hbm_gbps);
+    None for schedules outside the linear model (copy engines, LL above its size cap)."""
+    out = (ctypes.c_double * 4)()
+    rc = lib().flexar_model_features(spec.encode(), nranks, float(nbytes), int(links), out)
+    if rc == 2:
+        return None
+    check(rc, "model_features")
+    return list(out)
 
 
 def select_plan(nranks: int, nbytes: float) -> str:

@@ -44,9 +44,13 @@ def default_candidates(world: int, nbytes: int) -> list[str]:
 
 
 def autotune(comm, sizes: Optional[Sequence[int]] = None, dtype=None, candidates=None, iters: int = 0,
-             install: bool = True, verbose: bool = False) -> list[tuple[int, str, float]]:
+             install: bool = True, verbose: bool = False, calibrate: bool = True,
+             rows_out: Optional[list] = None) -> list[tuple[int, str, float]]:
     """Measure and (``install``) apply a per-size algorithm table. Returns [(bytes, spec, busbw_GBps)].
-    ``sizes``: buffer bytes (default 4 KiB .. 256 MiB, x4). Collective over the communicator's group."""
+    ``sizes``: buffer bytes (default 4 KiB .. 256 MiB, x4). Collective over the communicator's group.
+    ``calibrate``: also fit the cost model to every measurement (``Communicator.calibrate``), so sizes
+    between and beyond the measured ones are priced with this node's constants; ``rows_out`` collects the
+    (spec, bytes, us) rows (max over ranks)."""
     import torch
     import torch.distributed as dist
 
@@ -67,7 +71,7 @@ def autotune(comm, sizes: Optional[Sequence[int]] = None, dtype=None, candidates
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
         return float(t.item())
 
-    table = []
+    table, rows = [], []
     tol = {torch.float32: 1e-5, torch.bfloat16: 2e-2, torch.float16: 4e-3}.get(dtype, 1e-5) * 4 * math.sqrt(world)
     for nbytes in sizes:
         n = max(1, nbytes // es)
@@ -107,6 +111,7 @@ def autotune(comm, sizes: Optional[Sequence[int]] = None, dtype=None, candidates
                     print(f"[autotune] {n * es:>11d} B  {spec:16s} excluded (wrong or failed on a rank)", flush=True)
                 continue
             t = agree_max(t)
+            rows.append({"spec": spec, "bytes": n * es, "us": t * 1e6})
             if verbose and comm.rank == 0:
                 print(f"[autotune] {n * es:>11d} B  {spec:16s} {t * 1e6:10.2f} us  "
                       f"busbw {busbw_gbps(n * es, t, world):8.1f} GB/s", flush=True)
@@ -122,4 +127,14 @@ def autotune(comm, sizes: Optional[Sequence[int]] = None, dtype=None, candidates
                 lines.append(f"{world} {nbytes} {spec}")
                 prev = spec
         comm.set_tune_table("\n".join(lines))
+    if calibrate and install and hasattr(comm, "calibrate"):
+        try:
+            fit = comm.calibrate(rows)  # identical rows on every rank (max over ranks): identical model
+            if verbose and comm.rank == 0:
+                print(f"[autotune] cost model fitted: FLEXAR_MODEL={fit['FLEXAR_MODEL']} "
+                      f"(median rel err {fit['median_rel_err']:.2f})", flush=True)
+        except ValueError:
+            pass  # too few executor measurements to fit 4 parameters
+    if rows_out is not None:
+        rows_out.extend(rows)
     return table

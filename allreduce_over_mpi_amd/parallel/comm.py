@@ -181,6 +181,19 @@ class Communicator:
             raise nv.FlexarError(1, nv.last_error())
         return float(v)
 
+    def calibrate(self, rows, install: bool = True) -> dict:
+        """Fit the cost model to measured rows ({"spec", "bytes", "us"}: ``autotune``'s or
+        tools/flexar_tune.py's) on this node's probed link count, and install it (every rank must pass the
+        same rows, e.g. max-over-ranks timings). Returns the fit (utils/costfit.py)."""
+        from ..utils.costfit import fit_model
+
+        links = int(self.topology().get("links", 0)) if self.world_size > 1 else 0
+        fit = fit_model(rows, self.world_size, links)
+        if install:
+            nv.check(self._lib.flexar_comm_set_model(self._h, fit["alpha_launch_us"], fit["alpha_sync_us"],
+                                                     fit["link_gbps"], fit["hbm_gbps"], links), "set_model")
+        return fit
+
     # ------------------------------------------------------------------ config
     def set_algo(self, spec: str):
         """Default algorithm spec (see README); ``"rccl"`` routes allreduces to RCCL (comparator / fallback)."""

@@ -69,38 +69,52 @@ struct XgmiModel {
   }
   double reduce_us(double bytes_read) const { return bytes_read / (hbm_gbps * 1e3); }
 
-  double cost_us(const AlgoSpec& s, int N, double S) const {
-    if (N <= 1) return alpha_launch_us + reduce_us(2 * S);
+  // The executor schedules' cost is linear in theta = (alpha_launch_us, alpha_sync_us, 1 / link_gbps,
+  // 1 / hbm_gbps): cost_us = f . theta with f = (launches, hand-offs, link bytes / (1e3 * link share),
+  // HBM bytes / 1e3). features() returns f (false for the copy-engine path and out-of-range LL, which
+  // have their own terms); costfit.py fits theta to measured (spec, bytes, us) rows by least squares.
+  bool features(const AlgoSpec& s, int N, double S, double f[4]) const {
+    auto share = [&](int fan) { return fan <= links ? 1.0 : (double)links / fan; };
+    f[0] = 1.0; f[1] = f[2] = f[3] = 0.0;
+    if (N <= 1) { f[3] = 2 * S / 1e3; return true; }
     switch (s.kind) {
       case AlgoKind::ONESHOT:
-        return alpha_launch_us + alpha_sync_us + fanout_us(S, N - 1) + reduce_us(N * S);
+        f[1] = 1.0; f[2] = S / (1e3 * share(N - 1)); f[3] = N * S / 1e3;
+        return true;
       case AlgoKind::LL:  // flag-free 8-B {data, epoch} granules: half the hop cost, 2x the bytes
-        if (S > kLLMaxBytes) return 1e30;
-        return alpha_launch_us + 0.5 * alpha_sync_us + fanout_us(2 * S, N - 1) + reduce_us(2 * N * S);
-      case AlgoKind::RING: {
-        int C = s.channels < 1 ? 1 : s.channels;
-        double blk = S / ((double)C * N);
-        double step = alpha_sync_us + fanout_us(blk, 1) + reduce_us(2 * blk);
-        // C rings run concurrently on distinct links; a step's hop latency overlaps across grid blocks
-        return alpha_launch_us + 2.0 * (N - 1) * step;
+        if (S > kLLMaxBytes) return false;
+        f[1] = 0.5; f[2] = 2 * S / (1e3 * share(N - 1)); f[3] = 2 * N * S / 1e3;
+        return true;
+      case AlgoKind::RING: {  // C rings on distinct links; 2 (N - 1) steps of S / (C N) bytes
+        const int C = s.channels < 1 ? 1 : s.channels;
+        const double blk = S / ((double)C * N);
+        f[1] = 2.0 * (N - 1); f[2] = 2.0 * (N - 1) * blk / 1e3; f[3] = 2.0 * (N - 1) * 2 * blk / 1e3;
+        return true;
       }
       case AlgoKind::TREE: {
-        double t = alpha_launch_us, G = 1;
+        double G = 1;
         for (int w : s.widths) {
           G *= w;
-          double per_peer = S / G;
-          double stage = alpha_sync_us + fanout_us(per_peer, w - 1) + reduce_us(w * per_peer);
-          t += 2.0 * stage;
+          const double per_peer = S / G;
+          f[1] += 2.0;
+          f[2] += 2.0 * per_peer / (1e3 * share(w - 1));
+          f[3] += 2.0 * w * per_peer / 1e3;
         }
-        if (s.ag == AgMode::PUSH || s.ag == AgMode::AUTO) t += reduce_us(S);  // local copy-out of pushed blocks
-        return t;
+        if (s.ag == AgMode::PUSH || s.ag == AgMode::AUTO) f[3] += S / 1e3;  // local copy-out of pushed blocks
+        return true;
       }
-      case AlgoKind::DMA:  // copy engines: CU-free, but a host-enqueued fork/join and 2 stream-memory hand-offs
-        return alpha_launch_us + 2.0 * alpha_dma_us + 2.0 * fanout_us_at(S / N, N - 1, dma_link_gbps) +
-               reduce_us(S);
       default:
-        return 1e30;
+        return false;
     }
+  }
+
+  double cost_us(const AlgoSpec& s, int N, double S) const {
+    double f[4];
+    if (features(s, N, S, f))
+      return f[0] * alpha_launch_us + f[1] * alpha_sync_us + f[2] / link_gbps + f[3] / hbm_gbps;
+    if (s.kind == AlgoKind::DMA)  // copy engines: CU-free, but a host-enqueued fork/join and 2 stream-memory hand-offs
+      return alpha_launch_us + 2.0 * alpha_dma_us + 2.0 * fanout_us_at(S / N, N - 1, dma_link_gbps) + reduce_us(S);
+    return 1e30;
   }
 };
 

@@ -155,6 +155,10 @@ uint32_t flexar_comm_disabled(flexar_comm_t comm);
 int flexar_comm_topology(flexar_comm_t comm, char* buf, size_t buflen);
 /* Cost-model estimate (us) of spec ("auto" = the model's own choice) on this communicator's model. */
 double flexar_comm_predict_us(flexar_comm_t comm, const char* spec, double bytes);
+/* Install fitted cost-model parameters on this communicator (auto selection then uses them; links from
+ * the connect-time probe unless links > 0). Collective in effect: every rank must install the same. */
+int flexar_comm_set_model(flexar_comm_t comm, double alpha_launch_us, double alpha_sync_us, double link_gbps,
+                          double hbm_gbps, int links);
 /* JSON statistics (calls, bytes; per-algorithm device time when FLEXAR_PROFILE=1). */
 int flexar_comm_stats(flexar_comm_t comm, char* buf, size_t buflen);
 /* Describe the algorithm the communicator would run for (count, dtype). */
@@ -225,6 +229,9 @@ uint64_t flexar_count_factorizations(int n);
 int flexar_enumerate_plans(int nranks, char* out, size_t outlen);
 /* Cost-model estimate (microseconds) of spec for (nranks, bytes). */
 double flexar_model_cost_us(const char* spec, int nranks, double bytes);
+/* Linear cost features of spec (see XgmiModel::features): 4 doubles, cost = f . (alpha_launch_us,
+ * alpha_sync_us, 1/link_gbps, 1/hbm_gbps). links <= 0: the model's default link count. */
+int flexar_model_features(const char* spec, int nranks, double bytes, int links, double* out);
 /* Cost-model choice for (nranks, bytes) written to out. */
 int flexar_select_plan(int nranks, double bytes, char* out, size_t outlen);
 /* Reference cost model (cost_model/CostModel.h) score, fixed: returns the argmin spec and cost. */

@@ -1,7 +1,10 @@
 // Timers (reference cost_model/timer.h:1-134: a std::chrono stopwatch in ms/us/ns/s).
-// HostTimer: steady_clock stopwatch. DeviceTimer (HIP translation units only): hipEvent pair
-// timing the work enqueued on a stream between start() and stop().
+// HostTimer: steady_clock stopwatch (bench/flexar_bench.cpp host-path timing). DeviceTimer: a hipEvent
+// pair timing the work enqueued on a stream between start() and stop(); the FLEXAR_PROFILE per-call
+// records of the communicator (comm.hip ProfRec) are DeviceTimers resolved by flexar_comm_stats.
 #pragma once
+
+#include <hip/hip_runtime_api.h>
 
 #include <chrono>
 
@@ -20,32 +23,30 @@ class HostTimer {
   std::chrono::steady_clock::time_point t0_;
 };
 
-#if defined(__HIP_PLATFORM_AMD__) || defined(__HIPCC__)
-}  // namespace flexar
-#include <hip/hip_runtime.h>
-namespace flexar {
 class DeviceTimer {
  public:
   DeviceTimer() {
-    (void)hipEventCreate(&a_);
-    (void)hipEventCreate(&b_);
+    if (hipEventCreate(&a_) != hipSuccess || hipEventCreate(&b_) != hipSuccess) ok_ = false;
   }
   ~DeviceTimer() {
-    (void)hipEventDestroy(a_);
-    (void)hipEventDestroy(b_);
+    if (a_) (void)hipEventDestroy(a_);
+    if (b_) (void)hipEventDestroy(b_);
   }
-  void start(hipStream_t s = nullptr) { (void)hipEventRecord(a_, s); }
-  void stop(hipStream_t s = nullptr) { (void)hipEventRecord(b_, s); }
-  double ms() {  // synchronises on the stop event
+  DeviceTimer(const DeviceTimer&) = delete;
+  DeviceTimer& operator=(const DeviceTimer&) = delete;
+  bool ok() const { return ok_; }
+  void start(hipStream_t s = nullptr) { ok_ = ok_ && hipEventRecord(a_, s) == hipSuccess; }
+  void stop(hipStream_t s = nullptr) { ok_ = ok_ && hipEventRecord(b_, s) == hipSuccess; }
+  // synchronises on the stop event; < 0 if an event could not be created / recorded
+  double ms() {
     float m = 0;
-    (void)hipEventSynchronize(b_);
-    (void)hipEventElapsedTime(&m, a_, b_);
+    if (!ok_ || hipEventSynchronize(b_) != hipSuccess || hipEventElapsedTime(&m, a_, b_) != hipSuccess) return -1.0;
     return m;
   }
 
  private:
-  hipEvent_t a_, b_;
+  hipEvent_t a_ = nullptr, b_ = nullptr;
+  bool ok_ = true;
 };
-#endif
 
 }  // namespace flexar

@@ -167,6 +167,19 @@ double flexar_model_cost_us(const char* spec, int nranks, double bytes) {
   return XgmiModel::from_env().cost_us(s, nranks, bytes);
 }
 
+// Cost-model feature vector of (spec, nranks, bytes) under `links` concurrent links (<= 0: FLEXAR_MODEL /
+// default): cost_us = out[0] alpha_launch + out[1] alpha_sync + out[2] / link_gbps + out[3] / hbm_gbps.
+int flexar_model_features(const char* spec, int nranks, double bytes, int links, double* out) {
+  if (!out || nranks < 1) { set_error("bad arguments"); return FLEXAR_ERR_INVALID; }
+  AlgoSpec s;
+  std::string err;
+  if (!spec_for(spec, nranks, bytes, &s, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  XgmiModel m = XgmiModel::from_env();
+  if (links > 0) m.links = links;
+  if (!m.features(s, nranks, bytes, out)) { set_error("no linear cost features for " + s.str()); return FLEXAR_ERR_UNSUPPORTED; }
+  return 0;
+}
+
 int flexar_select_plan(int nranks, double bytes, char* out, size_t outlen) {
   if (nranks < 1) return FLEXAR_ERR_INVALID;
   return copy_out(select_plan(XgmiModel::from_env(), nranks, bytes).str(), out, outlen);

@@ -32,6 +32,7 @@
 #include "flexar/log.hpp"
 #include "flexar/planner.hpp"
 #include "flexar/readiness.hpp"
+#include "flexar/timer.hpp"
 #include "internal.hpp"
 
 namespace flexar {
@@ -94,7 +95,7 @@ static Roctx& roctx() {
 struct ProfRec {
   std::string algo;
   uint64_t bytes;
-  hipEvent_t a, b;
+  std::unique_ptr<DeviceTimer> t;
 };
 
 static uint64_t env_u64(const char* name, uint64_t dflt) {
@@ -1031,6 +1032,22 @@ double flexar_comm_predict_us(flexar_comm_t c, const char* spec, double bytes) {
   return c->model.cost_us(s, c->nranks, bytes);
 }
 
+int flexar_comm_set_model(flexar_comm_t c, double alpha_launch_us, double alpha_sync_us, double link_gbps,
+                          double hbm_gbps, int links) {
+  if (!c || !(link_gbps > 0) || !(hbm_gbps > 0) || alpha_launch_us < 0 || alpha_sync_us < 0) {
+    set_error("cost model: positive bandwidths and non-negative latencies required");
+    return FLEXAR_ERR_INVALID;
+  }
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->model.alpha_launch_us = alpha_launch_us;
+  c->model.alpha_sync_us = alpha_sync_us;
+  c->model.link_gbps = link_gbps;
+  c->model.hbm_gbps = hbm_gbps;
+  if (links > 0) c->model.links = links;
+  c->memo_gen++;
+  return 0;
+}
+
 int flexar_comm_set_disabled(flexar_comm_t c, uint32_t families) {
   if (!c) return FLEXAR_ERR_INVALID;
   std::lock_guard<std::mutex> lk(c->mu);
@@ -1268,12 +1285,8 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     la.stream = st;
     la.proto = proto_of(s);
     la.wire = dp->prog.wire;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    if (c->profile) {
-      FX_HIP(hipEventCreate(&ev0));
-      FX_HIP(hipEventCreate(&ev1));
-      FX_HIP(hipEventRecord(ev0, st));
-    }
+    std::unique_ptr<DeviceTimer> tm(c->profile ? new DeviceTimer : nullptr);
+    if (tm) tm->start(st);
     c->calls++;
     c->bytes += count * es;
     rc = launch_dtype(dtype, op, la);
@@ -1281,20 +1294,16 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
       c->launches++;
       remember(piece, dp, la.grid);
     }
-    if (c->profile) {
-      (void)hipEventRecord(ev1, st);
-      c->prof_pending.push_back(ProfRec{sdesc, (uint64_t)count * es, ev0, ev1});
+    if (tm) {
+      tm->stop(st);
+      c->prof_pending.push_back(ProfRec{sdesc, (uint64_t)count * es, std::move(tm)});
     }
     if (roctx().pop) roctx().pop();
     return rc;
   }
   remember(piece, nullptr, 0);
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  if (c->profile) {
-    FX_HIP(hipEventCreate(&ev0));
-    FX_HIP(hipEventCreate(&ev1));
-    FX_HIP(hipEventRecord(ev0, st));
-  }
+  std::unique_ptr<DeviceTimer> tm(c->profile ? new DeviceTimer : nullptr);
+  if (tm) tm->start(st);
   c->calls++;
   c->bytes += count * es;
   for (uint64_t off = 0; off < count; off += piece) {
@@ -1315,9 +1324,9 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     if (rc) break;
     c->launches++;
   }
-  if (c->profile) {
-    (void)hipEventRecord(ev1, st);
-    c->prof_pending.push_back(ProfRec{sdesc, (uint64_t)count * es, ev0, ev1});
+  if (tm) {
+    tm->stop(st);
+    c->prof_pending.push_back(ProfRec{sdesc, (uint64_t)count * es, std::move(tm)});
   }
   if (roctx().pop) roctx().pop();
   return rc;
@@ -1328,15 +1337,13 @@ int flexar_comm_stats(flexar_comm_t c, char* buf, size_t buflen) {
   if (!c || !buf) return FLEXAR_ERR_INVALID;
   std::lock_guard<std::mutex> lk(c->mu);
   for (auto& p : c->prof_pending) {
-    float ms = 0;
-    if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+    const double ms = p.t->ms();
+    if (ms >= 0) {
       auto& a = c->prof[p.algo];
       a.calls++;
       a.bytes += p.bytes;
       a.ms += ms;
     }
-    (void)hipEventDestroy(p.a);
-    (void)hipEventDestroy(p.b);
   }
   c->prof_pending.clear();
   std::string j = "{\"calls\": " + std::to_string(c->calls) + ", \"bytes\": " + std::to_string(c->bytes) +

@@ -12,6 +12,13 @@ lines "nranks bytes spec" (cost_model.hpp TuneTable: a row covers sizes >= bytes
     FLEXAR_TUNE_FILE=tune_mi355x_8.txt python train.py ...
 
 FLEXAR_BENCH_SHARED_GPU=1 rehearses it with every rank on device 0 (gloo bootstrap).
+
+The same measurements calibrate the cost model: every run also fits the model's
+(alpha_launch, alpha_sync, link_gbps, hbm_gbps) to the rows (utils/costfit.py) and prints FLEXAR_MODEL, and
+
+    python tools/flexar_tune.py --fit rows.jsonl --nranks 4        # offline, no GPU
+
+fits a saved --jsonl file.
 """
 from __future__ import annotations
 
@@ -45,7 +52,17 @@ def main():
     ap.add_argument("--iters", type=int, default=0, help="timed calls per candidate (0 = by size)")
     ap.add_argument("--out", default="flexar_tune.txt")
     ap.add_argument("--jsonl", default="", help="also write every measurement as JSON lines")
+    ap.add_argument("--fit", default="", help="offline: fit the cost model to this --jsonl file and exit")
+    ap.add_argument("--nranks", type=int, default=0, help="--fit: world size of the rows (default: n_gpus field)")
+    ap.add_argument("--links", type=int, default=0, help="--fit: concurrent links per GPU (0: the model default)")
     args = ap.parse_args()
+    if args.fit:
+        from allreduce_over_mpi_amd.utils.costfit import fit_model
+
+        rows = [json.loads(line) for line in open(args.fit) if line.strip()]
+        n = args.nranks or int(rows[0].get("n_gpus", 0))
+        print(json.dumps(fit_model(rows, n, args.links)))
+        return
 
     import torch
     import torch.distributed as dist
@@ -149,7 +166,14 @@ def main():
             with open(args.jsonl, "w") as f:
                 for r in rows:
                     f.write(json.dumps(r) + "\n")
-        print(json.dumps({"tune_file": args.out, "rows": len(table)}), flush=True)
+        from allreduce_over_mpi_amd.utils.costfit import fit_model
+
+        try:
+            fit = fit_model(rows, world, int(comm.topology().get("links", 0)))
+            fit.pop("sizes")
+        except ValueError as e:
+            fit = {"error": str(e)}
+        print(json.dumps({"tune_file": args.out, "rows": len(table), "model_fit": fit}), flush=True)
     comm.close()
     dist.destroy_process_group()
 
