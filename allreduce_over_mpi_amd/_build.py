@@ -101,16 +101,34 @@ def build(verbose: bool = False, force: bool = False) -> str:
     common = ["-O3", "-fPIC", "-std=c++17", "-I" + INCLUDE, "-Wall", "-Wno-unused-function"]
     jobs = []
     objs = []
+
+    def stale(src, obj):
+        # an object is rebuilt when its source or a header it included (compiler -MMD list) is newer
+        dep = obj + ".d"
+        if force or not os.path.exists(obj) or not os.path.exists(dep):
+            return True
+        t = os.path.getmtime(obj)
+        with open(dep) as f:
+            files = f.read().replace("\\\n", " ").split(":", 1)[-1].split()
+        return any(not os.path.exists(x) or os.path.getmtime(x) > t for x in [src] + files)
+
     for s in hip:
         o = os.path.join(BUILD_DIR, os.path.basename(s) + ".o")
         objs.append(o)
-        jobs.append([_hipcc(), "--offload-arch=" + ARCH, "-munsafe-fp-atomics", *common, *EXTRA_CFLAGS, "-c", s, "-o", o])
+        if stale(s, o):
+            jobs.append([_hipcc(), "--offload-arch=" + ARCH, "-munsafe-fp-atomics", *common, *EXTRA_CFLAGS, "-MMD", "-MF",
+                         o + ".d", "-c", s, "-o", o])
     cxx = os.environ.get("CXX", "g++")
     for s in cpp:
         o = os.path.join(BUILD_DIR, os.path.basename(s) + ".o")
         objs.append(o)
-        jobs.append([cxx, *common, "-march=x86-64-v2", "-c", s, "-o", o])
-    nproc = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", "8"))))
+        if stale(s, o):
+            jobs.append([cxx, *common, "-march=x86-64-v2", "-MMD", "-MF", o + ".d", "-c", s, "-o", o])
+    # objects of sources that no longer exist must not be linked
+    objs = [o for o in objs if o]
+    nproc = max(1, min(max(1, len(jobs)), int(os.environ.get("MAX_JOBS", "8"))))
+    # the slowest translation units first: the typed executors dominate the build
+    jobs.sort(key=lambda j: 0 if "k_mx_" in j[-3] else 1)
     with cf.ThreadPoolExecutor(nproc) as ex:
         for out in ex.map(_run, jobs):
             if verbose and out.strip():

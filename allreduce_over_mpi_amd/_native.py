@@ -80,6 +80,8 @@ def _sig(lib):
         "flexar_group_broadcast": (i, [c.POINTER(vp), i, i, c.POINTER(vp), c.POINTER(vp), sz, i, vp, cp]),
         "flexar_simulate_bcast": (i, [cp, i, sz, i, i, c.POINTER(vp), c.POINTER(vp), i, i]),
         "flexar_simulate_typed": (i, [cp, i, sz, i, i, c.POINTER(vp), c.POINTER(vp), i, i, f, f]),
+        "flexar_simulate_msg": (i, [cp, i, sz, i, i, c.POINTER(vp), c.POINTER(vp), i, f]),
+        "flexar_msg_plan_dump": (i, [cp, i, i, sz, i, cp, sz]),
         "flexar_allreduce_fp8": (i, [vp, vp, vp, sz, i, i, vp, i, vp, cp]),
         "flexar_group_allreduce_fp8": (i, [c.POINTER(vp), i, c.POINTER(vp), c.POINTER(vp), sz, i, i, vp, i,
                                             c.POINTER(vp)]),
@@ -89,6 +91,10 @@ def _sig(lib):
         "flexar_comm_topology": (i, [vp, cp, sz]),
         "flexar_comm_predict_us": (d, [vp, cp, d]),
         "flexar_comm_set_model": (i, [vp, d, d, d, d, i]),
+        "flexar_rccl_available": (i, []),
+        "flexar_rccl_unique_id": (i, [vp, sz]),
+        "flexar_comm_init_msg": (i, [vp, vp]),
+        "flexar_comm_connect_msg_only": (i, [vp]),
         "flexar_model_features": (i, [cp, i, d, i, c.POINTER(d)]),
         "flexar_kernel_info": (i, [i, i, i, i, c.POINTER(i), c.POINTER(i)]),
         "flexar_downgrade_spec": (i, [cp, i, u32, i, cp, sz]),
@@ -237,7 +243,7 @@ def plan_dump(spec: str, rank: int, nranks: int, count: int, dtype="float32") ->
 
 
 # protocol families (csrc/include/flexar/readiness.hpp)
-FAMILIES = {"fence": 1, "wt": 2, "ll": 4, "dma": 8}
+FAMILIES = {"fence": 1, "wt": 2, "ll": 4, "dma": 8, "rccl": 16}
 
 
 def family_names(mask: int) -> list[str]:
@@ -333,6 +339,28 @@ def simulate_mx(spec: str, inputs, dtype: str, op="sum", grid=2, ncalls=2, scale
                                      grid, ncalls, float(scale), float(pre))
     check(rc, "simulate_typed")
     return outs
+
+
+def simulate_msg(spec: str, inputs, op="sum", ncalls=2, scale=1.0, dtype: str | None = None):
+    """Run the message-transport plans (send/recv + local executor segments, what the RCCL transport posts)
+    on host numpy arrays. Returns the per-rank outputs."""
+    import numpy as np
+
+    ins = [np.ascontiguousarray(x) for x in inputs]
+    outs = [np.empty_like(x) for x in ins]
+    code = DTYPES[dtype] if dtype else dtype_code(ins[0].dtype)
+    check(lib().flexar_simulate_msg(spec.encode(), len(ins), ins[0].size, code, op_code(op),
+                                    _ptr_array([x.ctypes.data for x in ins]), _ptr_array([o.ctypes.data for o in outs]),
+                                    ncalls, float(scale)), "simulate_msg")
+    return outs
+
+
+def msg_plan(spec: str, rank: int, nranks: int, count: int, dtype="float32") -> dict:
+    import json
+
+    b = _strbuf(1 << 20)
+    check(lib().flexar_msg_plan_dump(spec.encode(), rank, nranks, count, dtype_code(dtype), b, 1 << 20), "msg_plan")
+    return json.loads(b.value.decode())
 
 
 def reduce_host(srcs, op="sum", scale=1.0, dtype: str | None = None):

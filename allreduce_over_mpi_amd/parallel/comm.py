@@ -89,9 +89,15 @@ class Communicator:
 
     def __init__(self, group=None, device: Optional[int] = None, workspace_bytes: int = 0,
                  algo: Optional[str] = None, rank: Optional[int] = None, world_size: Optional[int] = None,
-                 exchange=None):
+                 exchange=None, transport: Optional[str] = None):
         """``exchange(bytes) -> list[bytes]`` all-gathers the handle bytes (default: torch.distributed
-        all_gather_object on ``group``; :func:`store_exchange` bootstraps from a c10d Store)."""
+        all_gather_object on ``group``; :func:`store_exchange` bootstraps from a c10d Store).
+
+        ``transport`` (default FLEXAR_TRANSPORT or "auto"): "ipc" = peer workspaces mapped over HIP IPC,
+        fail if that is impossible; "auto" = IPC, and if any rank cannot map its peers, every call runs
+        over the message transport (RCCL send/recv + local executor segments, csrc/include/flexar/
+        msg_plan.hpp) with the same FlexTree / ring / RHD schedules; "rccl" = IPC plus the message
+        transport (algorithm suffix "+rccl")."""
         import torch
         import torch.distributed as dist
 
@@ -112,6 +118,7 @@ class Communicator:
         self._h = h
         self._hi = int(h.value or 0)  # the handle as an int, for the fast-call path
         self.selftest_failed = []
+        self.transport_note = None
         if self.world_size > 1:
             hs = int(self._lib.flexar_handle_size())
             buf = ctypes.create_string_buffer(hs)
@@ -122,20 +129,46 @@ class Communicator:
                     dist.all_gather_object(gathered, data, group=group)
                     return gathered
             allb = b"".join(exchange(bytes(buf.raw)))
+            transport = transport or os.environ.get("FLEXAR_TRANSPORT", "auto")
+            if transport not in ("auto", "ipc", "rccl"):
+                raise nv.FlexarError(1, f"unknown transport {transport!r} (auto | ipc | rccl)")
             rc = self._lib.flexar_comm_connect(self._h, allb)
             # agreement round (also the barrier: everyone has mapped everyone before the first collective);
             # a rank that failed to map a peer must not leave the others waiting in a later collective
-            msg = b"" if rc == 0 else f"rank {self.rank}: {nv.last_error()}".encode()
+            msg = b"" if rc == 0 else f"{rc}:rank {self.rank}: {nv.last_error()}".encode()
             bad = [m.decode(errors="replace") for m in exchange(msg) if m]
-            if bad:
+            # only a failed peer mapping (HIP error) falls back; settings mismatches etc. stay errors
+            mapping_only = bool(bad) and all(b.split(":", 1)[0] == "3" for b in bad)
+            fallback = bool(bad) and transport == "auto" and mapping_only and self._lib.flexar_rccl_available()
+            if bad and not fallback:
                 self.close()
-                raise nv.FlexarError(rc or 5, "comm_connect: " + "; ".join(bad))
+                raise nv.FlexarError(rc or 5, "comm_connect: " + "; ".join(b.split(":", 1)[1] for b in bad))
+            if transport == "rccl" or fallback:
+                self._init_msg(exchange)
+                if fallback:
+                    nv.check(self._lib.flexar_comm_connect_msg_only(self._h), "connect_msg_only")
+                    self.transport_note = "IPC unavailable (" + "; ".join(b.split(":", 1)[1] for b in bad) + \
+                                          "): every call runs over the RCCL message transport"
             self._readiness(exchange)
         self._rccl_default = False
         self._rccl_group = None
         env_algo = os.environ.get("FLEXAR_ALGO", "")
         if algo or env_algo == "rccl":
             self.set_algo(algo or env_algo)
+
+    def _init_msg(self, exchange):
+        """Create the RCCL communicator of the message transport (collective): rank 0's unique id is
+        all-gathered through ``exchange``."""
+        uid = ctypes.create_string_buffer(128)
+        if self.rank == 0:
+            nv.check(self._lib.flexar_rccl_unique_id(uid, 128), "rccl_unique_id")
+        ids = exchange(bytes(uid.raw) if self.rank == 0 else b"")
+        rc = self._lib.flexar_comm_init_msg(self._h, ids[0])
+        bad = [m.decode(errors="replace") for m in exchange(b"" if rc == 0 else
+                                                            f"rank {self.rank}: {nv.last_error()}".encode()) if m]
+        if bad:
+            self.close()
+            raise nv.FlexarError(7, "message transport: " + "; ".join(bad))
 
     def _readiness(self, exchange):
         """Connect-time self-test (flexar_comm_selftest): every protocol family runs exact integer
@@ -162,7 +195,8 @@ class Communicator:
             nv.check(self._lib.flexar_comm_set_disabled(self._h, mask), "set_disabled")
             self.selftest_failed = nv.family_names(mask)
             exchange(b"")  # nobody issues a production call before every rank installed the mask
-            if mask == fam:
+            tested = sum(nv.FAMILIES[n] for n in self.topology()["selftested"].split(",") if n in nv.FAMILIES)
+            if tested & ~mask == 0:
                 self.close()
                 raise nv.FlexarError(2, "no device protocol passed the connect-time self-test on this node")
 

@@ -149,6 +149,12 @@ int flexar_comm_clear_error(flexar_comm_t comm);
  * fence -> +wt -> dma) or fail with FLEXAR_ERR_UNSUPPORTED when none is left. */
 int flexar_comm_selftest(flexar_comm_t comm, uint32_t families, uint32_t* failed_out);
 int flexar_comm_set_disabled(flexar_comm_t comm, uint32_t families);
+/* Message transport (RCCL ncclSend/ncclRecv + local executor segments; family 16): algorithm suffix "+rccl",
+ * or every call when IPC mapping is unavailable. RCCL is resolved at run time (the process's librccl). */
+int flexar_rccl_available(void);
+int flexar_rccl_unique_id(void* out, size_t len);                       /* rank 0; len >= 128 */
+int flexar_comm_init_msg(flexar_comm_t comm, const void* unique_id);    /* collective */
+int flexar_comm_connect_msg_only(flexar_comm_t comm);                   /* no IPC: all calls over RCCL */
 uint32_t flexar_comm_disabled(flexar_comm_t comm);
 /* JSON: per-peer PCI bus id, device ordinal, link class (same-device / xgmi / pcie / unknown) and hop
  * count from the connect-time probe; links used by the cost model; self-test state. */
@@ -251,6 +257,12 @@ int flexar_simulate(const char* spec, int nranks, size_t count, int dtype, int o
  * pre-scale `pre` given explicitly (the device derives it from the global amax). */
 int flexar_simulate_typed(const char* spec, int nranks, size_t count, int dtype, int op, const void* const* inputs,
                           void* const* outputs, int grid, int ncalls, float scale, float pre);
+/* Message-transport plans (msg_plan.hpp: the schedule as local executor segments + grouped send/recv,
+ * what the RCCL transport runs) on host memory through in-order per-pair mailboxes. */
+int flexar_simulate_msg(const char* spec, int nranks, size_t count, int dtype, int op, const void* const* inputs,
+                        void* const* outputs, int ncalls, float scale);
+/* JSON summary of rank's message plan: steps (executor ops / group sends+receives with peer, bytes, source). */
+int flexar_msg_plan_dump(const char* spec, int rank, int nranks, size_t count, int dtype, char* out, size_t outlen);
 /* Broadcast programs from `root` (inputs: root's source; outputs: every rank's destination). */
 int flexar_simulate_bcast(const char* spec, int nranks, size_t count, int dtype, int root, const void* const* inputs,
                           void* const* outputs, int grid, int ncalls);

@@ -43,6 +43,7 @@
 #include "flexar/cost_model.hpp"
 #include "flexar/flexar.h"
 #include "flexar/host_exec.hpp"
+#include "flexar/msg_plan.hpp"
 #include "flexar/planner.hpp"
 #include "flexar/readiness.hpp"
 
@@ -302,6 +303,7 @@ struct ShmRun {
 
 // Build the p2p message plan for rank h.rank: replay every peer's program to learn what it
 // writes into us and under which SIGNAL slot it publishes it.
+// The coalescing is the message transport's (msg_plan.hpp msg_regions): one message per (peer, SIGNAL).
 inline std::unique_ptr<P2PPlan> build_p2p(HostComm& h, const AlgoSpec& s, size_t count, size_t es, float fs) {
   std::unique_ptr<P2PPlan> pp(new P2PPlan);
   std::string err;
@@ -309,23 +311,16 @@ inline std::unique_ptr<P2PPlan> build_p2p(HostComm& h, const AlgoSpec& s, size_t
     Program Q;
     Planner pl(h.size, p, count, (uint32_t)es, fs);
     pl.build(s, &Q, &err);
-    std::map<int, std::vector<std::pair<uint64_t, uint64_t>>> pend;  // dst rank -> regions since its last signal
-    for (const Op& o : Q.ops) {
-      if (o.kind == OP_XFER) {
-        for (int d = 0; d < o.ndst; ++d)
-          if (o.dst[d].rank != (uint16_t)p) pend[o.dst[d].rank].push_back({o.dst[d].off, o.len});
-      } else if (o.kind == OP_SIGNAL) {
-        for (int k = 0; k < o.npeers; ++k) {
-          int q = o.peers[k];
-          uint64_t tot = 0;
-          for (auto& rg : pend[q]) tot += rg.second;
-          if (q == h.rank) {
-            pp->incoming[{p, o.slot}] = pend[q];
-            pp->incoming_elems[{p, o.slot}] = tot;
-          }
-          if (p == h.rank) pp->outgoing_elems[{q, o.slot}] = tot;
-          pend[q].clear();
+    for (int q = 0; q < h.size; ++q) {
+      if (q == p || (p != h.rank && q != h.rank)) continue;
+      for (const MsgRegions& m : msg_regions(Q, (uint32_t)p, (uint32_t)q)) {
+        uint64_t tot = 0;
+        for (auto& rg : m.regions) tot += rg.second;
+        if (q == h.rank) {
+          pp->incoming[{p, m.slot}] = m.regions;
+          pp->incoming_elems[{p, m.slot}] = tot;
         }
+        if (p == h.rank) pp->outgoing_elems[{q, m.slot}] = tot;
       }
     }
   }

@@ -27,10 +27,12 @@ enum : uint32_t {
   PF_WT = 2,     // executor, write-through payload ("+wt")
   PF_LL = 4,     // flag-free {data, epoch} granules ("ll")
   PF_DMA = 8,    // copy engines + stream-ordered flag writes ("dma")
-  PF_ALL = 15
+  PF_ALL = 15,
+  PF_MSG = 16    // message transport: RCCL send/recv + local executor segments ("+rccl")
 };
 
 inline uint32_t proto_family(const AlgoSpec& s) {
+  if (s.msg) return PF_MSG;
   switch (s.kind) {
     case AlgoKind::LL: return PF_LL;
     case AlgoKind::DMA: return PF_DMA;
@@ -39,9 +41,9 @@ inline uint32_t proto_family(const AlgoSpec& s) {
 }
 
 inline std::string family_names(uint32_t mask) {
-  static const char* n[] = {"fence", "wt", "ll", "dma"};
+  static const char* n[] = {"fence", "wt", "ll", "dma", "rccl"};
   std::string s;
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 5; ++i)
     if (mask & (1u << i)) s += (s.empty() ? "" : ",") + std::string(n[i]);
   return s.empty() ? "none" : s;
 }
@@ -51,12 +53,26 @@ inline std::string family_names(uint32_t mask) {
 //   fence -> the same schedule with "+wt"
 //   wt    -> dma (the flat exchange on the copy engines) when the spec is an allreduce schedule
 //   dma   -> flat+pull on the executor (fence, then wt)
+//   any IPC family -> the same schedule over the message transport when every IPC route is gone and
+//   the transport exists (allow_msg)
 // Returns false (and says why) when no verified family is left for this call.
-inline bool downgrade_spec(AlgoSpec* s, int nranks, uint32_t disabled, bool allow_dma, std::string* why) {
-  disabled &= PF_ALL;
+inline bool downgrade_spec(AlgoSpec* s, int nranks, uint32_t disabled, bool allow_dma, std::string* why,
+                           bool allow_msg = false) {
+  disabled &= PF_ALL | PF_MSG;
+  const AlgoSpec orig = *s;
   for (int hop = 0; hop < 6; ++hop) {
     const uint32_t f = proto_family(*s);
     if (!(disabled & f)) return true;
+    if (f == PF_MSG) break;
+    if (allow_msg && !(disabled & PF_MSG) && (disabled & (PF_FENCE | PF_WT)) == (PF_FENCE | PF_WT) &&
+        (!allow_dma || (disabled & PF_DMA))) {
+      *s = orig;  // every peer-memory route failed: same schedule, bytes over send/recv
+      s->msg = true;
+      s->wt = s->nts = false;
+      if (s->kind == AlgoKind::LL) s->kind = AlgoKind::ONESHOT;
+      if (s->kind == AlgoKind::DMA) *s = AlgoSpec(), s->kind = AlgoKind::TREE, s->widths = {nranks}, s->msg = true;
+      return true;
+    }
     switch (f) {
       case PF_LL: s->kind = AlgoKind::ONESHOT; break;
       case PF_FENCE: s->wt = true; s->nts = false; break;

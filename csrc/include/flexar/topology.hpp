@@ -44,6 +44,9 @@ struct AlgoSpec {
   // multi-hop 16/8-bit schedule out of the fp32 staging default.
   int wire = 0;
   bool round_wire = false;
+  // message transport ("+rccl"): the schedule's transfers as grouped ncclSend / ncclRecv between local
+  // executor segments (msg_plan.hpp) instead of peer-memory access over IPC
+  bool msg = false;
 
   std::string str() const {
     std::ostringstream ss;
@@ -67,6 +70,7 @@ struct AlgoSpec {
     if (wire == 2) ss << "+e4m3";
     if (wire == 3) ss << "+e5m2";
     if (round_wire) ss << "+rw";
+    if (msg) ss << "+rccl";
     return ss.str();
   }
 };
@@ -194,6 +198,7 @@ inline bool parse_algo(const std::string& raw, int nranks, AlgoSpec* spec, std::
     else if (mod == "e4m3" || mod == "fp8") spec->wire = 2;
     else if (mod == "e5m2") spec->wire = 3;
     else if (mod == "rw") spec->round_wire = true;
+    else if (mod == "rccl" || mod == "msg") spec->msg = true;
     else { if (err) *err = "unknown algorithm modifier '+" + mod + "'"; return false; }
   }
   std::string head = s, arg;
@@ -239,9 +244,11 @@ inline bool parse_algo(const std::string& raw, int nranks, AlgoSpec* spec, std::
   if (head == "ft") {
     const char* env = getenv("FT_TOPO");
     AgMode ag = spec->ag; bool fuse = spec->fuse, nts = spec->nts, wt = spec->wt, rw = spec->round_wire;
+    bool msg = spec->msg;
     int wire = spec->wire;
     if (!parse_ft_topo(!arg.empty() ? arg.c_str() : env, nranks, spec, err)) return false;
     spec->ag = ag; spec->fuse = fuse; spec->nts = nts; spec->wt = wt; spec->wire = wire; spec->round_wire = rw;
+    spec->msg = msg;
     return true;
   }
   if (err) *err = "unknown algorithm '" + raw + "'";

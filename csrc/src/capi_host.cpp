@@ -1,6 +1,8 @@
 // Host-only part of the C API: errors, planning utilities, the reference
 // cost model, the program dump, the CPU simulator of the device protocol and
 // the host reduction. Compiled by the plain host C++ compiler (no HIP).
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
@@ -13,6 +15,7 @@
 #include "flexar/cost_model.hpp"
 #include "flexar/flexar.h"
 #include "flexar/host_exec.hpp"
+#include "flexar/msg_plan.hpp"
 #include "flexar/planner.hpp"
 #include "flexar/readiness.hpp"
 #include "internal.hpp"
@@ -105,6 +108,72 @@ struct SimRun {
         });
     for (auto& t : th) t.join();
     if (rc.load()) set_error("simulated wait timed out (deadlock in the program?)");
+    return rc.load();
+  }
+};
+
+// Host run of message plans (msg_plan.hpp): one thread per rank; executor segments run on the host
+// executor, groups exchange bytes through per-(source, destination) FIFO mailboxes (NCCL matches the
+// sends and receives of a rank pair in order, without tags).
+struct MsgSimRun {
+  template <typename T, typename OP>
+  static int run(const std::vector<MsgPlan>& plans, int nranks, int ncalls, const void* const* inputs,
+                 void* const* outputs, size_t count) {
+    const size_t es = sizeof(T);
+    struct Box {
+      std::mutex m;
+      std::condition_variable cv;
+      std::vector<std::vector<char>> q;
+      size_t head = 0;
+    };
+    std::vector<Box> boxes((size_t)nranks * nranks);
+    std::atomic<int> rc{0};
+    std::vector<std::thread> th;
+    for (int r = 0; r < nranks; ++r)
+      th.emplace_back([&, r] {
+        const MsgPlan& M = plans[r];
+        std::vector<char> stg(M.stg_bytes + 256, (char)0xA5);
+        HostExecCtx c;
+        c.rank = r;
+        c.local[BUF_IN] = (char*)inputs[r];
+        c.local[BUF_OUT] = (char*)outputs[r];
+        c.local[BUF_STG] = stg.data();
+        c.peer_stg.assign(nranks, stg.data());
+        c.peer_flags.assign(nranks, nullptr);
+        c.ranks_stride = nranks;
+        c.blocks_stride = 1;
+        c.stg_half_bytes = 0;
+        auto base = [&](uint16_t b) { return c.local[b]; };
+        for (int e = 1; e <= ncalls && !rc.load(); ++e) {
+          for (const MsgStep& s : M.steps) {
+            if (s.kind == MsgStep::EXEC) {
+              if (HostExec<T, OP>::run(s.prog, c, 0, 1, (uint64_t)e)) rc.store(FLEXAR_ERR_TIMEOUT);
+              continue;
+            }
+            for (const MsgXfer& x : s.sends) {
+              Box& b = boxes[(size_t)r * nranks + x.peer];
+              std::lock_guard<std::mutex> lk(b.m);
+              b.q.emplace_back(base(x.buf) + x.off, base(x.buf) + x.off + x.bytes);
+              b.cv.notify_all();
+            }
+            for (const MsgXfer& x : s.recvs) {
+              Box& b = boxes[(size_t)x.peer * nranks + r];
+              std::unique_lock<std::mutex> lk(b.m);
+              if (!b.cv.wait_for(lk, std::chrono::seconds(30), [&] { return b.q.size() > b.head; })) {
+                rc.store(FLEXAR_ERR_TIMEOUT);
+                return;
+              }
+              std::vector<char> msg = std::move(b.q[b.head++]);
+              if (msg.size() != x.bytes) { rc.store(FLEXAR_ERR_STATE); return; }
+              memcpy(base(x.buf) + x.off, msg.data(), msg.size());
+            }
+          }
+        }
+        (void)es;
+      });
+    for (auto& t : th) t.join();
+    if (rc.load() == FLEXAR_ERR_STATE) set_error("message size mismatch between a send and its receive");
+    else if (rc.load()) set_error("message simulation timed out (unmatched receive)");
     return rc.load();
   }
 };
@@ -252,6 +321,67 @@ int flexar_simulate_typed(const char* spec, int nranks, size_t count, int dtype,
   }
   if (grid % progs[0].nchan) { set_error("grid must be a multiple of the channel count"); return FLEXAR_ERR_INVALID; }
   return dispatch_dtype_op<SimRun>(dtype, op, progs, nranks, grid, ncalls, 0, inputs, outputs, count, pre);
+}
+
+// Message transport (RCCL send/recv) plans on host memory: inputs/outputs nranks host pointers.
+int flexar_simulate_msg(const char* spec, int nranks, size_t count, int dtype, int op, const void* const* inputs,
+                        void* const* outputs, int ncalls, float scale) {
+  size_t es = dtype_size(dtype);
+  if (!es || nranks < 1 || nranks > 64 || ncalls < 1 || !inputs || !outputs) {
+    set_error("bad simulate arguments");
+    return FLEXAR_ERR_INVALID;
+  }
+  if (!op_supported(dtype, op)) { set_error("unsupported dtype/op"); return FLEXAR_ERR_UNSUPPORTED; }
+  AlgoSpec s;
+  std::string err;
+  if (!parse_algo(spec ? spec : "auto", nranks, &s, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  if (s.kind == AlgoKind::AUTO) s = select_plan(XgmiModel::from_env(), nranks, (double)count * es);
+  float fs = scale * (op == FLEXAR_AVG ? 1.0f / (float)nranks : 1.0f);
+  std::vector<MsgPlan> plans(nranks);
+  for (int r = 0; r < nranks; ++r) {
+    if (!build_msg_plan(nranks, r, count, (uint32_t)es, fs, s, &plans[r], &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+    for (auto& st : plans[r].steps)
+      if (st.kind == MsgStep::EXEC && !validate_program(st.prog, nranks, r, count, count, &err)) {
+        set_error(err);
+        return FLEXAR_ERR_INVALID;
+      }
+  }
+  return dispatch_dtype_op<MsgSimRun>(dtype, op, plans, nranks, ncalls, inputs, outputs, count);
+}
+
+// Message-plan summary (JSON): per step, the executor segment's op count or the group's sends/receives
+// (peer, bytes, zero-copy source buffer) - what the RCCL transport posts for (spec, count, dtype) on `rank`.
+int flexar_msg_plan_dump(const char* spec, int rank, int nranks, size_t count, int dtype, char* out, size_t outlen) {
+  size_t es = dtype_size(dtype);
+  if (!es || rank < 0 || rank >= nranks) { set_error("bad arguments"); return FLEXAR_ERR_INVALID; }
+  AlgoSpec s;
+  std::string err;
+  if (!parse_algo(spec ? spec : "auto", nranks, &s, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  if (s.kind == AlgoKind::AUTO) s = select_plan(XgmiModel::from_env(), nranks, (double)count * es);
+  MsgPlan M;
+  if (!build_msg_plan(nranks, rank, count, (uint32_t)es, 1.0f, s, &M, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  static const char* bn[] = {"in", "out", "stg"};
+  std::string j = "{\"stg_bytes\": " + std::to_string(M.stg_bytes) + ", \"messages\": " + std::to_string(M.msgs) +
+                  ", \"message_bytes\": " + std::to_string(M.msg_bytes) + ", \"zero_copy\": " +
+                  std::to_string(M.zero_copy) + ", \"steps\": [";
+  for (size_t i = 0; i < M.steps.size(); ++i) {
+    const MsgStep& st = M.steps[i];
+    j += i ? ", " : "";
+    if (st.kind == MsgStep::EXEC) {
+      j += "{\"exec\": " + std::to_string(st.prog.ops.size()) + "}";
+      continue;
+    }
+    auto lst = [&](const std::vector<MsgXfer>& v) {
+      std::string t = "[";
+      for (size_t k = 0; k < v.size(); ++k)
+        t += std::string(k ? ", " : "") + "[" + std::to_string(v[k].peer) + ", " + std::to_string(v[k].bytes) + ", \"" +
+             bn[v[k].buf] + "\"]";
+      return t + "]";
+    };
+    j += "{\"send\": " + lst(st.sends) + ", \"recv\": " + lst(st.recvs) + "}";
+  }
+  j += "]}";
+  return copy_out(j, out, outlen);
 }
 
 int flexar_simulate_coll(int coll, const char* spec, int nranks, size_t count, int dtype, int op,

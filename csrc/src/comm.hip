@@ -13,6 +13,7 @@
 //    FLEXAR_ERR_TIMEOUT instead of a hang.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -30,6 +31,7 @@
 #include "flexar/cost_model.hpp"
 #include "flexar/flexar.h"
 #include "flexar/log.hpp"
+#include "flexar/msg_plan.hpp"
 #include "flexar/planner.hpp"
 #include "flexar/readiness.hpp"
 #include "flexar/timer.hpp"
@@ -96,6 +98,49 @@ struct ProfRec {
   std::string algo;
   uint64_t bytes;
   std::unique_ptr<DeviceTimer> t;
+};
+
+// RCCL entry points for the message transport, resolved at run time from the process's RCCL (the one
+// torch already mapped, else /opt/rocm's): libflexar has no link-time RCCL dependency and a process never
+// holds two RCCL instances.
+struct RcclApi {
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
+  const char* (*GetErrorString)(ncclResult_t) = nullptr;
+  bool ok = false;
+  RcclApi() {
+    void* h = nullptr;
+    for (const char* n : {"librccl.so.1", "librccl.so"})
+      if (!h) h = dlopen(n, RTLD_NOW | RTLD_NOLOAD);
+    for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so"})
+      if (!h) h = dlopen(n, RTLD_NOW | RTLD_LOCAL);
+    if (!h) return;
+    GetUniqueId = (decltype(GetUniqueId))dlsym(h, "ncclGetUniqueId");
+    CommInitRank = (decltype(CommInitRank))dlsym(h, "ncclCommInitRank");
+    CommDestroy = (decltype(CommDestroy))dlsym(h, "ncclCommDestroy");
+    Send = (decltype(Send))dlsym(h, "ncclSend");
+    Recv = (decltype(Recv))dlsym(h, "ncclRecv");
+    GroupStart = (decltype(GroupStart))dlsym(h, "ncclGroupStart");
+    GroupEnd = (decltype(GroupEnd))dlsym(h, "ncclGroupEnd");
+    GetErrorString = (decltype(GetErrorString))dlsym(h, "ncclGetErrorString");
+    ok = GetUniqueId && CommInitRank && CommDestroy && Send && Recv && GroupStart && GroupEnd && GetErrorString;
+  }
+};
+static RcclApi& rccl() {
+  static RcclApi a;
+  return a;
+}
+
+// A message plan with its executor segments uploaded.
+struct DevMsgPlan {
+  MsgPlan plan;
+  std::vector<Op*> d_ops;
+  std::vector<uint32_t*> d_chan;
 };
 
 static uint64_t env_u64(const char* name, uint64_t dflt) {
@@ -185,6 +230,13 @@ struct flexar_comm {
   char peer_bus[kMaxRanks][32] = {};
   bool links_from_env = false;  // FLEXAR_MODEL fixed the link count: the probe does not override it
   int resident = 0;             // executor workgroups resident at once on this GPU (occupancy x CUs)
+  // message transport (msg_plan.hpp over RCCL): its own staging arena (never the IPC workspace, whose
+  // parity halves peers may still read), the RCCL communicator, plans per call shape
+  bool ipc = true;              // peer workspaces mapped (false: every call runs the message transport)
+  ncclComm_t nccl = nullptr;
+  char* msg_ws = nullptr;
+  size_t msg_ws_bytes = 0;
+  std::map<std::string, std::unique_ptr<DevMsgPlan>> msg_cache;
   int* st_buf = nullptr;        // self-test buffers (device)
   uint32_t* st_bad = nullptr;   // self-test mismatch counter (host-mapped)
   uint32_t* st_bad_dev = nullptr;
@@ -227,9 +279,17 @@ static int resolve_spec(flexar_comm* c, const char* algo, double bytes, AlgoSpec
     }
   }
   if (s.kind == AlgoKind::TREE && s.ag == AgMode::AUTO) s.ag = AgMode::PULL;
+  if (!c->ipc) s.msg = true;  // no peer memory: every schedule runs over the message transport
   if (c->disabled) {
     std::string why;
-    if (!downgrade_spec(&s, c->nranks, c->disabled, true, &why)) { set_error(why); return FLEXAR_ERR_UNSUPPORTED; }
+    if (!downgrade_spec(&s, c->nranks, c->disabled, true, &why, c->nccl != nullptr)) {
+      set_error(why);
+      return FLEXAR_ERR_UNSUPPORTED;
+    }
+  }
+  if (s.msg && !c->nccl) {
+    set_error("the message transport (+rccl) is not initialised on this communicator (flexar_comm_init_msg)");
+    return FLEXAR_ERR_STATE;
   }
   *out = s;
   return 0;
@@ -259,11 +319,16 @@ static int typed_spec(AlgoSpec* s, int dtype, int op, bool have_amax) {
 }
 
 static int executor_proto(flexar_comm* c, AlgoSpec* s) {
+  if (!c->ipc) s->msg = true;
   if (!c->disabled) return 0;
   std::string why;
-  if (!downgrade_spec(s, c->nranks, c->disabled, false, &why)) { set_error(why); return FLEXAR_ERR_UNSUPPORTED; }
+  if (!downgrade_spec(s, c->nranks, c->disabled, false, &why, c->nccl != nullptr)) {
+    set_error(why);
+    return FLEXAR_ERR_UNSUPPORTED;
+  }
   return 0;
 }
+
 
 // LL is valid for 1/2/4-byte elements up to kLLMaxBytes when the communicator reserved its region.
 static bool ll_usable(flexar_comm* c, uint64_t count, uint32_t es) {
@@ -382,6 +447,119 @@ static void fill_ctx(flexar_comm* c, DevProgram* dp, const void* in, void* out, 
   x->fi_ticks = c->fi_ticks;
 }
 
+// ---- message transport (msg_plan.hpp over RCCL) ----------------------------------------------------
+static int rccl_check(ncclResult_t r, const char* what) {
+  if (r == ncclSuccess) return 0;
+  set_error(std::string(what) + ": " + (rccl().GetErrorString ? rccl().GetErrorString(r) : "RCCL error"));
+  return FLEXAR_ERR_RCCL;
+}
+
+static int get_msg_plan(flexar_comm* c, const AlgoSpec& s, uint64_t count, uint32_t es, float fs, Coll coll,
+                        uint64_t stride, DevMsgPlan** out) {
+  char key[320];
+  uint32_t sb;
+  memcpy(&sb, &fs, 4);
+  snprintf(key, sizeof(key), "%d|%s|%llu|%u|%08x|%llu", (int)coll, s.str().c_str(), (unsigned long long)count, es, sb,
+           (unsigned long long)stride);
+  auto it = c->msg_cache.find(key);
+  if (it != c->msg_cache.end()) { *out = it->second.get(); return 0; }
+  std::unique_ptr<DevMsgPlan> dp(new DevMsgPlan);
+  std::string err;
+  if (!build_msg_plan(c->nranks, c->rank, count, es, fs, s, &dp->plan, &err, coll, stride)) {
+    set_error(err);
+    return FLEXAR_ERR_INVALID;
+  }
+  uint64_t in_el, out_el;
+  io_extent(coll, c->nranks, count, stride, &in_el, &out_el);
+  for (auto& st : dp->plan.steps) {
+    if (st.kind != MsgStep::EXEC) continue;
+    if (!validate_program(st.prog, c->nranks, c->rank, in_el, out_el, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+    mark_barriers(st.prog, c->rank);
+    Op* d_ops = nullptr;
+    uint32_t* d_chan = nullptr;
+    FX_HIP(hipMalloc(&d_ops, st.prog.ops.size() * sizeof(Op)));
+    FX_HIP(hipMalloc(&d_chan, st.prog.chan_start.size() * sizeof(uint32_t)));
+    FX_HIP(hipMemcpy(d_ops, st.prog.ops.data(), st.prog.ops.size() * sizeof(Op), hipMemcpyHostToDevice));
+    FX_HIP(hipMemcpy(d_chan, st.prog.chan_start.data(), st.prog.chan_start.size() * sizeof(uint32_t),
+                     hipMemcpyHostToDevice));
+    dp->d_ops.push_back(d_ops);
+    dp->d_chan.push_back(d_chan);
+  }
+  logf(LOG_INFO, c->rank, "msg plan %s: count=%llu steps=%zu messages=%llu (%llu zero-copy) arena=%llu B",
+       s.str().c_str(), (unsigned long long)count, dp->plan.steps.size(), (unsigned long long)dp->plan.msgs,
+       (unsigned long long)dp->plan.zero_copy, (unsigned long long)dp->plan.stg_bytes);
+  *out = dp.get();
+  c->msg_cache[key] = std::move(dp);
+  return 0;
+}
+
+// One call over the message transport: executor segments (local-only programs) and grouped
+// ncclSend / ncclRecv, all on `st`. The arena is the transport's own (parity-free: RCCL orders calls).
+static int run_msg(flexar_comm* c, const AlgoSpec& s, Coll coll, const void* in, void* out, uint64_t count, int dtype,
+                   int op, float fs, uint64_t stride, hipStream_t st) {
+  const uint32_t es = (uint32_t)dtype_size(dtype);
+  DevMsgPlan* dp = nullptr;
+  int rc = get_msg_plan(c, s, count, es, fs, coll, stride, &dp);
+  if (rc) return rc;
+  if (dp->plan.stg_bytes > c->msg_ws_bytes) {  // grow (first calls only): nothing of ours may still read it
+    FX_HIP(hipDeviceSynchronize());
+    if (c->msg_ws) FX_HIP(hipFree(c->msg_ws));
+    c->msg_ws = nullptr;
+    c->msg_ws_bytes = 0;
+    FX_HIP(hipMalloc(&c->msg_ws, dp->plan.stg_bytes + 256));
+    c->msg_ws_bytes = dp->plan.stg_bytes;
+  }
+  const int op_k = coll == Coll::ALLREDUCE || coll == Coll::REDUCE_SCATTER ? op : FLEXAR_SUM;
+  auto ptr = [&](uint16_t buf) -> char* {
+    return buf == BUF_IN ? (char*)in : (buf == BUF_OUT ? (char*)out : c->msg_ws);
+  };
+  size_t ex = 0;
+  for (const MsgStep& stp : dp->plan.steps) {
+    if (stp.kind == MsgStep::EXEC) {
+      LaunchArgs la;
+      la.kind = LAUNCH_EXEC;
+      DevCtx& x = la.ctx;
+      memset(&x, 0, sizeof(x));
+      x.ops = dp->d_ops[ex];
+      x.chan_start = dp->d_chan[ex];
+      x.nchan = 1;
+      x.rank = c->rank;
+      x.nranks = c->nranks;
+      x.local[BUF_IN] = (char*)in;
+      x.local[BUF_OUT] = (char*)out;
+      x.local[BUF_STG] = c->msg_ws;
+      for (int r = 0; r < c->nranks; ++r) x.peer_stg[r] = c->msg_ws;  // local-only program
+      x.peer_flags[c->rank] = c->flags;
+      x.epochs = c->epochs;
+      x.stg_half_bytes = 0;
+      x.err = c->err_dev;
+      x.timeout_ticks = c->timeout_ticks;
+      x.vec_ok = ((((uintptr_t)in) | ((uintptr_t)out)) & 15) == 0;
+      x.stg_unit = es;
+      uint64_t span = 0;
+      for (const Op& o : stp.prog.ops) span = std::max<uint64_t>(span, o.len);
+      la.grid = choose_grid(c, span * es * 2, 1);
+      la.stream = st;
+      la.proto = PM_FENCE;
+      if ((rc = launch_dtype(dtype, op_k, la))) return rc;
+      c->launches++;
+      ++ex;
+      continue;
+    }
+    if ((rc = rccl_check(rccl().GroupStart(), "ncclGroupStart"))) return rc;
+    for (const MsgXfer& m : stp.sends)
+      if ((rc = rccl_check(rccl().Send(ptr(m.buf) + m.off, m.bytes, ncclUint8, (int)m.peer, c->nccl, st), "ncclSend")))
+        break;
+    for (const MsgXfer& m : stp.recvs) {
+      if (rc) break;
+      rc = rccl_check(rccl().Recv(ptr(m.buf) + m.off, m.bytes, ncclUint8, (int)m.peer, c->nccl, st), "ncclRecv");
+    }
+    const int rc2 = rccl_check(rccl().GroupEnd(), "ncclGroupEnd");
+    if (rc || rc2) return rc ? rc : rc2;
+  }
+  return 0;
+}
+
 // Split a call into pieces whose staging fits one parity half of the workspace.
 static int plan_pieces(flexar_comm* c, const AlgoSpec& s, uint64_t count, uint32_t esize, float fs,
                        uint64_t* piece, Coll coll = Coll::ALLREDUCE, uint64_t stride = 0) {
@@ -420,6 +598,12 @@ static int run_rs_ag(flexar_comm* c, Coll coll, const void* in, void* out, size_
   if ((rc = executor_proto(c, &s))) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
   if ((rc = order_call(c, st))) return rc;
+  if (s.msg) {
+    s.wire = 0;
+    c->calls++;
+    c->bytes += count * es * c->nranks;
+    return run_msg(c, s, coll, in, out, count, dtype, coll == Coll::ALL_GATHER ? FLEXAR_SUM : op, fs, count, st);
+  }
   uint64_t piece = count;
   if (c->nranks > 1 && (rc = plan_pieces(c, s, count, es, fs, &piece, coll, count))) return rc;
   for (uint64_t off = 0; off < count; off += piece) {
@@ -469,6 +653,11 @@ static int run_bcast(flexar_comm* c, const void* in, void* out, size_t count, in
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
   if ((rc = order_call(c, st))) return rc;
+  if (s.msg) {
+    c->calls++;
+    c->bytes += count * es;
+    return run_msg(c, s, Coll::BROADCAST, in, out, count, dtype, FLEXAR_SUM, 1.0f, (uint64_t)root, st);
+  }
   uint64_t piece = count;
   if (c->nranks > 1 && (rc = plan_pieces(c, s, count, es, 1.0f, &piece, Coll::BROADCAST, (uint64_t)root))) return rc;
   for (uint64_t off = 0; off < count; off += piece) {
@@ -920,11 +1109,12 @@ int flexar_comm_connect(flexar_comm_t c, const void* all) {
       }
     }
   }
+  const bool no_ipc = env_u64("FLEXAR_FAULT_NO_IPC", 0) != 0;  // tests: behave as if mapping were impossible
   for (int r = 0; r < c->nranks; ++r) {
     if (r == c->rank) continue;
     const CommHandle& h = hs[r];
     void* p = nullptr;
-    hipError_t e = hipIpcOpenMemHandle(&p, h.stg, hipIpcMemLazyEnablePeerAccess);
+    hipError_t e = no_ipc ? hipErrorInvalidValue : hipIpcOpenMemHandle(&p, h.stg, hipIpcMemLazyEnablePeerAccess);
     if (e == hipSuccess) {
       c->peer_stg[r] = (char*)p;
       e = hipIpcOpenMemHandle(&p, h.flags, hipIpcMemLazyEnablePeerAccess);
@@ -975,7 +1165,12 @@ int flexar_comm_selftest(flexar_comm_t c, uint32_t families, uint32_t* failed_ou
   c->timeout_ticks = env_u64("FLEXAR_SELFTEST_TIMEOUT_MS", 2000) * 100000ull;
   struct Case { uint32_t fam; const char* spec; };
   const Case cases[] = {{PF_FENCE, "flat+pull"}, {PF_FENCE, "ring"}, {PF_WT, "flat+pull+wt"}, {PF_LL, "ll"},
-                        {PF_DMA, "dma"}};
+                        {PF_DMA, "dma"}, {PF_MSG, "flat+rccl"}, {PF_MSG, "ring+rccl"}};
+  if (!c->nccl) families &= ~(uint32_t)PF_MSG;
+  if (!c->ipc) {  // no peer memory on this communicator: only the message transport exists
+    families &= PF_MSG;
+    *failed_out |= PF_ALL;
+  }
   int* in = c->st_buf;
   int* out = c->st_buf + n;
   const int N = c->nranks;
@@ -1032,6 +1227,44 @@ double flexar_comm_predict_us(flexar_comm_t c, const char* spec, double bytes) {
   return c->model.cost_us(s, c->nranks, bytes);
 }
 
+int flexar_rccl_available(void) { return rccl().ok ? 1 : 0; }
+
+int flexar_rccl_unique_id(void* out, size_t len) {
+  if (!out || len < sizeof(ncclUniqueId)) { set_error("unique id buffer too small (128 bytes)"); return FLEXAR_ERR_INVALID; }
+  if (!rccl().ok) { set_error("RCCL not found (librccl.so)"); return FLEXAR_ERR_UNSUPPORTED; }
+  ncclUniqueId id;
+  int rc = rccl_check(rccl().GetUniqueId(&id), "ncclGetUniqueId");
+  if (rc) return rc;
+  memcpy(out, &id, sizeof(id));
+  return 0;
+}
+
+// Collective: every rank passes rank 0's unique id; creates the RCCL communicator of the message
+// transport ("+rccl" specs, and every call when the communicator has no IPC mapping).
+int flexar_comm_init_msg(flexar_comm_t c, const void* unique_id) {
+  if (!c || !unique_id) { set_error("null argument"); return FLEXAR_ERR_INVALID; }
+  if (!rccl().ok) { set_error("RCCL not found (librccl.so)"); return FLEXAR_ERR_UNSUPPORTED; }
+  if (c->nccl) return 0;
+  FX_HIP(hipSetDevice(c->device));
+  ncclUniqueId id;
+  memcpy(&id, unique_id, sizeof(id));
+  int rc = rccl_check(rccl().CommInitRank(&c->nccl, c->nranks, id, c->rank), "ncclCommInitRank");
+  if (rc) c->nccl = nullptr;
+  c->memo_gen++;
+  return rc;
+}
+
+// After a failed flexar_comm_connect on some rank (no usable IPC mapping): run every call over the
+// message transport instead (flexar_comm_init_msg first). Collective in effect.
+int flexar_comm_connect_msg_only(flexar_comm_t c) {
+  if (!c) return FLEXAR_ERR_INVALID;
+  if (!c->nccl) { set_error("message transport not initialised"); return FLEXAR_ERR_STATE; }
+  c->ipc = false;
+  c->connected = true;
+  c->memo_gen++;
+  return 0;
+}
+
 int flexar_comm_set_model(flexar_comm_t c, double alpha_launch_us, double alpha_sync_us, double link_gbps,
                           double hbm_gbps, int links) {
   if (!c || !(link_gbps > 0) || !(hbm_gbps > 0) || alpha_launch_us < 0 || alpha_sync_us < 0) {
@@ -1065,7 +1298,8 @@ int flexar_comm_topology(flexar_comm_t c, char* buf, size_t buflen) {
                   ", \"links\": " + std::to_string(c->model.links) + ", \"resident_blocks\": " +
                   std::to_string(c->resident) + ", \"selftested\": \"" + family_names(c->selftested) +
                   "\", \"disabled\": \"" + (c->disabled ? family_names(c->disabled) : std::string()) +
-                  "\", \"peers\": [";
+                  "\", \"ipc\": " + (c->ipc ? "true" : "false") + ", \"rccl\": " + (c->nccl ? "true" : "false") +
+                  ", \"peers\": [";
   for (int r = 0; r < c->nranks; ++r) {
     char t[256];
     snprintf(t, sizeof(t), "%s{\"rank\": %d, \"bus\": \"%s\", \"device\": %d, \"link\": \"%s\", \"hops\": %d}",
@@ -1097,6 +1331,12 @@ int flexar_comm_destroy(flexar_comm_t c) {
   }
   if (c->dma_fork) (void)hipEventDestroy(c->dma_fork);
   if (c->order_ev) (void)hipEventDestroy(c->order_ev);
+  for (auto& kv : c->msg_cache) {
+    for (Op* p : kv.second->d_ops) (void)hipFree(p);
+    for (uint32_t* p : kv.second->d_chan) (void)hipFree(p);
+  }
+  if (c->msg_ws) (void)hipFree(c->msg_ws);
+  if (c->nccl && rccl().ok) (void)rccl().CommDestroy(c->nccl);
   if (c->st_buf) (void)hipFree(c->st_buf);
   if (c->st_bad) (void)hipHostFree(c->st_bad);
   (void)hipFree(c->stg);
@@ -1226,6 +1466,7 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     s = f;
     if ((rc = executor_proto(c, &s))) return rc;
   }
+  if (s.msg) s.wire = 0;  // the message transport runs the schedule untyped
   auto remember = [&](uint64_t piece, DevProgram* dp, int grid) {
     if (hit) return;
     m.gen = c->memo_gen;
@@ -1239,6 +1480,15 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     m.dp = dp;
     m.grid = grid;
   };
+  if (s.msg) {
+    remember(0, nullptr, 0);
+    if (roctx().push) roctx().push(("flexar allreduce " + s.str() + " " + std::to_string(count * es) + "B").c_str());
+    c->calls++;
+    c->bytes += count * es;
+    rc = run_msg(c, s, Coll::ALLREDUCE, in, out, count, dtype, op, fs, 0, st);
+    if (roctx().pop) roctx().pop();
+    return rc;
+  }
   if (s.kind == AlgoKind::DMA) {
     remember(0, nullptr, 0);
     if (roctx().push) roctx().push(("flexar allreduce dma " + std::to_string(count * es) + "B").c_str());
@@ -1403,6 +1653,10 @@ int flexar_allreduce_fp8(flexar_comm_t c, const void* in, void* out, size_t coun
   s.wt = wt;
   s.wire = wire_dtype == FLEXAR_FP8_E4M3 ? 2 : 3;
   if ((rc = executor_proto(c, &s))) return rc;
+  if (s.msg) {
+    set_error("fp8 wire compression runs on the IPC executor (the message transport has no typed staging)");
+    return FLEXAR_ERR_UNSUPPORTED;
+  }
   std::lock_guard<std::mutex> lk(c->mu);
   if ((rc = order_call(c, st))) return rc;
   uint64_t piece = count;

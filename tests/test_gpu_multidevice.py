@@ -30,16 +30,18 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, specs, q):
+def _worker(rank, world, port, specs, q, transport="rccl", no_ipc=False):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_TIMEOUT_MS="20000")
+        if no_ipc:
+            os.environ["FLEXAR_FAULT_NO_IPC"] = "1"  # every peer mapping fails: the RCCL fallback carries all
         import torch.distributed as dist
 
         torch.cuda.set_device(rank)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from allreduce_over_mpi_amd.parallel import Communicator
 
-        comm = Communicator(workspace_bytes=128 << 20)
+        comm = Communicator(workspace_bytes=128 << 20, transport=transport)
         dev = torch.device("cuda", rank)
         results = {}
         for spec in specs:
@@ -75,11 +77,11 @@ def test_allreduce_one_process_per_gpu(cuda):
     import torch.multiprocessing as mp
 
     world = min(_ngpu(), 8)
-    specs = ["flat", "flat+push", "flat+wt", "ring", "ring+wt", "oneshot", "ll", "dma"]
+    specs = ["flat", "flat+push", "flat+wt", "ring", "ring+wt", "oneshot", "ll", "dma", "flat+rccl", "ring+rccl"]
     if world > 2:
         specs.append("ring:2")
     if world >= 4 and (world & (world - 1)) == 0:
-        specs.append("rhd")
+        specs += ["rhd", "rhd+rccl"]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -99,13 +101,43 @@ def test_allreduce_one_process_per_gpu(cuda):
         # connect-time probe: every peer is another GPU reachable peer-to-peer; the self-test verified
         # every protocol family on the real links
         assert failed == [], (rank, failed, topo)
-        assert topo["selftested"] == "fence,wt,ll,dma", topo
+        assert topo["selftested"] == "fence,wt,ll,dma,rccl", topo
         for p in topo["peers"]:
             if p["rank"] != rank:
                 assert p["link"] in ("xgmi", "pcie"), topo
                 assert p["device"] == p["rank"], topo  # torch.cuda.set_device(rank) in _worker
         if all(p["link"] == "xgmi" and p["hops"] <= 1 for p in topo["peers"] if p["rank"] != rank):
             assert topo["links"] == world - 1, topo
+        for key, err in res.items():
+            tol = 1e-5 if "float32" in key[1] else 2e-2
+            assert err < tol, (rank, key, err)
+
+
+@pytest.mark.skipif(_ngpu() < 2, reason="needs >= 2 GPUs (one RCCL rank per device)")
+def test_rccl_fallback_when_ipc_is_unavailable(cuda):
+    """Every peer mapping fails (FLEXAR_FAULT_NO_IPC): the communicator still comes up and every schedule
+    (FlexTree, ring, RHD, flat) runs over the RCCL message transport with the same results."""
+    import torch.multiprocessing as mp
+
+    world = min(_ngpu(), 4)
+    specs = ["flat", "ring", "oneshot"] + (["rhd", "tree:2,2"] if world == 4 else [])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, specs, q, "auto", True)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        rank, res, err = q.get(timeout=600)
+        assert err is None, f"rank {rank} failed:\n{err}"
+        out[rank] = res
+    for p in procs:
+        p.join(timeout=60)
+    for rank, res in out.items():
+        topo, failed = res.pop("readiness")
+        assert topo["ipc"] is False and topo["rccl"] is True, topo
+        assert topo["selftested"] == "rccl" and "rccl" not in failed, (topo, failed)
         for key, err in res.items():
             tol = 1e-5 if "float32" in key[1] else 2e-2
             assert err < tol, (rank, key, err)
