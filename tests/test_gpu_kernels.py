@@ -385,6 +385,31 @@ def test_chunk_and_channel_knobs(cuda, monkeypatch):
 
 
 @pytest.mark.parametrize("n", [2, 4, 8])
+def test_dma_pipelined_pieces(cuda, monkeypatch, n):
+    """Copy-engine allreduce split into many pieces (FLEXAR_CHUNK_BYTES): the pipelined schedule (RS copies
+    of piece k+1 while piece k reduces, AG copies of k while k+1 scatters, staging halves reused every
+    other piece) gives exact integer-valued sums, in and out of place, over consecutive calls."""
+    from allreduce_over_mpi_amd.parallel import LocalGroup
+
+    monkeypatch.setenv("FLEXAR_CHUNK_BYTES", str(256 << 10))
+    grp = LocalGroup(n, workspace_bytes=16 << 20)
+    try:
+        for size in ((1 << 20) + 77, 3 << 20):
+            g = torch.Generator(device=cuda).manual_seed(size + n)
+            xs = [torch.randint(-50, 50, (size,), device=cuda, generator=g).float() for _ in range(n)]
+            ref = torch.stack(xs).sum(0)
+            for it in range(3):
+                outs = grp.all_reduce([x.clone() for x in xs], algo="dma")
+                outs2 = grp.all_reduce([x * 2 for x in xs], outs=[torch.empty_like(x) for x in xs], algo="dma")
+                torch.cuda.synchronize()
+                for o, o2 in zip(outs, outs2):
+                    assert torch.equal(o, ref) and torch.equal(o2, 2 * ref), (size, it)
+        grp.check()
+    finally:
+        grp.close()
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
 def test_group_broadcast(cuda, groups, n):
     """Broadcast from every root: direct (small/auto) and scatter + all-gather (large/flat), fp32 and bf16,
     with data that changes every call (stale staging would show)."""
