@@ -94,6 +94,8 @@ def main():
     ap.add_argument("--no-rccl", action="store_true", help="skip the RCCL comparison run")
     ap.add_argument("--no-small", action="store_true", help="skip the 8 KiB latency companion figure")
     ap.add_argument("--no-tune", action="store_true", help="use the cost model instead of the start-up tuner")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "auto", "ipc"],
+                    help="Communicator transport at N > 1 (rccl: IPC + the '+rccl' message transport candidates)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -138,14 +140,23 @@ def main():
     ws_bytes = max(512 << 20, 4 * nbytes + (64 << 20))
     fallback = None
 
+    # one rank per GPU: IPC plus the RCCL message transport, so the tuner also measures the FlexTree / ring /
+    # RHD schedules over ncclSend/ncclRecv ("+rccl"); if RCCL cannot be set up, IPC alone
+    transports = ["ipc"] if (world == 1 or shared) else [args.transport, "ipc"] if args.transport != "ipc" else ["ipc"]
+
     def make_comm():
-        try:
-            return Communicator(workspace_bytes=ws_bytes)
-        except nv.FlexarError as e:
-            if world == 1 or shared:
-                raise
-            log(rank, f"flexar communicator unavailable on this node ({e}); measuring RCCL instead")
-            return None
+        err = None
+        for tr in transports:
+            try:
+                return Communicator(workspace_bytes=ws_bytes, transport=tr)
+            except nv.FlexarError as e:
+                err = e
+                if world > 1 and not shared:
+                    log(rank, f"flexar communicator with transport={tr} failed: {e}")
+        if world == 1 or shared:
+            raise err
+        log(rank, f"flexar communicator unavailable on this node ({err}); measuring RCCL instead")
+        return None
 
     comm = make_comm()
     if comm is None:
@@ -242,6 +253,8 @@ def main():
         # flat-stage protocols, rings on 1..4 arc-disjoint channels, RHD, two-stage FlexTree factorizations,
         # the copy engines (and the latency protocols for small buffers)
         cands = default_candidates(world, nbytes)
+        if comm.topology().get("rccl"):  # the schedules over RCCL send/recv as well
+            cands += ["flat+rccl", "ring+rccl"] + (["rhd+rccl"] if world > 2 and not world & (world - 1) else [])
         timings = {}
         for spec in cands:
             failed = 0.0
