@@ -1,10 +1,11 @@
-"""Topology helpers (Python face of csrc/include/flexar/topology.hpp + cost_model.hpp).
+"""Topology helpers on top of csrc/include/flexar/topology.hpp + cost_model.hpp (through ``_native``).
 
-* ``get_factor_count`` — reference ``topo_count/factor_count.py:1-15`` (number of
-  ordered factorizations H(n), i.e. the size of the FlexTree search space), here
-  memoised instead of exponential.
-* ``parse_ft_topo`` / ``enumerate_plans`` / ``select_plan`` / ``legacy_cost`` call
-  the native implementations so Python and the runtime can never disagree.
+* ``get_factor_count`` - the size of the FlexTree search space H(n), the number of ordered factorizations
+  of n (reference ``topo_count/factor_count.py:1-15``, an exponential recursion): a divisor DP here,
+  checked against the native ``count_factorizations`` in tests/test_topology.py.
+* ``legacy_best`` - the reference cost model's argmin over ordered factorizations (CostModel.h:82-119).
+* ``selection_table`` - the runtime selector's choice and predicted time per buffer size (what
+  ``tools/flexar_plan select`` prints), for reports and notebooks.
 """
 from __future__ import annotations
 
@@ -15,35 +16,18 @@ from .. import _native as nv
 
 @lru_cache(maxsize=None)
 def get_factor_count(num: int) -> int:
+    """H(num): ordered factorizations of num into factors >= 2 (H(1) = 1, H(n <= 0) = 0)."""
     if num <= 0:
         return 0
-    if num == 1:
-        return 1
-    return sum(get_factor_count(num // i) for i in range(2, num + 1) if num % i == 0)
-
-
-def parse_ft_topo(ft_topo, nranks: int) -> str:
-    return nv.parse_ft_topo(ft_topo, nranks)
-
-
-def enumerate_plans(nranks: int):
-    return nv.enumerate_plans(nranks)
-
-
-def select_plan(nranks: int, nbytes: float) -> str:
-    return nv.select_plan(nranks, nbytes)
-
-
-def model_cost_us(spec: str, nranks: int, nbytes: float) -> float:
-    return nv.model_cost_us(spec, nranks, nbytes)
-
-
-def legacy_cost(widths, nranks: int, chunk: float = 100.0) -> float:
-    return nv.legacy_cost(widths, nranks, chunk)
+    h = [0] * (num + 1)
+    h[1] = 1
+    for m in range(2, num + 1):
+        h[m] = sum(h[m // f] for f in range(2, m + 1) if m % f == 0)
+    return h[num]
 
 
 def legacy_best(nranks: int, chunk: float = 100.0):
-    """The reference cost model's argmin over ordered factorizations (CostModel.h:82-119)."""
+    """The reference cost model's argmin over ordered factorizations: (widths, cost)."""
     best = None
     for p in nv.enumerate_plans(nranks):
         if not p.startswith("tree:"):
@@ -53,3 +37,13 @@ def legacy_best(nranks: int, chunk: float = 100.0):
         if best is None or c < best[1]:
             best = (w, c)
     return best
+
+
+def selection_table(nranks: int, sizes=None):
+    """[(bytes, spec, predicted_us)] of the runtime selector (FLEXAR_MODEL / defaults) per buffer size."""
+    sizes = sizes or [4096 << (2 * k) for k in range(11)]
+    rows = []
+    for b in sizes:
+        spec = nv.select_plan(nranks, float(b))
+        rows.append((b, spec, nv.model_cost_us(spec, nranks, float(b))))
+    return rows

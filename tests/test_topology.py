@@ -142,3 +142,11 @@ def test_plans_move_bandwidth_optimal_bytes(nv, n):
         for r in range(n):
             got = _remote_elems(nv.plan_dump(spec, r, n, count), r)
             assert abs(got - want) <= 0.01 * want, (spec, n, r, got, want)
+
+
+def test_selection_table_matches_selector():
+    from allreduce_over_mpi_amd.utils.topology import selection_table
+
+    rows = selection_table(8, [4096, 1 << 20, 256 << 20])
+    assert [r[1] for r in rows] == [nv.select_plan(8, b) for b in (4096, 1 << 20, 256 << 20)]
+    assert rows[0][2] < rows[1][2] < rows[2][2]
