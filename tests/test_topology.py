@@ -145,6 +145,7 @@ def test_plans_move_bandwidth_optimal_bytes(nv, n):
 
 
 def test_selection_table_matches_selector():
+    from allreduce_over_mpi_amd import _native as nv
     from allreduce_over_mpi_amd.utils.topology import selection_table
 
     rows = selection_table(8, [4096, 1 << 20, 256 << 20])
