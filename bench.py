@@ -94,6 +94,8 @@ def main():
     ap.add_argument("--no-rccl", action="store_true", help="skip the RCCL comparison run")
     ap.add_argument("--no-small", action="store_true", help="skip the 8 KiB latency companion figure")
     ap.add_argument("--no-tune", action="store_true", help="use the cost model instead of the start-up tuner")
+    ap.add_argument("--no-calibrate", action="store_true",
+                    help="skip fitting the cost model to the tuner's timings plus a 64 KiB..64 MiB mini-sweep")
     ap.add_argument("--transport", default="rccl", choices=["rccl", "auto", "ipc"],
                     help="Communicator transport at N > 1 (rccl: IPC + the '+rccl' message transport candidates)")
     args = ap.parse_args()
@@ -245,6 +247,7 @@ def main():
     # ---------------------------------------------------------------- start-up tuner
     algo = args.algo
     tune_log = {}
+    calib = None
     if fallback:
         algo = "rccl"
     elif world > 1 and algo == "auto" and not args.no_tune:
@@ -285,6 +288,8 @@ def main():
             timings[spec] = t
             tune_log[spec] = round(busbw_gbps(nbytes, t, world), 2)
             log(rank, f"tuner: {spec:14s} {t*1e3:8.3f} ms  busbw {busbw_gbps(nbytes, t, world):8.1f} GB/s")
+        if timings and not fallback and not args.no_calibrate:
+            calib = calibrate_model(comm, timings, nbytes, esize, world, x, y, op, dist, max_over_ranks, rank, shared)
         if not timings or fallback:
             fallback = fallback or "no flexar algorithm produced correct results on this node"
             log(rank, f"tuner: {fallback}; measuring RCCL instead")
@@ -423,6 +428,7 @@ def main():
         "fallback": fallback,
         "tuner": tune_log or None,
         "cost_model": model,
+        "cost_model_fit": calib,
         "readiness": readiness,
         "small_msg_8KiB_us_per_call": small,
     }
@@ -436,6 +442,66 @@ def main():
     comm.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+CALIB_SIZES = (64 << 10, 1 << 20, 8 << 20, 64 << 20)
+
+
+def calibrate_model(comm, timings, nbytes, esize, world, x, y, op, dist, max_over_ranks, rank, shared):
+    """Fit the cost model (utils/costfit.py) to this node: the tuner's timings at the headline size plus a
+    mini-sweep of the correct executor schedules at CALIB_SIZES, and report the fitted constants, the fit
+    error and the schedule the FITTED model would pick at the headline size next to the tuner's winner.
+    That is the "cost-model-selected" configuration of BASELINE #4, priced with measured constants instead
+    of defaults. Not installed: the timed region runs the tuner's pick. Max over ranks, so every rank
+    fits the same rows."""
+    import torch
+
+    from allreduce_over_mpi_amd import _native as nv
+    from allreduce_over_mpi_amd.utils.costfit import fit_model
+
+    links = int(comm.topology().get("links", 0)) if not shared else 0
+    # executor schedules over IPC only: the model prices neither the copy engines nor the message transport
+    specs = [s for s in timings if "+rccl" not in s and "+msg" not in s
+             and nv.model_features(s, world, float(nbytes), links) is not None]
+    rows = [{"spec": s, "bytes": nbytes, "us": timings[s] * 1e6} for s in specs]
+    for b in CALIB_SIZES:
+        n = b // esize
+        if n >= x.numel():
+            continue
+        xv, yv = x[:n], y[:n]
+        iters = max(5, min(50, int(2e8 // b)))
+        for s in specs:
+            try:
+                comm.all_reduce(xv, out=yv, op=op, algo=s)
+                torch.cuda.synchronize()
+                if world > 1:
+                    dist.barrier()
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    comm.all_reduce(xv, out=yv, op=op, algo=s)
+                torch.cuda.synchronize()
+                comm.check()
+                t = max_over_ranks(time.perf_counter() - t0) / iters
+            except Exception as e:  # noqa: BLE001 - a spec failing at a small size is reported, not fatal
+                log(rank, f"calibration: {s} at {b} B failed: {e}")
+                return {"error": f"{s} at {b} B: {e}"}
+            rows.append({"spec": s, "bytes": b, "us": t * 1e6})
+    try:
+        fit = fit_model(rows, world, links)
+    except ValueError as e:
+        return {"error": str(e)}
+    feats = {s: nv.model_features(s, world, float(nbytes), links) for s in specs}
+    theta = (fit["alpha_launch_us"], fit["alpha_sync_us"], 1.0 / fit["link_gbps"], 1.0 / fit["hbm_gbps"])
+    pick = min(specs, key=lambda s: sum(f * t for f, t in zip(feats[s], theta)))
+    best = min(timings, key=timings.get)
+    out = {"FLEXAR_MODEL": fit["FLEXAR_MODEL"], "rows": fit["rows"], "median_rel_err": round(fit["median_rel_err"], 3),
+           "max_rel_err": round(fit["max_rel_err"], 3), "winner_agreement": round(fit["winner_agreement"], 2),
+           "fitted_choice": pick, "fitted_choice_us": round(timings[pick] * 1e6, 1),
+           "tuner_best": best, "tuner_best_us": round(timings[best] * 1e6, 1),
+           "sizes": fit["sizes"]}
+    log(rank, f"calibration: FLEXAR_MODEL={fit['FLEXAR_MODEL']} median rel err {out['median_rel_err']}, "
+              f"fitted choice {pick} ({out['fitted_choice_us']} us) vs tuner best {best} ({out['tuner_best_us']} us)")
+    return out
 
 
 def parse_bytes(v: str) -> int:
