@@ -159,28 +159,54 @@ inline bool build_msg_plan(uint32_t N, uint32_t r, uint64_t count, uint32_t esiz
       for (const Reg& g : regs) total += g.bytes;
       m.bytes = total;
       bool zc = false;
-      if (regs.size() == 1) {
-        // zero copy: every destination of an XFER receives the same value, so a single-region message is
-        // sent straight from the op's local destination (e.g. OUT of a reduction), or from the source of a
-        // pure copy - provided nothing overwrites that range before the message goes out
-        const Op& o = ops[regs[0].op];
-        int local = -1;
-        for (int d = 0; d < o.ndst && local < 0; ++d)
-          if (o.dst[d].rank == r && !writes_overlap(regs[0].op, kv.first, o.dst[d], o.len)) local = d;
-        const bool copy_src = o.nsrc == 1 && o.scale == 1.0f && !writes_overlap(regs[0].op, kv.first, o.src[0], o.len);
-        if (local >= 0 || copy_src) {
-          const Loc& from = local >= 0 ? o.dst[local] : o.src[0];
-          m.buf = from.buf;
-          m.off = from.off * es;
-          zc = true;
-          ++M->zero_copy;
-          // remove that destination from the XFER (drop the op if nothing else is left)
-          Op& w = ops[regs[0].op];
-          const int d0 = find_dst(w, regs[0].peer, regs[0].off);
+      // zero copy: every destination of an XFER receives the same value, so a message whose regions are
+      // contiguous at the receiver is sent straight from a local copy of the same bytes - the ops' local
+      // destinations (e.g. OUT of a reduction) or the sources of pure copies - when those are contiguous
+      // too (the digit-reversed tree layout makes every (stage, peer) payload one span, planner.hpp
+      // build_tree) and nothing overwrites them before the message goes out
+      bool dst_contig = true;
+      for (size_t i = 1; i < regs.size() && dst_contig; ++i)
+        dst_contig = regs[i - 1].off + regs[i - 1].bytes / es == regs[i].off;
+      const Loc* from = nullptr;
+      if (dst_contig && !regs.empty()) {
+        // candidate source of region i: local destination d (d >= 0) or the copy source (d = -1)
+        auto cand = [&](size_t i, int d) -> const Loc* {
+          const Op& o = ops[regs[i].op];
+          if (d >= 0) return o.dst[d].rank == r ? &o.dst[d] : nullptr;
+          return o.nsrc == 1 && o.scale == 1.0f && o.src[0].rank == r ? &o.src[0] : nullptr;
+        };
+        const Op& o0 = ops[regs[0].op];
+        for (int d0 = 0; d0 <= o0.ndst && !from; ++d0) {
+          const int sel = d0 < o0.ndst ? d0 : -1;  // local destinations first, then the copy source
+          const Loc* first = cand(0, sel);
+          if (!first || writes_overlap(regs[0].op, kv.first, *first, ops[regs[0].op].len)) continue;
+          uint64_t next = first->off + ops[regs[0].op].len;
+          bool ok = true;
+          for (size_t i = 1; i < regs.size() && ok; ++i) {
+            const Op& o = ops[regs[i].op];
+            const Loc* hit = nullptr;
+            for (int d = (sel >= 0 ? 0 : -1); d < (sel >= 0 ? o.ndst : 0) && !hit; ++d) {
+              const Loc* c = cand(i, d);
+              if (c && c->buf == first->buf && c->off == next) hit = c;
+            }
+            ok = hit && !writes_overlap(regs[i].op, kv.first, *hit, o.len);
+            next += o.len;
+          }
+          if (ok) from = first;
+        }
+      }
+      if (from) {
+        m.buf = from->buf;
+        m.off = from->off * es;
+        zc = true;
+        ++M->zero_copy;
+        for (const Reg& g : regs) {  // remove the peer destinations (drop an op if nothing else is left)
+          Op& w = ops[g.op];
+          const int d0 = find_dst(w, g.peer, g.off);
           if (d0 < 0) { if (err) *err = "internal: message region lost"; return false; }
           for (int d = d0; d + 1 < w.ndst; ++d) w.dst[d] = w.dst[d + 1];
           --w.ndst;
-          if (w.ndst == 0) drop[regs[0].op] = true;
+          if (w.ndst == 0) drop[g.op] = true;
         }
       }
       if (!zc) {
@@ -247,8 +273,12 @@ inline bool build_msg_plan(uint32_t N, uint32_t r, uint64_t count, uint32_t esiz
         const auto& regs = incoming[p][next_in[p]++].regions;
         MsgXfer m;
         m.peer = p;
-        for (auto& g : regs) m.bytes += g.second * es;
-        if (regs.size() == 1) {  // lands in place
+        bool contig = true;
+        for (size_t j = 0; j < regs.size(); ++j) {
+          m.bytes += regs[j].second * es;
+          if (j) contig = contig && regs[j - 1].first + regs[j - 1].second == regs[j].first;
+        }
+        if (!regs.empty() && contig) {  // one span of staging: lands in place
           m.buf = BUF_STG;
           m.off = regs[0].first * es;
         } else {

@@ -523,12 +523,6 @@ class Planner {
   void build_tree(const std::vector<int>& widths, const uint32_t N, uint16_t first, bool pull, bool fuse) {
     const uint32_t S = (uint32_t)widths.size();
     uint64_t split = round_up((count + N - 1) / N);
-    auto blen = [&](uint32_t k) -> uint64_t {
-      uint64_t s = (uint64_t)k * split;
-      return s >= count ? 0 : std::min(split, count - s);
-    };
-    auto boff = [&](uint32_t k) { return (uint64_t)k * split; };
-
     std::vector<Stage> st(S);
     uint32_t g = 1;
     for (uint32_t s = 0; s < S; ++s) {
@@ -542,10 +536,27 @@ class Planner {
       g = x.G;
     }
     auto digit = [&](uint32_t rank, uint32_t s) { return (rank / st[s].g) % st[s].w; };
-    // blocks of member p at stage s: k == p (mod G_s)
+    // Digit-reversed block placement: block k, with mixed-radix digits d_s = digit(k, s),
+    // lives at physical block pos(k) = sum_s d_s * N / G_s (the stage-0 digit most significant). The blocks
+    // a stage-s member sends one peer (k == p mod G_s: digits 0..s fixed) are then ONE contiguous span of
+    // the buffer, and the slot index pos(k) mod (N / G_s) keeps their staging slots contiguous in the same
+    // order: one region per (stage, peer) message (msg_plan.hpp sends it in place, zero copy). Flat (one
+    // stage) is the identity. Ops stay one per block: the executor slices every op over the workgroups, so
+    // all ops touching a block must share its span for each workgroup to read only what it wrote.
+    std::vector<uint32_t> pos(N, 0);
+    for (uint32_t k = 0; k < N; ++k)
+      for (uint32_t s = 0; s < S; ++s) pos[k] += digit(k, s) * (N / st[s].G);
+    auto boff = [&](uint32_t k) { return (uint64_t)pos[k] * split; };
+    auto blen = [&](uint32_t k) -> uint64_t {
+      uint64_t s = boff(k);
+      return s >= count ? 0 : std::min(split, count - s);
+    };
+    auto sidx = [&](uint32_t s, uint32_t k) { return (uint64_t)(pos[k] % (N / st[s].G)); };
+    // blocks of member p at stage s: k == p (mod G_s), in buffer order
     auto blocks_of = [&](uint32_t p, uint32_t s) {
       std::vector<uint32_t> b;
       for (uint32_t k = p % st[s].G; k < N; k += st[s].G) b.push_back(k);
+      std::sort(b.begin(), b.end(), [&](uint32_t a, uint32_t c) { return pos[a] < pos[c]; });
       return b;
     };
     // Staging layout (identical on every rank): rs[s], ag[s] (push) or pub (pull). Wire mode 1: the RS
@@ -562,7 +573,7 @@ class Planner {
     else
       for (uint32_t s = 0; s < S; ++s) ag_base[s] = alloc((uint64_t)st[s].w * (N / st[s].G) * split);
     auto rs_off = [&](uint32_t s, uint32_t j, uint32_t k) {
-      return rs_base[s] + ((uint64_t)j * (N / st[s].G) + k / st[s].G) * slot_units(s);
+      return rs_base[s] + ((uint64_t)j * (N / st[s].G) + sidx(s, k)) * slot_units(s);
     };
     auto rs_loc = [&](uint32_t s, uint32_t rank, uint32_t j, uint32_t k) {
       return acc && s > 0 ? wloc(rank, rs_off(s, j, k)) : loc(BUF_STG, rank, rs_off(s, j, k));
@@ -573,9 +584,9 @@ class Planner {
       return acc ? rs_loc(s, r, st[s].myj, k) : loc(BUF_OUT, r, boff(k));
     };
     auto ag_off = [&](uint32_t s, uint32_t j, uint32_t k) {
-      return ag_base[s] + ((uint64_t)j * (N / st[s].G) + k / st[s].G) * split;
+      return ag_base[s] + ((uint64_t)j * (N / st[s].G) + sidx(s, k)) * split;
     };
-    auto pub_off = [&](uint32_t k) { return pub_base + (uint64_t)k * split; };
+    auto pub_off = [&](uint32_t k) { return pub_base + boff(k); };
     // rank in stage-s group of `r` that owns block k after stage s
     auto owner_at = [&](uint32_t k, uint32_t s) { return st[s].base + digit(k, s) * st[s].g; };
 
