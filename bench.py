@@ -21,8 +21,10 @@ as an extra key for whole-job accounting.
 
 At N >= 2 the line also carries the cost model's own choice for this size (no tune table: what
 `auto` runs in production), the model's predicted time for it and its measured time, next to the
-start-up tuner's choice (BASELINE config #4 "cost-model-selected"), and the connect-time readiness
-result (probed links, self-tested protocol families).
+start-up tuner's choice (BASELINE config #4 "cost-model-selected"), the connect-time readiness
+result (probed links, self-tested protocol families), and `cost_model_fit`: every correct candidate at
+64 KiB / 1 MiB / 8 MiB / 64 MiB (checked against RCCL) next to RCCL's own allreduce, and the cost model
+fitted to those timings with its pick at the headline size.
 
 Correctness: every tuner candidate and the final choice are checked against RCCL's result
 (torch.distributed "nccl") on three consecutive calls whose inputs are scaled by 1, 1/2 and 1/4 (exact
@@ -95,7 +97,7 @@ def main():
     ap.add_argument("--no-small", action="store_true", help="skip the 8 KiB latency companion figure")
     ap.add_argument("--no-tune", action="store_true", help="use the cost model instead of the start-up tuner")
     ap.add_argument("--no-calibrate", action="store_true",
-                    help="skip fitting the cost model to the tuner's timings plus a 64 KiB..64 MiB mini-sweep")
+                    help="skip the 64 KiB..64 MiB mini-sweep of the tuner's candidates vs RCCL and the cost-model fit")
     ap.add_argument("--transport", default="rccl", choices=["rccl", "auto", "ipc"],
                     help="Communicator transport at N > 1 (rccl: IPC + the '+rccl' message transport candidates)")
     args = ap.parse_args()
@@ -215,6 +217,11 @@ def main():
             worst = max(worst, err)
         return worst <= tol, worst
 
+    def verify(out, n):
+        """A prefix of n elements of the last result against the same prefix of the reference."""
+        err = float((out.float() - ref_f[:n]).abs().max().item()) / ref_max
+        return err <= tol, err
+
     def timed(spec, iters, warm=1):
         a = None if spec == "auto" else spec
         for _ in range(warm):
@@ -269,7 +276,7 @@ def main():
                     tune_log[spec] = f"WRONG (max rel err {err:.3g})"
                     log(rank, f"tuner: {spec} produced wrong results (rel err {err:.3g}); excluded")
                 else:
-                    t = timed(spec, 5)
+                    t = timed(spec, 5, warm=2)
                     comm.check()
             except nv.FlexarError as e:
                 failed = 1.0
@@ -289,7 +296,14 @@ def main():
             tune_log[spec] = round(busbw_gbps(nbytes, t, world), 2)
             log(rank, f"tuner: {spec:14s} {t*1e3:8.3f} ms  busbw {busbw_gbps(nbytes, t, world):8.1f} GB/s")
         if timings and not fallback and not args.no_calibrate:
-            calib = calibrate_model(comm, timings, nbytes, esize, world, x, y, op, dist, max_over_ranks, rank, shared)
+            calib = calibrate_model(comm, timings, nbytes, esize, world, x, y, op, dist, max_over_ranks, rank, shared,
+                                    verify, world > 1 and not args.no_rccl and dtype != torch.float8_e4m3fn)
+            if calib.get("broken"):  # a candidate failed at a small size: start from a fresh communicator
+                comm.close()
+                torch.cuda.synchronize()
+                comm = make_comm() or RcclOnly(dist)
+                if isinstance(comm, RcclOnly):
+                    fallback = "flexar communicator could not be rebuilt"
         if not timings or fallback:
             fallback = fallback or "no flexar algorithm produced correct results on this node"
             log(rank, f"tuner: {fallback}; measuring RCCL instead")
@@ -447,58 +461,100 @@ def main():
 CALIB_SIZES = (64 << 10, 1 << 20, 8 << 20, 64 << 20)
 
 
-def calibrate_model(comm, timings, nbytes, esize, world, x, y, op, dist, max_over_ranks, rank, shared):
-    """Fit the cost model (utils/costfit.py) to this node: the tuner's timings at the headline size plus a
-    mini-sweep of the correct executor schedules at CALIB_SIZES, and report the fitted constants, the fit
-    error and the schedule the FITTED model would pick at the headline size next to the tuner's winner.
-    That is the "cost-model-selected" configuration of BASELINE #4, priced with measured constants instead
-    of defaults. Not installed: the timed region runs the tuner's pick. Max over ranks, so every rank
-    fits the same rows."""
+def calibrate_model(comm, timings, nbytes, esize, world, x, y, op, dist, max_over_ranks, rank, shared, verify,
+                    with_rccl):
+    """Mini-sweep of every correct tuner candidate at CALIB_SIZES (each result checked against the RCCL
+    reference, which is elementwise, so a prefix of it is the reference of the prefix), next to RCCL's own
+    allreduce of the same bytes: a flexar-vs-RCCL table across sizes from the driver's run (BASELINE #4).
+    Then fit the cost model (utils/costfit.py) to the executor schedules' timings (these sizes plus the
+    tuner's at the headline size) and report the fitted constants, the fit error and the schedule the
+    FITTED model would pick at the headline size next to the tuner's winner ("cost-model-selected" priced
+    with measured constants). Not installed: the timed region runs the tuner's pick. Times are max over
+    ranks, so every rank fits the same rows."""
     import torch
 
     from allreduce_over_mpi_amd import _native as nv
     from allreduce_over_mpi_amd.utils.costfit import fit_model
+    from allreduce_over_mpi_amd.utils.perf import busbw_gbps
 
     links = int(comm.topology().get("links", 0)) if not shared else 0
-    # executor schedules over IPC only: the model prices neither the copy engines nor the message transport
-    specs = [s for s in timings if "+rccl" not in s and "+msg" not in s
-             and nv.model_features(s, world, float(nbytes), links) is not None]
-    rows = [{"spec": s, "bytes": nbytes, "us": timings[s] * 1e6} for s in specs]
+    # the model prices executor schedules over IPC only (not the copy engines or the message transport)
+    model_specs = [s for s in timings if "+rccl" not in s and "+msg" not in s
+                   and nv.model_features(s, world, float(nbytes), links) is not None]
+    rows = [{"spec": s, "bytes": nbytes, "us": timings[s] * 1e6} for s in model_specs]
+    table, wrong = [], []
+
+    def t_of(fn, iters):
+        fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize()
+        return max_over_ranks(time.perf_counter() - t0) / iters
+
+    broken = None
     for b in CALIB_SIZES:
         n = b // esize
         if n >= x.numel():
             continue
         xv, yv = x[:n], y[:n]
         iters = max(5, min(50, int(2e8 // b)))
-        for s in specs:
+        # the latency protocols join at the sizes they are built for
+        extra = [s for s in (["ll", "oneshot"] if b <= (1 << 20) else ["oneshot"] if b <= (8 << 20) else [])
+                 if s not in timings]
+        best, best_t = None, float("inf")
+        for s in list(timings) + extra:
+            # local first call + check (a failure on any rank is agreed on before anything collective)
+            failed, err = 0.0, 0.0
             try:
                 comm.all_reduce(xv, out=yv, op=op, algo=s)
                 torch.cuda.synchronize()
-                if world > 1:
-                    dist.barrier()
-                t0 = time.perf_counter()
-                for _ in range(iters):
-                    comm.all_reduce(xv, out=yv, op=op, algo=s)
-                torch.cuda.synchronize()
                 comm.check()
-                t = max_over_ranks(time.perf_counter() - t0) / iters
-            except Exception as e:  # noqa: BLE001 - a spec failing at a small size is reported, not fatal
-                log(rank, f"calibration: {s} at {b} B failed: {e}")
-                return {"error": f"{s} at {b} B: {e}"}
-            rows.append({"spec": s, "bytes": b, "us": t * 1e6})
+                ok, err = verify(yv, n)
+                failed = 0.0 if ok else 0.5
+            except Exception as e:  # noqa: BLE001 - reported in the JSON line
+                log(rank, f"calibration: {s} at {b} B failed on this rank: {e}")
+                failed = 1.0
+            failed = max_over_ranks(failed)
+            if failed:
+                wrong.append(f"{s}@{b}" + (" (error)" if failed >= 1.0 else f" (rel err {err:.3g})"))
+                if failed >= 1.0:  # the communicator may be inconsistent now: the caller rebuilds it
+                    broken = f"{s} at {b} B"
+                    break
+                continue
+            t = t_of(lambda: comm.all_reduce(xv, out=yv, op=op, algo=s), iters)
+            if "+rccl" not in s and nv.model_features(s, world, float(b), links) is not None:
+                rows.append({"spec": s, "bytes": b, "us": t * 1e6})
+            if t < best_t:
+                best, best_t = s, t
+        if broken:
+            break
+        row = {"bytes": b, "flexar_best": best, "flexar_us": round(best_t * 1e6, 1) if best else None,
+               "flexar_busbw": round(busbw_gbps(b, best_t, world), 2) if best else None}
+        if with_rccl:
+            z = xv.clone()
+            tr = t_of(lambda: dist.all_reduce(z), iters)
+            row.update(rccl_us=round(tr * 1e6, 1), rccl_busbw=round(busbw_gbps(b, tr, world), 2))
+        table.append(row)
+        log(rank, "calibration sweep", json.dumps(row))
+    out = {"sweep_vs_rccl": table, "wrong": wrong or None, "broken": broken}
     try:
         fit = fit_model(rows, world, links)
     except ValueError as e:
-        return {"error": str(e)}
-    feats = {s: nv.model_features(s, world, float(nbytes), links) for s in specs}
+        out["error"] = str(e)
+        return out
+    feats = {s: nv.model_features(s, world, float(nbytes), links) for s in model_specs}
     theta = (fit["alpha_launch_us"], fit["alpha_sync_us"], 1.0 / fit["link_gbps"], 1.0 / fit["hbm_gbps"])
-    pick = min(specs, key=lambda s: sum(f * t for f, t in zip(feats[s], theta)))
+    pick = min(model_specs, key=lambda s: sum(f * t for f, t in zip(feats[s], theta)))
     best = min(timings, key=timings.get)
-    out = {"FLEXAR_MODEL": fit["FLEXAR_MODEL"], "rows": fit["rows"], "median_rel_err": round(fit["median_rel_err"], 3),
-           "max_rel_err": round(fit["max_rel_err"], 3), "winner_agreement": round(fit["winner_agreement"], 2),
-           "fitted_choice": pick, "fitted_choice_us": round(timings[pick] * 1e6, 1),
-           "tuner_best": best, "tuner_best_us": round(timings[best] * 1e6, 1),
-           "sizes": fit["sizes"]}
+    out.update({"FLEXAR_MODEL": fit["FLEXAR_MODEL"], "rows": fit["rows"],
+                "median_rel_err": round(fit["median_rel_err"], 3), "max_rel_err": round(fit["max_rel_err"], 3),
+                "winner_agreement": round(fit["winner_agreement"], 2),
+                "fitted_choice": pick, "fitted_choice_us": round(timings[pick] * 1e6, 1),
+                "tuner_best": best, "tuner_best_us": round(timings[best] * 1e6, 1), "sizes": fit["sizes"]})
     log(rank, f"calibration: FLEXAR_MODEL={fit['FLEXAR_MODEL']} median rel err {out['median_rel_err']}, "
               f"fitted choice {pick} ({out['fitted_choice_us']} us) vs tuner best {best} ({out['tuner_best_us']} us)")
     return out
