@@ -95,6 +95,11 @@ def _sig(lib):
         "flexar_rccl_unique_id": (i, [vp, sz]),
         "flexar_comm_init_msg": (i, [vp, vp]),
         "flexar_comm_connect_msg_only": (i, [vp]),
+        "flexar_reg_handle_size": (sz, []),
+        "flexar_reg_export": (i, [vp, vp, sz, vp]),
+        "flexar_reg_open": (i, [vp, vp, sz, vp, c.POINTER(i)]),
+        "flexar_reg_close": (i, [vp, i]),
+        "flexar_reg_count": (i, [vp]),
         "flexar_model_features": (i, [cp, i, d, i, c.POINTER(d)]),
         "flexar_kernel_info": (i, [i, i, i, i, c.POINTER(i), c.POINTER(i)]),
         "flexar_downgrade_spec": (i, [cp, i, u32, i, cp, sz]),

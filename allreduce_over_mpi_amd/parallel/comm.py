@@ -119,6 +119,8 @@ class Communicator:
         self._hi = int(h.value or 0)  # the handle as an int, for the fast-call path
         self.selftest_failed = []
         self.transport_note = None
+        self._exchange = None
+        self._regs = {}
         if self.world_size > 1:
             hs = int(self._lib.flexar_handle_size())
             buf = ctypes.create_string_buffer(hs)
@@ -128,6 +130,7 @@ class Communicator:
                     gathered = [None] * self.world_size
                     dist.all_gather_object(gathered, data, group=group)
                     return gathered
+            self._exchange = exchange
             allb = b"".join(exchange(bytes(buf.raw)))
             transport = transport or os.environ.get("FLEXAR_TRANSPORT", "auto")
             if transport not in ("auto", "ipc", "rccl"):
@@ -290,6 +293,40 @@ class Communicator:
         nv.check(self._lib.flexar_comm_stats(self._h, b, 1 << 16), "comm_stats")
         return json.loads(b.value.decode())
 
+    # ------------------------------------------------------------------ registered buffers
+    def register(self, tensor) -> int:
+        """Register a device buffer for zero-copy allreduce (algorithm suffix "+zc", e.g. "flat+zc"): the
+        flat schedule then reads every peer's input and output straight over IPC, with no staging copies.
+        Collective: every rank registers its corresponding tensor (same byte size), in the same order.
+        The communicator holds a reference until :meth:`deregister`. A "+zc" call takes tensors that lie
+        inside registrations, at the same offset on every rank (DDP buckets, FSDP flat parameters)."""
+        _require_cuda(tensor)
+        nbytes = tensor.numel() * tensor.element_size()
+        blob = ctypes.create_string_buffer(int(self._lib.flexar_reg_handle_size()))
+        rc = self._lib.flexar_reg_export(self._h, tensor.data_ptr(), nbytes, blob)
+        err = nv.last_error() if rc else ""
+        rows = [bytes(blob.raw) if rc == 0 else b""]
+        if self.world_size > 1:
+            rows = self._exchange(rows[0])
+            if any(not r for r in rows):  # every rank agrees before anything is mapped
+                raise nv.FlexarError(rc or 1, f"register: export failed on rank(s) "
+                                              f"{[i for i, r in enumerate(rows) if not r]} {err}".rstrip())
+        rid = ctypes.c_int(0)
+        rc = self._lib.flexar_reg_open(self._h, tensor.data_ptr(), nbytes, b"".join(rows), ctypes.byref(rid))
+        msg = b"" if rc == 0 else f"rank {self.rank}: {nv.last_error()}".encode()
+        bad = [m.decode(errors="replace") for m in (self._exchange(msg) if self.world_size > 1 else [msg]) if m]
+        if bad:
+            if rc == 0:
+                self._lib.flexar_reg_close(self._h, rid.value)
+            raise nv.FlexarError(rc or 1, "register: " + "; ".join(bad))
+        self._regs[rid.value] = tensor
+        return rid.value
+
+    def deregister(self, rid: int):
+        """Drop a registration (every rank, once the calls using it have completed)."""
+        nv.check(self._lib.flexar_reg_close(self._h, int(rid)), "deregister")
+        self._regs.pop(int(rid), None)
+
     # ------------------------------------------------------------------ collectives
     def all_reduce(self, tensor, op="sum", out=None, algo: Optional[str] = None, scale: float = 1.0, stream=None):
         """Allreduce ``tensor`` (in place unless ``out`` is given). Returns the result tensor."""
@@ -392,8 +429,9 @@ class Communicator:
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
             self._hi = 0
-            self._lib.flexar_comm_destroy(self._h)
+            self._lib.flexar_comm_destroy(self._h)  # also closes the registrations' peer mappings
             self._h = ctypes.c_void_p()
+            self._regs = {}
 
     def __del__(self):
         try:

@@ -156,6 +156,17 @@ int flexar_rccl_unique_id(void* out, size_t len);                       /* rank 
 int flexar_comm_init_msg(flexar_comm_t comm, const void* unique_id);    /* collective */
 int flexar_comm_connect_msg_only(flexar_comm_t comm);                   /* no IPC: all calls over RCCL */
 uint32_t flexar_comm_disabled(flexar_comm_t comm);
+/* Registered buffers for zero-copy allreduce (algorithm suffix "+zc", flat schedule): the reduce-scatter
+ * reads every peer's input and the all-gather every peer's output directly over IPC, with no staging.
+ * Registration is collective: every rank exports its buffer of the same size (flexar_reg_export), the
+ * blobs are all-gathered rank-major, and every rank opens them (flexar_reg_open). A "+zc" call then takes
+ * buffers that lie inside registrations, at the same offsets on every rank. */
+#define FLEXAR_REG_HANDLE_BYTES 128
+size_t flexar_reg_handle_size(void);
+int flexar_reg_export(flexar_comm_t comm, const void* ptr, size_t bytes, void* out);
+int flexar_reg_open(flexar_comm_t comm, const void* ptr, size_t bytes, const void* all_blobs, int* id_out);
+int flexar_reg_close(flexar_comm_t comm, int id);
+int flexar_reg_count(flexar_comm_t comm);
 /* JSON: per-peer PCI bus id, device ordinal, link class (same-device / xgmi / pcie / unknown) and hop
  * count from the connect-time probe; links used by the cost model; self-test state. */
 int flexar_comm_topology(flexar_comm_t comm, char* buf, size_t buflen);

@@ -31,6 +31,7 @@ struct HostExecCtx {
   float pre = 1.0f, post_inv = 1.0f;  // typed programs, fp8 wire: pre-scale s and 1/s
   char* local[BUF_COUNT] = {nullptr, nullptr, nullptr};  // IN, OUT, STG of this rank
   std::vector<char*> peer_stg;                          // per rank (self = local STG)
+  std::vector<char*> peer_io[2];                        // zero-copy programs: every rank's IN / OUT
   std::vector<std::atomic<uint64_t>*> peer_flags;       // per rank flag arrays
   uint32_t ranks_stride = 0, blocks_stride = 0;         // flag layout strides
   uint64_t stg_half_bytes = 0;                          // parity offset
@@ -122,6 +123,7 @@ struct HostExec {
     const uint64_t par = (epoch & 1) ? c.stg_half_bytes : 0;
     auto addr = [&](const Loc& l) -> char* {
       if (l.buf == BUF_STG) return c.peer_stg[l.rank] + par + l.off * unit;
+      if (l.rank != c.rank) return c.peer_io[l.buf][l.rank] + l.off * sizeof(T);  // registered peer buffer
       return c.local[l.buf] + l.off * sizeof(T);
     };
     auto esz = [&](const Loc& l) -> uint64_t { return (l.pad & 1) ? P.wsize : sizeof(T); };

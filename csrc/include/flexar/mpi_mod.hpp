@@ -272,6 +272,7 @@ inline int resolve_algo(HostComm& h, double bytes, AlgoSpec* s) {
   if (s->kind == AlgoKind::DMA) s->kind = AlgoKind::TREE, s->widths = {h.size};  // copy engines: device only
   if (s->kind == AlgoKind::TREE && (!h.shared || s->ag == AgMode::AUTO)) s->ag = AgMode::PUSH;
   s->wire = 0;  // typed staging is a device-executor feature: the host engines run the dtype throughout
+  s->zc = false;  // so are registered (zero-copy) device buffers
   return 0;
 }
 

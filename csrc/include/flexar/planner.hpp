@@ -48,6 +48,8 @@ struct Program {
   int wire = 0;
   uint32_t wsize = 0;
   uint32_t unit = 0;
+  // zero-copy program (AlgoSpec::zc): IN / OUT operands of other ranks address their registered buffers
+  bool zc = false;
   std::string desc;
   uint32_t stg_unit() const { return unit ? unit : esize; }
   uint64_t stg_bytes() const { return stg_elems * stg_unit(); }
@@ -80,6 +82,14 @@ class Planner {
       if (count) xfer(count, {loc(BUF_IN, r, 0)}, {loc(BUF_OUT, r, 0)}, scale);
       finish_channel();
       P->desc = "copy";
+    } else if (spec.zc) {
+      if (wire || spec.msg || !(spec.kind == AlgoKind::TREE && spec.widths.size() == 1 && spec.widths[0] == (int)N)) {
+        if (err) *err = "zero-copy (+zc) runs the flat schedule over IPC-registered buffers (no wire type, no +rccl)";
+        return false;
+      }
+      build_flat_zc();
+      P->zc = true;
+      P->desc = spec.str();
     } else if (wire >= 2 && !(spec.kind == AlgoKind::TREE && spec.widths.size() == 1 && spec.widths[0] == (int)N)) {
       if (err) *err = "fp8 wire compression needs the flat schedule (one quantisation per contribution)";
       return false;
@@ -664,6 +674,37 @@ class Planner {
     }
   }
 
+  // Zero-copy flat allreduce over registered buffers ("+zc"): no staging and no copies into it. Rank k
+  // reduces block k straight from every rank's IN (remote loads over xGMI; rank order, so every owner
+  // sums in the same order) into its own OUT, then copies every other block from its owner's OUT. The
+  // reference's flat exchange (mpi_mod.hpp:952-1111 with one stage of width N) moves the same bytes
+  // through send/recv buffers; here each byte crosses a link once per phase and touches HBM twice less.
+  // Three hand-offs, per workgroup like every flag: slot 0 "my IN is final" (every rank has entered the
+  // call), slot 1 "my block is reduced" (and I have read your IN), slot 2 "I have read your OUT". The last
+  // one keeps a rank in the call until no peer can still read its buffers, so its caller may overwrite
+  // them as soon as the call completes on its stream. In place (IN == OUT) is safe: a rank writes a
+  // peer's block into its OUT only after slot 1, when every peer has finished reading that rank's IN.
+  void build_flat_zc() {
+    const uint64_t split = round_up((count + N - 1) / N);
+    auto boff = [&](uint32_t k) { return (uint64_t)k * split; };
+    auto blen = [&](uint32_t k) -> uint64_t {
+      const uint64_t s = boff(k);
+      return s >= count ? 0 : std::min(split, count - s);
+    };
+    auto peers = rotated_peers();
+    signal(peers, 0);
+    wait(peers, 0);
+    std::vector<Loc> srcs;
+    for (uint32_t p = 0; p < N; ++p) srcs.push_back(loc(BUF_IN, p, boff(r)));
+    xfer(blen(r), srcs, {loc(BUF_OUT, r, boff(r))}, scale);
+    signal(peers, 1);
+    wait(peers, 1);
+    for (uint32_t p : peers) xfer(blen(p), {loc(BUF_OUT, p, boff(p))}, {loc(BUF_OUT, r, boff(p))}, 1.0f);
+    signal(peers, 2);
+    wait(peers, 2);
+    finish_channel();
+  }
+
   // ------------------------------------------------------------------ reduce-scatter / all-gather
   std::vector<uint32_t> rotated_peers() const {
     std::vector<uint32_t> v;
@@ -887,7 +928,7 @@ inline bool validate_program(const Program& P, uint32_t N, uint32_t rank, uint64
     if (l.rank >= N || l.buf >= BUF_COUNT) return false;
     if (l.pad > 2 || (l.pad && (!P.wire || l.buf != BUF_STG))) return false;
     if (l.buf == BUF_STG) return l.off + P.extent(l, len) <= P.stg_elems;
-    if (l.rank != rank) return false;  // a caller buffer is never addressed on a peer
+    if (l.rank != rank && !P.zc) return false;  // a caller buffer is addressed on a peer only when registered
     return l.off + len <= (l.buf == BUF_IN ? in_elems : out_elems);
   };
   for (size_t i = 0; i < P.ops.size(); ++i) {

@@ -47,6 +47,10 @@ struct AlgoSpec {
   // message transport ("+rccl"): the schedule's transfers as grouped ncclSend / ncclRecv between local
   // executor segments (msg_plan.hpp) instead of peer-memory access over IPC
   bool msg = false;
+  // zero-copy ("+zc", flat only): the reduce-scatter reads every peer's INPUT and the all-gather every
+  // peer's OUTPUT directly over IPC (buffers registered with flexar_reg_*), no staging copies; a closing
+  // hand-off keeps each rank in the call until its peers have finished reading its buffers
+  bool zc = false;
 
   std::string str() const {
     std::ostringstream ss;
@@ -71,6 +75,7 @@ struct AlgoSpec {
     if (wire == 3) ss << "+e5m2";
     if (round_wire) ss << "+rw";
     if (msg) ss << "+rccl";
+    if (zc) ss << "+zc";
     return ss.str();
   }
 };
@@ -199,6 +204,7 @@ inline bool parse_algo(const std::string& raw, int nranks, AlgoSpec* spec, std::
     else if (mod == "e5m2") spec->wire = 3;
     else if (mod == "rw") spec->round_wire = true;
     else if (mod == "rccl" || mod == "msg") spec->msg = true;
+    else if (mod == "zc") spec->zc = true;
     else { if (err) *err = "unknown algorithm modifier '+" + mod + "'"; return false; }
   }
   std::string head = s, arg;
@@ -244,11 +250,12 @@ inline bool parse_algo(const std::string& raw, int nranks, AlgoSpec* spec, std::
   if (head == "ft") {
     const char* env = getenv("FT_TOPO");
     AgMode ag = spec->ag; bool fuse = spec->fuse, nts = spec->nts, wt = spec->wt, rw = spec->round_wire;
-    bool msg = spec->msg;
+    bool msg = spec->msg, zc = spec->zc;
     int wire = spec->wire;
     if (!parse_ft_topo(!arg.empty() ? arg.c_str() : env, nranks, spec, err)) return false;
     spec->ag = ag; spec->fuse = fuse; spec->nts = nts; spec->wt = wt; spec->wire = wire; spec->round_wire = rw;
     spec->msg = msg;
+    spec->zc = zc;
     return true;
   }
   if (err) *err = "unknown algorithm '" + raw + "'";

@@ -79,6 +79,8 @@ struct SimRun {
       for (int p = 0; p < nranks; ++p) {
         c.peer_stg.push_back(stg[p].data());
         c.peer_flags.push_back(flags[p].get());
+        c.peer_io[BUF_IN].push_back(in_place ? (char*)outputs[p] : (char*)inputs[p]);
+        c.peer_io[BUF_OUT].push_back((char*)outputs[p]);
       }
       c.ranks_stride = nranks;
       c.blocks_stride = grid;

@@ -242,6 +242,14 @@ struct flexar_comm {
   char* msg_ws = nullptr;
   size_t msg_ws_bytes = 0;
   std::map<std::string, std::unique_ptr<DevMsgPlan>> msg_cache;
+  // registered caller buffers (zero-copy "+zc"): every rank registered its buffer of the same size in
+  // the same order; peer[p] is rank p's buffer mapped into this process. IPC mappings of one peer
+  // allocation are shared by every registration inside it (torch's allocator carves tensors out of
+  // larger segments).
+  struct Reg { int id; char* base; size_t bytes; bool aligned; char* peer[kMaxRanks]; std::string key[kMaxRanks]; };
+  std::vector<Reg> regs;
+  int next_reg = 1;
+  std::map<std::string, std::pair<char*, int>> ipc_maps;  // (peer, handle) -> mapped base, references
   int* st_buf = nullptr;        // self-test buffers (device)
   uint32_t* st_bad = nullptr;   // self-test mismatch counter (host-mapped)
   uint32_t* st_bad_dev = nullptr;
@@ -409,6 +417,28 @@ static int get_program(flexar_comm* c, const AlgoSpec& s, uint64_t count, uint32
 }
 
 static int proto_of(const AlgoSpec& s) { return s.wt ? PM_WT : s.nts ? PM_FENCE_NTS : PM_FENCE; }
+
+// Zero-copy program: the peers' buffers of this call. `in` / `out` must lie inside registrations; every
+// rank passes the same offsets into its corresponding registration (the registration contract, like
+// NCCL's registered buffers), so rank p's operand is its registered base + the same offset.
+static int zc_bind(flexar_comm* c, const void* in, const void* out, uint64_t bytes, DevCtx* x) {
+  const void* ptrs[2] = {in, out};
+  for (int b = 0; b < 2; ++b) {
+    const char* q = (const char*)ptrs[b];
+    const flexar_comm::Reg* g = nullptr;
+    for (const auto& r : c->regs)
+      if (q >= r.base && q + bytes <= r.base + r.bytes) { g = &r; break; }
+    if (!g) {
+      set_error(std::string("zero-copy (+zc) needs registered buffers: the ") + (b ? "output" : "input") +
+                " is not inside a registration (Communicator.register / flexar_reg_open)");
+      return FLEXAR_ERR_INVALID;
+    }
+    const uint64_t d = (uint64_t)(q - g->base);
+    for (int p = 0; p < c->nranks; ++p) x->peer_io[b][p] = p == c->rank ? (char*)q : g->peer[p] + d;
+    if (!g->aligned || (d & 15)) x->vec_ok = 0;
+  }
+  return 0;
+}
 
 static int choose_grid(flexar_comm* c, uint64_t bytes, uint32_t nchan) {
   int g = c->grid_override;
@@ -1311,6 +1341,131 @@ int flexar_comm_connect_msg_only(flexar_comm_t c) {
   return 0;
 }
 
+// ---- registered buffers (zero-copy "+zc") --------------------------------------------------------
+// Registration blob: the IPC handle of the allocation holding the buffer and the buffer's place in it.
+struct RegBlob {
+  hipIpcMemHandle_t h;
+  uint64_t offset;  // buffer start - allocation base
+  uint64_t bytes;
+  int32_t device, pad;
+};
+static_assert(sizeof(RegBlob) <= FLEXAR_REG_HANDLE_BYTES, "registration blob size");
+
+size_t flexar_reg_handle_size(void) { return FLEXAR_REG_HANDLE_BYTES; }
+
+int flexar_reg_export(flexar_comm_t c, const void* ptr, size_t bytes, void* out) {
+  if (!c || !ptr || !out || !bytes) { set_error("null argument"); return FLEXAR_ERR_INVALID; }
+  FX_HIP(hipSetDevice(c->device));
+  RegBlob b;
+  memset(&b, 0, sizeof(b));
+  if (c->nranks > 1 && !c->group_member) {
+    void* base = nullptr;
+    size_t size = 0;
+    FX_HIP(hipMemGetAddressRange(&base, &size, const_cast<void*>(ptr)));
+    if ((const char*)ptr + bytes > (const char*)base + size) {
+      set_error("registered range exceeds its allocation");
+      return FLEXAR_ERR_INVALID;
+    }
+    FX_HIP(hipIpcGetMemHandle(&b.h, base));
+    b.offset = (uint64_t)((const char*)ptr - (const char*)base);
+  }
+  b.bytes = bytes;
+  b.device = c->device;
+  memset(out, 0, FLEXAR_REG_HANDLE_BYTES);
+  memcpy(out, &b, sizeof(b));
+  return 0;
+}
+
+// Collective in effect: every rank opens the blobs of all ranks (rank-major, flexar_reg_handle_size()
+// bytes each) for its own buffer of the same size.
+int flexar_reg_open(flexar_comm_t c, const void* ptr, size_t bytes, const void* all, int* id_out) {
+  if (!c || !ptr || !all || !id_out) { set_error("null argument"); return FLEXAR_ERR_INVALID; }
+  if (!c->connected && c->nranks > 1) { set_error("communicator not connected"); return FLEXAR_ERR_STATE; }
+  if (c->nranks > 1 && !c->ipc) { set_error("zero-copy needs IPC peer access (this communicator runs RCCL messages)"); return FLEXAR_ERR_UNSUPPORTED; }
+  std::lock_guard<std::mutex> lk(c->mu);
+  FX_HIP(hipSetDevice(c->device));
+  flexar_comm::Reg g;
+  g.id = c->next_reg++;
+  g.base = (char*)ptr;
+  g.bytes = bytes;
+  g.aligned = ((uintptr_t)ptr & 15) == 0;
+  for (int p = 0; p < kMaxRanks; ++p) g.peer[p] = nullptr;
+  std::vector<std::string> opened;
+  auto undo = [&]() {
+    for (const std::string& k : opened) {
+      auto it = c->ipc_maps.find(k);
+      if (it != c->ipc_maps.end() && --it->second.second == 0) {
+        (void)hipIpcCloseMemHandle(it->second.first);
+        c->ipc_maps.erase(it);
+      }
+    }
+  };
+  for (int p = 0; p < c->nranks; ++p) {
+    RegBlob b;
+    memcpy(&b, (const char*)all + (size_t)p * FLEXAR_REG_HANDLE_BYTES, sizeof(b));
+    if (b.bytes != bytes) {
+      undo();
+      set_error("rank " + std::to_string(p) + " registered " + std::to_string(b.bytes) + " bytes, this rank " +
+                std::to_string(bytes) + " (corresponding buffers must have the same size)");
+      return FLEXAR_ERR_INVALID;
+    }
+    if (p == c->rank) { g.peer[p] = (char*)ptr; continue; }
+    if (b.offset & 15) g.aligned = false;
+    const std::string key = std::to_string(p) + ":" + std::string((const char*)&b.h, sizeof(b.h));
+    auto it = c->ipc_maps.find(key);
+    char* mapped = nullptr;
+    if (it != c->ipc_maps.end()) {
+      mapped = it->second.first;
+      it->second.second++;
+    } else {
+      void* q = nullptr;
+      hipError_t e = hipIpcOpenMemHandle(&q, b.h, hipIpcMemLazyEnablePeerAccess);
+      if (e != hipSuccess) {
+        undo();
+        set_error("registering: mapping rank " + std::to_string(p) + "'s buffer failed: hipIpcOpenMemHandle: " +
+                  hipGetErrorString(e));
+        return FLEXAR_ERR_HIP;
+      }
+      mapped = (char*)q;
+      c->ipc_maps[key] = {mapped, 1};
+    }
+    opened.push_back(key);
+    g.key[p] = key;
+    g.peer[p] = mapped + b.offset;
+  }
+  c->regs.push_back(g);
+  *id_out = g.id;
+  logf(LOG_INFO, c->rank, "registered buffer %d: %zu bytes (%zu registrations, %zu peer mappings)", g.id, bytes,
+       c->regs.size(), c->ipc_maps.size());
+  return 0;
+}
+
+// Drop a registration (every rank, after the calls using it completed): its peer mappings are closed
+// once no other registration uses them.
+int flexar_reg_close(flexar_comm_t c, int id) {
+  if (!c) return FLEXAR_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  for (size_t i = 0; i < c->regs.size(); ++i) {
+    if (c->regs[i].id != id) continue;
+    FX_HIP(hipSetDevice(c->device));
+    FX_HIP(hipDeviceSynchronize());  // no call of ours still reads through the mappings
+    for (int p = 0; p < c->nranks; ++p) {
+      auto it = c->ipc_maps.find(c->regs[i].key[p]);
+      if (p == c->rank || it == c->ipc_maps.end()) continue;
+      if (--it->second.second == 0) {
+        (void)hipIpcCloseMemHandle(it->second.first);
+        c->ipc_maps.erase(it);
+      }
+    }
+    c->regs.erase(c->regs.begin() + (long)i);
+    return 0;
+  }
+  set_error("no registration " + std::to_string(id));
+  return FLEXAR_ERR_INVALID;
+}
+
+int flexar_reg_count(flexar_comm_t c) { return c ? (int)c->regs.size() : -1; }
+
 int flexar_comm_set_model(flexar_comm_t c, double alpha_launch_us, double alpha_sync_us, double link_gbps,
                           double hbm_gbps, int links) {
   if (!c || !(link_gbps > 0) || !(hbm_gbps > 0) || alpha_launch_us < 0 || alpha_sync_us < 0) {
@@ -1371,6 +1526,9 @@ int flexar_comm_destroy(flexar_comm_t c) {
       (void)hipIpcCloseMemHandle(c->peer_stg[r]);
       (void)hipIpcCloseMemHandle(c->peer_flags[r]);
     }
+  for (auto& kv : c->ipc_maps) (void)hipIpcCloseMemHandle(kv.second.first);
+  c->ipc_maps.clear();
+  c->regs.clear();
   for (int r = 0; r < kMaxRanks; ++r) {
     if (c->dma_st[r]) (void)hipStreamDestroy(c->dma_st[r]);
     if (c->dma_ag[r]) (void)hipStreamDestroy(c->dma_ag[r]);
@@ -1581,6 +1739,7 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     LaunchArgs la;
     la.kind = LAUNCH_EXEC;
     fill_ctx(c, dp, in, out, &la.ctx);
+    if (dp->prog.zc && (rc = zc_bind(c, in, out, (uint64_t)count * es, &la.ctx))) return rc;
     la.grid = hit ? m.grid : choose_grid(c, count * es, dp->prog.nchan);
     la.stream = st;
     la.proto = proto_of(s);
@@ -1612,6 +1771,7 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     if ((rc = get_program(c, s, n, es, fs, &dp))) return rc;
     DevCtx x;
     fill_ctx(c, dp, (const char*)in + off * es, (char*)out + off * es, &x);
+    if (dp->prog.zc && (rc = zc_bind(c, (const char*)in + off * es, (char*)out + off * es, n * es, &x))) break;
     int grid = choose_grid(c, n * es, dp->prog.nchan);
     LaunchArgs la;
     la.kind = LAUNCH_EXEC;
@@ -1892,6 +2052,12 @@ static int group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
       if (rc) return rc;
       const char* in = ins && ins[r] ? (const char*)ins[r] : (const char*)outs[r];
       fill_ctx(comms[r], dp, in + off * es, (char*)outs[r] + off * es, &h[r]);
+      if (dp->prog.zc)  // one process: every rank's buffers are plain device pointers, no registration
+        for (int p = 0; p < nranks; ++p) {
+          h[r].peer_io[BUF_IN][p] = (char*)(ins && ins[p] ? ins[p] : outs[p]) + off * es;
+          h[r].peer_io[BUF_OUT][p] = (char*)outs[p] + off * es;
+          if ((((uintptr_t)h[r].peer_io[BUF_IN][p]) | ((uintptr_t)h[r].peer_io[BUF_OUT][p])) & 15) h[r].vec_ok = 0;
+        }
       if (amax_parts) h[r].amax_parts = amax_parts[r];
       wire = dp->prog.wire;
       int g = choose_grid(comms[r], n * es, dp->prog.nchan);

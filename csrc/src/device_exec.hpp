@@ -36,6 +36,7 @@ struct DevCtx {
   char* local[BUF_COUNT];          // IN, OUT, STG (this rank)
   char* peer_stg[kMaxRanks];       // IPC-mapped staging of every rank (self = local)
   uint64_t* peer_flags[kMaxRanks]; // IPC-mapped flag arrays of every rank (self = local)
+  char* peer_io[2][kMaxRanks];     // zero-copy programs: every rank's registered IN / OUT for this call
   uint64_t* epochs;                // [kMaxGridBlocks] per-workgroup call counter (local)
   uint64_t stg_half_bytes;         // parity offset (calls alternate staging halves)
   uint32_t* err;                   // device pointer of a host-mapped error word
@@ -274,6 +275,12 @@ __device__ FX_INLINE void st_flag(uint64_t* f, uint64_t v) {
   __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Caller-buffer operand: this rank's IN / OUT, or a peer's registered one (zero-copy programs only; the
+// planner addresses peer IN / OUT nowhere else, planner.hpp validate_program)
+__device__ FX_INLINE char* io_base(const DevCtx& c, const Loc& l) {
+  return l.rank == c.rank ? c.local[l.buf] : c.peer_io[l.buf][l.rank];
+}
+
 template <typename T, typename OP, int PM>
 __device__ FX_INLINE void xfer_op(const DevCtx& c, const Op* o, uint32_t lb, uint32_t nb, uint32_t quantum,
                                   uint64_t par) {
@@ -289,7 +296,7 @@ __device__ FX_INLINE void xfer_op(const DevCtx& c, const Op* o, uint32_t lb, uin
     s[k] = nullptr;
     if (k < ns) {
       const Loc l = o->src[k];
-      char* base = (l.buf == BUF_STG) ? c.peer_stg[l.rank] + par : c.local[l.buf];
+      char* base = (l.buf == BUF_STG) ? c.peer_stg[l.rank] + par : io_base(c, l);
       s[k] = base + (l.off + lo) * sizeof(T);
       vec &= (l.buf == BUF_STG) || c.vec_ok;
     }
@@ -299,7 +306,7 @@ __device__ FX_INLINE void xfer_op(const DevCtx& c, const Op* o, uint32_t lb, uin
     d[k] = nullptr;
     if (k < nd) {
       const Loc l = o->dst[k];
-      char* base = (l.buf == BUF_STG) ? c.peer_stg[l.rank] + par : c.local[l.buf];
+      char* base = (l.buf == BUF_STG) ? c.peer_stg[l.rank] + par : io_base(c, l);
       d[k] = base + (l.off + lo) * sizeof(T);
       vec &= (l.buf == BUF_STG) || c.vec_ok;
     }

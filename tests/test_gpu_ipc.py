@@ -546,3 +546,79 @@ def test_ipc_connect_readiness_gate(cuda, fault):
         else:
             assert failed == [] and stats["disabled"] == ""
         assert all(e == 0 for e in errs.values()), errs
+
+
+def _zc_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
+                          FLEXAR_TIMEOUT_MS="20000")
+        import torch.distributed as dist
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from allreduce_over_mpi_amd.parallel import Communicator
+
+        comm = Communicator(workspace_bytes=32 << 20)
+        dev = torch.device("cuda", 0)
+        n = 1 << 20
+        # two tensors carved out of one allocation (torch's allocator does this): one peer mapping serves both
+        arena = torch.empty(2 * n + 64, device=dev)
+        x, y = arena[:n], arena[n + 64:2 * n + 64]
+        rx, ry = comm.register(x), comm.register(y)
+        errs = {}
+        for spec in ("flat+zc", "flat+zc+wt", "flat+zc+nts"):
+            for size in (7, 4096, 300001, n):
+                for call in range(3):  # consecutive calls: a peer still reading the last call would show
+                    src = torch.randn(size, generator=torch.Generator().manual_seed(1000 * rank + size + call))
+                    x[:size].copy_(src.to(dev))
+                    comm.all_reduce(x[:size], out=y[:size], algo=spec)
+                    torch.cuda.synchronize()
+                refs = [torch.randn(size, generator=torch.Generator().manual_seed(1000 * r + size + 2)) for r in range(world)]
+                ref = torch.stack(refs).double().sum(0)
+                errs[(spec, size)] = (y[:size].double().cpu() - ref).abs().max().item()
+        # in place, at an offset inside the registration (the same offset on every rank)
+        x[100:100 + 5003].fill_(float(rank + 1))
+        comm.all_reduce(x[100:100 + 5003], algo="flat+zc")
+        torch.cuda.synchronize()
+        errs["in_place"] = (x[100:100 + 5003] - world * (world + 1) / 2).abs().max().item()
+        # an unregistered buffer is refused, not read through a stale mapping
+        try:
+            comm.all_reduce(torch.ones(64, device=dev), algo="flat+zc")
+            errs["unregistered"] = "accepted"
+        except Exception as e:  # noqa: BLE001
+            errs["unregistered"] = "refused" if "registered" in str(e) else str(e)
+        comm.deregister(rx)
+        comm.deregister(ry)
+        errs["regs_left"] = comm._lib.flexar_reg_count(comm._h)
+        comm.check()
+        comm.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, errs, None))
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ipc_zero_copy_registered_buffers(cuda, world):
+    """"+zc": every rank reads its peers' registered input / output through IPC mappings (no staging)."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_zc_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, errs, tb in res:
+        assert tb is None, f"rank {rank} failed:\n{tb}"
+        assert errs.pop("unregistered") == "refused"
+        assert errs.pop("regs_left") == 0
+        for key, err in errs.items():
+            assert err < 1e-4, (rank, key, err)

@@ -1,0 +1,53 @@
+"""Zero-copy flat allreduce over registered buffers ("+zc", planner.hpp build_flat_zc) on the CPU simulator.
+
+The program reads every peer's IN (reduce-scatter) and OUT (all-gather) directly - the device executor
+does the same through IPC-mapped registered buffers (comm.hip zc_bind, flexar_reg_*). Checked here:
+exact sums for every rank count including uneven tails and in-place calls, determinism across ranks,
+the program shape (no staging, three hand-offs), and that the spec is refused where it cannot run.
+"""
+import numpy as np
+import pytest
+
+from allreduce_over_mpi_amd import _native as nv
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 7, 8, 12, 16])
+@pytest.mark.parametrize("count", [1, 35, 4099, 10007])
+@pytest.mark.parametrize("spec", ["flat+zc", "flat+zc+wt", "flat+zc+nts"])
+def test_zero_copy_exact_sum(n, count, spec):
+    ins = [np.random.default_rng(7 * r + count).integers(-99, 99, count).astype(np.int32) for r in range(n)]
+    want = np.sum(ins, axis=0)
+    for o in nv.simulate(spec, ins, ncalls=3, grid=3):
+        np.testing.assert_array_equal(o, want)
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_zero_copy_in_place(n):
+    # IN == OUT: a rank overwrites its OUT blocks only after every peer finished reading its IN
+    ins = [np.random.default_rng(r).integers(-50, 50, 5003).astype(np.int32) for r in range(n)]
+    want = np.sum(ins, axis=0)
+    for o in nv.simulate("flat+zc", ins, ncalls=4, grid=4, in_place=True):
+        np.testing.assert_array_equal(o, want)
+
+
+def test_zero_copy_float_is_rank_order_deterministic():
+    n = 8
+    ins = [np.random.default_rng(r).standard_normal(9001).astype(np.float32) * (r + 1) for r in range(n)]
+    outs = nv.simulate("flat+zc", ins, grid=2, op="avg")
+    for o in outs[1:]:
+        assert np.array_equal(o, outs[0])  # the owner of each block sums in rank order; others copy it
+    np.testing.assert_allclose(outs[0], np.mean(np.stack(ins).astype(np.float64), axis=0), rtol=1e-5, atol=1e-5)
+
+
+def test_zero_copy_program_shape():
+    d = nv.plan_dump("flat+zc", 1, 4, 4096, "float32")
+    assert "staging 0 elems" in d and "3 flag slots" in d
+    assert "IN@0" in d and "OUT@2" in d  # peer buffers are addressed directly
+    assert "STG" not in d
+
+
+def test_zero_copy_refused_outside_flat():
+    ins = [np.zeros(64, np.int32) for _ in range(4)]
+    for spec in ("ring+zc", "rhd+zc", "tree:2,2+zc"):
+        with pytest.raises(nv.FlexarError):
+            nv.simulate(spec, ins)
