@@ -173,6 +173,24 @@ def main():
     x = x.to(dtype)
     y = torch.empty_like(x)
     xs = torch.empty_like(x)  # scaled copies of x for the stale-staging check
+    zc_note = None
+
+    def register_buffers(cm):
+        """Register x, xs and y for the zero-copy candidates ("+zc": the flat schedule reads the peers'
+        buffers over IPC, no staging). Collective; a failure on any rank drops the candidates everywhere."""
+        nonlocal zc_note
+        if world == 1 or not isinstance(cm, Communicator):
+            return False
+        try:
+            for t in (x, xs, y):
+                cm.register(t)
+            return True
+        except nv.FlexarError as e:
+            zc_note = f"registration failed: {e}"
+            log(rank, f"zero-copy candidates skipped: {e}")
+            return False
+
+    zc = register_buffers(comm)
 
     def max_over_ranks(v: float) -> float:
         if world == 1:
@@ -265,6 +283,8 @@ def main():
         cands = default_candidates(world, nbytes)
         if comm.topology().get("rccl"):  # the schedules over RCCL send/recv as well
             cands += ["flat+rccl", "ring+rccl"] + (["rhd+rccl"] if world > 2 and not world & (world - 1) else [])
+        if zc:  # registered buffers: the flat schedule straight from / to the peers' x and y
+            cands += ["flat+zc", "flat+zc+nts", "flat+zc+wt"]
         timings = {}
         for spec in cands:
             failed = 0.0
@@ -291,6 +311,7 @@ def main():
                 if isinstance(comm, RcclOnly):
                     fallback = "flexar communicator could not be rebuilt"
                     break
+                zc = register_buffers(comm)
                 continue
             timings[spec] = t
             tune_log[spec] = round(busbw_gbps(nbytes, t, world), 2)
@@ -304,6 +325,7 @@ def main():
                 comm = make_comm() or RcclOnly(dist)
                 if isinstance(comm, RcclOnly):
                     fallback = "flexar communicator could not be rebuilt"
+                zc = register_buffers(comm)
         if not timings or fallback:
             fallback = fallback or "no flexar algorithm produced correct results on this node"
             log(rank, f"tuner: {fallback}; measuring RCCL instead")
@@ -444,6 +466,7 @@ def main():
         "cost_model": model,
         "cost_model_fit": calib,
         "readiness": readiness,
+        "zero_copy": {"registered": zc, "note": zc_note} if world > 1 else None,
         "small_msg_8KiB_us_per_call": small,
     }
     if args.sweep:
