@@ -373,17 +373,41 @@ class FlexarHookState:
     """State for :func:`flexar_allreduce_hook`: a flexar Communicator over the DDP process group."""
 
     def __init__(self, process_group=None, algo: str | None = None, communicator: Communicator | None = None,
-                 grid: int | None = None):
+                 grid: int | None = None, zero_copy: bool | None = None):
         """``grid``: workgroups per executor launch (default: one per 32 KiB, at most 256 = one per CU).
         Gradient buckets are reduced while backward still runs; a smaller grid leaves CUs to the
-        backward kernels (the xGMI links, not the CUs, bound a bucket's allreduce)."""
+        backward kernels (the xGMI links, not the CUs, bound a bucket's allreduce).
+
+        ``zero_copy`` (default FLEXAR_HOOK_ZC=1): register every gradient bucket with the communicator the
+        first time it is seen (collective: every rank sees the buckets in the same order) and reduce it
+        with the zero-copy flat schedule ("flat+zc": peers read the bucket over IPC, no staging copies,
+        half the HBM traffic next to the backward kernels). A bucket whose storage changes (DDP rebuilds
+        its buckets after the first iteration) is re-registered and the old registration dropped."""
         self.comm = communicator or Communicator(group=process_group)
         self.algo = algo
         self.calls = 0
         self._streams = {}
+        if zero_copy is None:
+            zero_copy = os.environ.get("FLEXAR_HOOK_ZC", "0") == "1"
+        self.zero_copy = bool(zero_copy) and self.comm.world_size > 1 and hasattr(self.comm, "register")
+        self._bucket_regs = {}  # bucket index -> (data_ptr, nbytes, registration id)
         grid = grid if grid is not None else int(os.environ.get("FLEXAR_HOOK_GRID", "0") or 0)
         if grid and hasattr(self.comm, "set_grid"):
             self.comm.set_grid(grid)
+
+    def bucket_algo(self, bucket, buf):
+        """The algorithm for this bucket: "flat+zc" once the bucket is registered (zero_copy), else ``algo``."""
+        if not self.zero_copy or buf.data_ptr() % 16:
+            return self.algo
+        key = bucket.index()
+        nbytes = buf.numel() * buf.element_size()
+        have = self._bucket_regs.get(key)
+        if have is None or have[0] != buf.data_ptr() or have[1] != nbytes:
+            if have is not None:
+                self.comm.deregister(have[2])
+            self._bucket_regs[key] = (buf.data_ptr(), nbytes, self.comm.register(buf))
+        proto = "+wt" if self.algo and "+wt" in self.algo else "+nts" if self.algo and "+nts" in self.algo else ""
+        return "flat+zc" + proto
 
     def stream(self, dev):
         s = self._streams.get(dev.index)
@@ -398,12 +422,13 @@ def flexar_allreduce_hook(state, bucket):
     bucket with the flexar executor kernel (in place, on the current stream). (No annotations: this
     module uses postponed evaluation and DDP compares the annotation objects.)"""
     buf = bucket.buffer()
+    algo = state.bucket_algo(bucket, buf)  # (registration is collective: before any stream work)
     cur = torch.cuda.current_stream(buf.device)
     side = state.stream(buf.device)
     side.wait_stream(cur)
     with torch.cuda.stream(side):
         buf.record_stream(side)
-        state.comm.all_reduce(buf, op="avg" if buf.is_floating_point() else "sum", algo=state.algo)
+        state.comm.all_reduce(buf, op="avg" if buf.is_floating_point() else "sum", algo=algo)
         fut = torch.futures.Future(devices=[buf.device])
         fut.set_result(buf)  # CUDA-aware: DDP's wait joins the side stream, backward keeps overlapping
     state.calls += 1

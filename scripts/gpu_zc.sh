@@ -1,12 +1,12 @@
 #!/bin/bash
 # Zero-copy ("+zc") checks: the group tests (every schedule incl. flat+zc), the multi-process registered
-# buffer test, then the shared-GPU N=2 bench rehearsal (tuner candidates include flat+zc).
+# buffer test and DDP with zero-copy gradient buckets.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(pwd)}"
 cd "$R"; mkdir -p gpurun_out
 export FLEXAR_NO_BUILD=1
-timeout -k 10 400 python3 -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_ipc.py -x -v -m gpu --timeout 120 \
-    --timeout-method thread -k "all_algorithms or zero_copy or ipc_allreduce_processes" \
+timeout -k 10 500 python3 -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_ipc.py tests/test_gpu_backend.py -x -v \
+    -m gpu --timeout 120 --timeout-method thread -k "all_algorithms or zero_copy or ipc_allreduce_processes or ddp" \
     > gpurun_out/test_zc.log 2>&1 && echo "zc tests ok"
 rc=$?
 tail -3 gpurun_out/test_zc.log

@@ -42,9 +42,10 @@ def _train(rank, world, port, mode, q, model_kind="mlp"):
         model.load_state_dict(ref.state_dict())
         ddp = DDP(model, device_ids=[0], bucket_cap_mb=1)
         state = None
-        if mode in ("hook", "fp8hook"):
-            state = fb.FlexarHookState()
-            ddp.register_comm_hook(state, fb.flexar_allreduce_hook if mode == "hook" else fb.flexar_fp8_compress_hook)
+        if mode in ("hook", "fp8hook", "zchook"):
+            # zchook: every gradient bucket registered on first sight, reduced by "flat+zc" (no staging)
+            state = fb.FlexarHookState(zero_copy=mode == "zchook")
+            ddp.register_comm_hook(state, fb.flexar_fp8_compress_hook if mode == "fp8hook" else fb.flexar_allreduce_hook)
         opt = torch.optim.SGD(ddp.parameters(), lr=0.05)
         ropt = torch.optim.SGD(ref.parameters(), lr=0.05)
         g = torch.Generator().manual_seed(42)
@@ -73,6 +74,8 @@ def _train(rank, world, port, mode, q, model_kind="mlp"):
         err = max((a - b).abs().max().item() for a, b in zip(model.parameters(), ref.parameters()))
         pg = dist.group.WORLD
         used = getattr(pg, "stats", {}).get("flexar_allreduce", 0) if mode == "backend" else state.calls
+        if mode == "zchook" and not state._bucket_regs:
+            used = 0  # the zero-copy path must actually have registered the buckets
         dist.destroy_process_group()
         q.put((rank, err, used, None))
     except Exception:
@@ -82,7 +85,7 @@ def _train(rank, world, port, mode, q, model_kind="mlp"):
 
 
 @pytest.mark.parametrize("mode,model_kind", [("backend", "mlp"), ("hook", "mlp"), ("backend", "gpt"), ("hook", "gpt"),
-                                             ("fp8hook", "mlp")])
+                                             ("fp8hook", "mlp"), ("zchook", "mlp"), ("zchook", "gpt")])
 def test_ddp_over_flexar(cuda, mode, model_kind):
     import torch.multiprocessing as mp
 
