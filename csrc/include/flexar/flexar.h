@@ -98,7 +98,9 @@ int flexar_comm_size(flexar_comm_t comm);
  *   "tree:a,b,c"           mixed-radix FlexTree with the given stage widths
  *   "oneshot"              every rank reduces the full buffer (small messages)
  *   "ft"                   honour FT_TOPO exactly like the reference (any 1 = ring)
- * Optional suffixes: "+pull" (all-gather pulls from owners) / "+push" (owners push).
+ * Optional suffixes: "+pull" (all-gather pulls from owners) / "+push" (owners push), "+nts" (streaming
+ * stores), "+wt" (write-through protocol), "+f32" / "+rw" (typed staging of 16/8-bit multi-hop schedules),
+ * "+rccl" (message transport), "+zc" (flat only: zero copy over registered buffers, flexar_reg_*).
  */
 int flexar_comm_set_algo(flexar_comm_t comm, const char* spec);
 int flexar_comm_set_grid(flexar_comm_t comm, int grid_blocks, int block_threads); /* 0 = auto */
@@ -167,6 +169,9 @@ int flexar_reg_export(flexar_comm_t comm, const void* ptr, size_t bytes, void* o
 int flexar_reg_open(flexar_comm_t comm, const void* ptr, size_t bytes, const void* all_blobs, int* id_out);
 int flexar_reg_close(flexar_comm_t comm, int id);
 int flexar_reg_count(flexar_comm_t comm);
+/* Registration holding [ptr, ptr + bytes): its id, 0 if none, -1 if its allocation was freed and the address
+ * reused (stale peer mappings). A new registration overlapping old ones replaces them. */
+int flexar_reg_find(flexar_comm_t comm, const void* ptr, size_t bytes);
 /* JSON: per-peer PCI bus id, device ordinal, link class (same-device / xgmi / pcie / unknown) and hop
  * count from the connect-time probe; links used by the cost model; self-test state. */
 int flexar_comm_topology(flexar_comm_t comm, char* buf, size_t buflen);

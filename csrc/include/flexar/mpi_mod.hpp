@@ -483,6 +483,34 @@ inline flexar_comm_t device_comm(MPI_Comm comm) {
 inline int allreduce(const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype datatype, MPI_Op mop,
                      MPI_Comm comm);
 
+// FLEXAR_ALGO=flat+zc with device buffers: the zero-copy schedule reads the peers' buffers directly, so
+// the call's buffer must be registered on every rank. Registration is collective and cached per range;
+// a range is (re-)registered when any rank lacks it or its allocation changed since (freed and its
+// address reused: flexar_reg_find < 0), and the new registration replaces the stale one on every rank.
+inline bool zc_requested() {
+  static const bool zc = getenv("FLEXAR_ALGO") && strstr(getenv("FLEXAR_ALGO"), "+zc") != nullptr;
+  return zc;
+}
+inline int ensure_registered(flexar_comm_t c, MPI_Comm comm, const void* p, size_t bytes) {
+  int mine = flexar_reg_find(c, p, bytes) > 0 ? 1 : 0, all = 0;
+  MPI_Allreduce(&mine, &all, 1, MPI_INT, MPI_MIN, comm);
+  if (all) return MPI_SUCCESS;
+  int size = 1;
+  MPI_Comm_size(comm, &size);
+  const size_t hs = flexar_reg_handle_size();
+  std::vector<char> blob(hs, 0), blobs(hs * size);
+  int ok = flexar_reg_export(c, p, bytes, blob.data()) == 0 ? 1 : 0, all_ok = 0;
+  if (!ok) fprintf(stderr, "[flexar] register: %s\n", flexar_last_error());
+  MPI_Allgather(blob.data(), (int)hs, MPI_BYTE, blobs.data(), (int)hs, MPI_BYTE, comm);
+  MPI_Allreduce(&ok, &all_ok, 1, MPI_INT, MPI_MIN, comm);
+  if (!all_ok) return MPI_ERR_OTHER;
+  int id = 0;
+  ok = flexar_reg_open(c, p, bytes, blobs.data(), &id) == 0 ? 1 : 0;
+  if (!ok) fprintf(stderr, "[flexar] register: %s\n", flexar_last_error());
+  MPI_Allreduce(&ok, &all_ok, 1, MPI_INT, MPI_MIN, comm);
+  return all_ok ? MPI_SUCCESS : MPI_ERR_OTHER;
+}
+
 // Device buffers spanning nodes: intra-node reduce-scatter over xGMI (flexar), inter-node allreduce
 // of each rank's 1/L shard through host memory (p2p engine over the cross-node communicator of the
 // ranks with the same node-local index), intra-node all-gather over xGMI. Each rank ships only 1/L of
@@ -550,6 +578,11 @@ inline int allreduce(const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
       return hierarchical_device_allreduce(*hc, in, recvbuf, count, datatype, mop, dt, op);
     if (hc->nodes == 1 || size <= 1) {  // one node: xGMI/IPC GPU engine
       flexar_comm_t c = device_comm(comm);
+      if (zc_requested() && size > 1) {
+        int e = ensure_registered(c, comm, in, count * es);
+        if (e == MPI_SUCCESS && in != recvbuf) e = ensure_registered(c, comm, recvbuf, count * es);
+        if (e != MPI_SUCCESS) return e;
+      }
       int rc = flexar_allreduce(c, in, recvbuf, count, dt, op, nullptr);
       // MPI semantics: recvbuf holds the result when the call returns (a NIC, MPI_Send or another stream
       // may read it next), and a device watchdog timeout is this call's error, not the next one's

@@ -246,7 +246,15 @@ struct flexar_comm {
   // the same order; peer[p] is rank p's buffer mapped into this process. IPC mappings of one peer
   // allocation are shared by every registration inside it (torch's allocator carves tensors out of
   // larger segments).
-  struct Reg { int id; char* base; size_t bytes; bool aligned; char* peer[kMaxRanks]; std::string key[kMaxRanks]; };
+  struct Reg {
+    int id;
+    char* base;
+    size_t bytes;
+    bool aligned;
+    uint64_t bufid;  // HIP's unique id of the local allocation at registration (0 = unknown)
+    char* peer[kMaxRanks];
+    std::string key[kMaxRanks];
+  };
   std::vector<Reg> regs;
   int next_reg = 1;
   std::map<std::string, std::pair<char*, int>> ipc_maps;  // (peer, handle) -> mapped base, references
@@ -1353,6 +1361,30 @@ static_assert(sizeof(RegBlob) <= FLEXAR_REG_HANDLE_BYTES, "registration blob siz
 
 size_t flexar_reg_handle_size(void) { return FLEXAR_REG_HANDLE_BYTES; }
 
+static uint64_t buffer_id(const void* p) {
+  unsigned long long id = 0;
+  if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)p) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return (uint64_t)id;
+}
+
+// Drop registration i: its peer mappings close once no other registration uses them (caller holds mu
+// and has synchronised the device).
+static void reg_drop(flexar_comm* c, size_t i) {
+  for (int p = 0; p < c->nranks; ++p) {
+    if (p == c->rank) continue;
+    auto it = c->ipc_maps.find(c->regs[i].key[p]);
+    if (it == c->ipc_maps.end()) continue;
+    if (--it->second.second == 0) {
+      (void)hipIpcCloseMemHandle(it->second.first);
+      c->ipc_maps.erase(it);
+    }
+  }
+  c->regs.erase(c->regs.begin() + (long)i);
+}
+
 int flexar_reg_export(flexar_comm_t c, const void* ptr, size_t bytes, void* out) {
   if (!c || !ptr || !out || !bytes) { set_error("null argument"); return FLEXAR_ERR_INVALID; }
   FX_HIP(hipSetDevice(c->device));
@@ -1384,8 +1416,20 @@ int flexar_reg_open(flexar_comm_t c, const void* ptr, size_t bytes, const void* 
   if (c->nranks > 1 && !c->ipc) { set_error("zero-copy needs IPC peer access (this communicator runs RCCL messages)"); return FLEXAR_ERR_UNSUPPORTED; }
   std::lock_guard<std::mutex> lk(c->mu);
   FX_HIP(hipSetDevice(c->device));
+  // a new registration of (part of) a registered range replaces the old one (the buffer was freed and its
+  // address reused, or a call outgrew it): every rank registers together, so every rank drops it
+  bool synced = false;
+  for (size_t i = c->regs.size(); i-- > 0;) {
+    const flexar_comm::Reg& o = c->regs[i];
+    if ((const char*)ptr < o.base + o.bytes && o.base < (const char*)ptr + bytes) {
+      if (!synced) FX_HIP(hipDeviceSynchronize());
+      synced = true;
+      reg_drop(c, i);
+    }
+  }
   flexar_comm::Reg g;
   g.id = c->next_reg++;
+  g.bufid = c->nranks > 1 && !c->group_member ? buffer_id(ptr) : 0;
   g.base = (char*)ptr;
   g.bytes = bytes;
   g.aligned = ((uintptr_t)ptr & 15) == 0;
@@ -1449,19 +1493,24 @@ int flexar_reg_close(flexar_comm_t c, int id) {
     if (c->regs[i].id != id) continue;
     FX_HIP(hipSetDevice(c->device));
     FX_HIP(hipDeviceSynchronize());  // no call of ours still reads through the mappings
-    for (int p = 0; p < c->nranks; ++p) {
-      auto it = c->ipc_maps.find(c->regs[i].key[p]);
-      if (p == c->rank || it == c->ipc_maps.end()) continue;
-      if (--it->second.second == 0) {
-        (void)hipIpcCloseMemHandle(it->second.first);
-        c->ipc_maps.erase(it);
-      }
-    }
-    c->regs.erase(c->regs.begin() + (long)i);
+    reg_drop(c, i);
     return 0;
   }
   set_error("no registration " + std::to_string(id));
   return FLEXAR_ERR_INVALID;
+}
+
+// The registration holding [p, p + bytes): its id, 0 if none, -1 if the allocation behind the registered
+// address is not the one registered any more (freed and reused: the peers' mappings are stale).
+int flexar_reg_find(flexar_comm_t c, const void* p, size_t bytes) {
+  if (!c || !p) return 0;
+  std::lock_guard<std::mutex> lk(c->mu);
+  for (const auto& r : c->regs)
+    if ((const char*)p >= r.base && (const char*)p + bytes <= r.base + r.bytes) {
+      if (r.bufid && buffer_id(p) != r.bufid) return -1;
+      return r.id;
+    }
+  return 0;
 }
 
 int flexar_reg_count(flexar_comm_t c) { return c ? (int)c->regs.size() : -1; }

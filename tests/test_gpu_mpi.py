@@ -30,11 +30,22 @@ def _mpirun(n, args, env=None):
                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300, env=e)
 
 
-@pytest.mark.parametrize("algo", ["flat", "ring", "ll", "oneshot"])
+@pytest.mark.parametrize("algo", ["flat", "ring", "ll", "oneshot", "flat+zc"])
 def test_mpi_device_buffers_ipc(tools, algo):
     r = _mpirun(2, [tools["flexar_bench"], "--mem", "device", "--size", "100003", "--repeat", "5", "--check",
                     "--algo", algo])
     assert r.returncode == 0 and "check n=100003: ok" in r.stdout, r.stdout[-3000:]
+
+
+def test_mpi_zero_copy_sweep_reregisters(tools):
+    """FLEXAR_ALGO=flat+zc through MPI_Allreduce_FT: every sweep size is a fresh hipMalloc (often at a
+    freed buffer's address), so the MPI layer must (re-)register collectively and drop stale mappings."""
+    r = _mpirun(2, [tools["flexar_bench"], "--mem", "device", "--sweep", "4K:4M", "--repeat", "3", "--check",
+                    "--algo", "flat+zc"])
+    assert r.returncode == 0 and r.stdout.count(": ok") >= 11, r.stdout[-3000:]
+    r = _mpirun(2, [tools["flexar_bench"], "--mem", "device", "--dtype", "bfloat16", "--size", "65539", "--check",
+                    "--algo", "flat+zc"])
+    assert r.returncode == 0 and "check n=65539: ok" in r.stdout, r.stdout[-3000:]
 
 
 def test_mpi_device_buffers_host_staging(tools):
