@@ -23,7 +23,7 @@ def main():
 
     mib = int(os.environ.get("ZCB_MIB", "64"))
     ranks = [int(v) for v in os.environ.get("ZCB_RANKS", "2,4,8").split(",")]
-    specs = ["flat+pull", "flat+pull+nts", "flat+zc", "flat+zc+nts", "flat+zc+wt"]
+    specs = os.environ.get("ZCB_SPECS", "flat+pull,flat+pull+nts,flat+zc,flat+zc+nts,flat+zc+wt").split(",")
     count = (mib << 20) // 4
     for n in ranks:
         grp = LocalGroup(n, workspace_bytes=(4 * mib + 64) << 20)
