@@ -1414,6 +1414,10 @@ int flexar_reg_open(flexar_comm_t c, const void* ptr, size_t bytes, const void* 
   if (!c || !ptr || !all || !id_out) { set_error("null argument"); return FLEXAR_ERR_INVALID; }
   if (!c->connected && c->nranks > 1) { set_error("communicator not connected"); return FLEXAR_ERR_STATE; }
   if (c->nranks > 1 && !c->ipc) { set_error("zero-copy needs IPC peer access (this communicator runs RCCL messages)"); return FLEXAR_ERR_UNSUPPORTED; }
+  if (c->group_member) {
+    set_error("in-process groups address every rank's buffers directly: no registration needed");
+    return FLEXAR_ERR_INVALID;
+  }
   std::lock_guard<std::mutex> lk(c->mu);
   FX_HIP(hipSetDevice(c->device));
   // a new registration of (part of) a registered range replaces the old one (the buffer was freed and its
