@@ -380,8 +380,9 @@ class FlexarHookState:
 
         ``zero_copy`` (default FLEXAR_HOOK_ZC=1): register every gradient bucket with the communicator the
         first time it is seen (collective: every rank sees the buckets in the same order) and reduce it
-        with the zero-copy flat schedule ("flat+zc": peers read the bucket over IPC, no staging copies,
-        half the HBM traffic next to the backward kernels). A bucket whose storage changes (DDP rebuilds
+        with the zero-copy flat schedule ("flat+zc+push": each rank reads its block of every peer's bucket
+        over IPC and writes the sum straight into every bucket, no staging copies, 2/5 of the HBM traffic
+        next to the backward kernels). A bucket whose storage changes (DDP rebuilds
         its buckets after the first iteration) is re-registered and the old registration dropped."""
         self.comm = communicator or Communicator(group=process_group)
         self.algo = algo
@@ -396,7 +397,7 @@ class FlexarHookState:
             self.comm.set_grid(grid)
 
     def bucket_algo(self, bucket, buf):
-        """The algorithm for this bucket: "flat+zc" once the bucket is registered (zero_copy), else ``algo``."""
+        """The algorithm for this bucket: "flat+zc+push" once it is registered (zero_copy), else ``algo``."""
         if not self.zero_copy or buf.data_ptr() % 16:
             return self.algo
         key = bucket.index()
@@ -407,7 +408,7 @@ class FlexarHookState:
                 self.comm.deregister(have[2])
             self._bucket_regs[key] = (buf.data_ptr(), nbytes, self.comm.register(buf))
         proto = "+wt" if self.algo and "+wt" in self.algo else "+nts" if self.algo and "+nts" in self.algo else ""
-        return "flat+zc" + proto
+        return "flat+zc+push" + proto
 
     def stream(self, dev):
         s = self._streams.get(dev.index)

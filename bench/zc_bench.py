@@ -23,7 +23,7 @@ def main():
 
     mib = int(os.environ.get("ZCB_MIB", "64"))
     ranks = [int(v) for v in os.environ.get("ZCB_RANKS", "2,4,8").split(",")]
-    specs = os.environ.get("ZCB_SPECS", "flat+pull,flat+pull+nts,flat+zc,flat+zc+nts,flat+zc+wt").split(",")
+    specs = os.environ.get("ZCB_SPECS", "flat+pull,flat+pull+nts,flat+zc,flat+zc+nts,flat+zc+wt,flat+zc+push,flat+zc+push+wt").split(",")
     count = (mib << 20) // 4
     for n in ranks:
         grp = LocalGroup(n, workspace_bytes=(4 * mib + 64) << 20)
@@ -44,7 +44,7 @@ def main():
             torch.cuda.synchronize()
             ms = a.elapsed_time(b) / iters
             S = count * 4
-            hbm = (S * ((n + 1) / n + 2 * (n - 1) / n) if "zc" in spec
+            hbm = (S * (1 + 1) if "zc+push" in spec else S * ((n + 1) / n + 2 * (n - 1) / n) if "zc" in spec
                    else S * (2 * (n - 1) / n + (n + 2) / n + 2 * (n - 1) / n))
             print(json.dumps({"ranks": n, "MiB_fp32": mib, "spec": spec, "ms": round(ms, 4),
                               "busbw_GBps": round(S / (ms * 1e-3) * 2 * (n - 1) / n / 1e9, 1),

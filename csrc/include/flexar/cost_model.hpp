@@ -100,9 +100,13 @@ struct XgmiModel {
           f[2] += 2.0 * per_peer / (1e3 * share(w - 1));
           f[3] += 2.0 * w * per_peer / 1e3;
         }
-        if (s.zc) {  // registered buffers (flat only): a third hand-off, no staging writes / reads (3/5 of
-          f[1] += 1.0;  // the staging schedule's HBM bytes, profiles/r2_zc)
-          f[3] *= 0.6;
+        if (s.zc) {  // registered buffers (flat only), no staging writes / reads: pull = a third hand-off
+          if (s.ag == AgMode::PUSH) {  // and 3/5 of the staging schedule's HBM bytes (profiles/r2_zc);
+            f[3] *= 0.4;               // push = each input byte read once, each result byte written once
+          } else {
+            f[1] += 1.0;
+            f[3] *= 0.6;
+          }
           return true;
         }
         if (s.ag == AgMode::PUSH || s.ag == AgMode::AUTO) f[3] += S / 1e3;  // local copy-out of pushed blocks

@@ -87,7 +87,7 @@ class Planner {
         if (err) *err = "zero-copy (+zc) runs the flat schedule over IPC-registered buffers (no wire type, no +rccl)";
         return false;
       }
-      build_flat_zc();
+      build_flat_zc(spec.ag == AgMode::PUSH);
       P->zc = true;
       P->desc = spec.str();
     } else if (wire >= 2 && !(spec.kind == AlgoKind::TREE && spec.widths.size() == 1 && spec.widths[0] == (int)N)) {
@@ -676,15 +676,19 @@ class Planner {
 
   // Zero-copy flat allreduce over registered buffers ("+zc"): no staging and no copies into it. Rank k
   // reduces block k straight from every rank's IN (remote loads over xGMI; rank order, so every owner
-  // sums in the same order) into its own OUT, then copies every other block from its owner's OUT. The
-  // reference's flat exchange (mpi_mod.hpp:952-1111 with one stage of width N) moves the same bytes
-  // through send/recv buffers; here each byte crosses a link once per phase and touches HBM twice less.
-  // Three hand-offs, per workgroup like every flag: slot 0 "my IN is final" (every rank has entered the
-  // call), slot 1 "my block is reduced" (and I have read your IN), slot 2 "I have read your OUT". The last
-  // one keeps a rank in the call until no peer can still read its buffers, so its caller may overwrite
-  // them as soon as the call completes on its stream. In place (IN == OUT) is safe: a rank writes a
-  // peer's block into its OUT only after slot 1, when every peer has finished reading that rank's IN.
-  void build_flat_zc() {
+  // sums in the same order). The reference's flat exchange (mpi_mod.hpp:952-1111 with one stage of width
+  // N) moves the same bytes through send/recv buffers; here HBM sees each byte far fewer times.
+  //  pull (default): the owner writes its own OUT, then every rank copies the other blocks from their
+  //    owners' OUT. Three hand-offs, per workgroup like every flag: slot 0 "my IN is final" (every rank
+  //    has entered the call), slot 1 "my block is reduced" (and I have read your IN), slot 2 "I have read
+  //    your OUT" - the last keeps a rank in the call until no peer can still read its buffers, so its
+  //    caller may overwrite them as soon as the call completes on its stream.
+  //  push ("+zc+push"): the owner writes the reduced block into its own OUT and every peer's OUT (remote
+  //    stores) - each input byte is read once and each result byte written once per rank. Two hand-offs:
+  //    slot 0 as above, slot 1 "I have read your IN and written your block".
+  // In place (IN == OUT) is safe in both: block k of a rank's IN is read only by its owner k, which
+  // writes that rank's block k (push) or lets it be overwritten (pull, after slot 1) only afterwards.
+  void build_flat_zc(bool push) {
     const uint64_t split = round_up((count + N - 1) / N);
     auto boff = [&](uint32_t k) { return (uint64_t)k * split; };
     auto blen = [&](uint32_t k) -> uint64_t {
@@ -696,12 +700,17 @@ class Planner {
     wait(peers, 0);
     std::vector<Loc> srcs;
     for (uint32_t p = 0; p < N; ++p) srcs.push_back(loc(BUF_IN, p, boff(r)));
-    xfer(blen(r), srcs, {loc(BUF_OUT, r, boff(r))}, scale);
+    std::vector<Loc> dsts{loc(BUF_OUT, r, boff(r))};
+    if (push)
+      for (uint32_t p : peers) dsts.push_back(loc(BUF_OUT, p, boff(r)));
+    xfer(blen(r), srcs, dsts, scale);
     signal(peers, 1);
     wait(peers, 1);
-    for (uint32_t p : peers) xfer(blen(p), {loc(BUF_OUT, p, boff(p))}, {loc(BUF_OUT, r, boff(p))}, 1.0f);
-    signal(peers, 2);
-    wait(peers, 2);
+    if (!push) {
+      for (uint32_t p : peers) xfer(blen(p), {loc(BUF_OUT, p, boff(p))}, {loc(BUF_OUT, r, boff(p))}, 1.0f);
+      signal(peers, 2);
+      wait(peers, 2);
+    }
     finish_channel();
   }
 

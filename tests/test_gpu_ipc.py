@@ -566,7 +566,7 @@ def _zc_worker(rank, world, port, q):
         x, y = arena[:n], arena[n + 64:2 * n + 64]
         rx, ry = comm.register(x), comm.register(y)
         errs = {}
-        for spec in ("flat+zc", "flat+zc+wt", "flat+zc+nts"):
+        for spec in ("flat+zc", "flat+zc+wt", "flat+zc+nts", "flat+zc+push", "flat+zc+push+wt"):
             for size in (7, 4096, 300001, n):
                 for call in range(3):  # consecutive calls: a peer still reading the last call would show
                     src = torch.randn(size, generator=torch.Generator().manual_seed(1000 * rank + size + call))
@@ -581,6 +581,10 @@ def _zc_worker(rank, world, port, q):
         comm.all_reduce(x[100:100 + 5003], algo="flat+zc")
         torch.cuda.synchronize()
         errs["in_place"] = (x[100:100 + 5003] - world * (world + 1) / 2).abs().max().item()
+        x[100:100 + 5003].fill_(float(rank + 1))
+        comm.all_reduce(x[100:100 + 5003], algo="flat+zc+push")
+        torch.cuda.synchronize()
+        errs["in_place_push"] = (x[100:100 + 5003] - world * (world + 1) / 2).abs().max().item()
         # an unregistered buffer is refused, not read through a stale mapping
         try:
             comm.all_reduce(torch.ones(64, device=dev), algo="flat+zc")

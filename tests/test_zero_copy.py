@@ -13,7 +13,7 @@ from allreduce_over_mpi_amd import _native as nv
 
 @pytest.mark.parametrize("n", [2, 3, 4, 7, 8, 12, 16])
 @pytest.mark.parametrize("count", [1, 35, 4099, 10007])
-@pytest.mark.parametrize("spec", ["flat+zc", "flat+zc+wt", "flat+zc+nts"])
+@pytest.mark.parametrize("spec", ["flat+zc", "flat+zc+wt", "flat+zc+nts", "flat+zc+push", "flat+zc+push+wt"])
 def test_zero_copy_exact_sum(n, count, spec):
     ins = [np.random.default_rng(7 * r + count).integers(-99, 99, count).astype(np.int32) for r in range(n)]
     want = np.sum(ins, axis=0)
@@ -21,12 +21,14 @@ def test_zero_copy_exact_sum(n, count, spec):
         np.testing.assert_array_equal(o, want)
 
 
-@pytest.mark.parametrize("n", [2, 4, 8])
-def test_zero_copy_in_place(n):
-    # IN == OUT: a rank overwrites its OUT blocks only after every peer finished reading its IN
+@pytest.mark.parametrize("n", [2, 4, 8, 11])
+@pytest.mark.parametrize("spec", ["flat+zc", "flat+zc+push"])
+def test_zero_copy_in_place(n, spec):
+    # IN == OUT: block k of a rank's IN is read only by its owner k, which overwrites it (push) or lets it
+    # be overwritten (pull) only afterwards
     ins = [np.random.default_rng(r).integers(-50, 50, 5003).astype(np.int32) for r in range(n)]
     want = np.sum(ins, axis=0)
-    for o in nv.simulate("flat+zc", ins, ncalls=4, grid=4, in_place=True):
+    for o in nv.simulate(spec, ins, ncalls=4, grid=4, in_place=True):
         np.testing.assert_array_equal(o, want)
 
 
@@ -44,6 +46,9 @@ def test_zero_copy_program_shape():
     assert "staging 0 elems" in d and "3 flag slots" in d
     assert "IN@0" in d and "OUT@2" in d  # peer buffers are addressed directly
     assert "STG" not in d
+    # push: one reduction straight into every rank's OUT, two hand-offs
+    d = nv.plan_dump("flat+zc+push", 1, 4, 4096, "float32")
+    assert "2 flag slots" in d and d.count("XFER") == 1 and "STG" not in d
 
 
 def test_zero_copy_refused_outside_flat():
