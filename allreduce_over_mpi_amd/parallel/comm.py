@@ -121,6 +121,8 @@ class Communicator:
         self.transport_note = None
         self._exchange = None
         self._regs = {}
+        self._zc_ok = None  # zero-copy readiness: None = not checked yet (first register())
+        self._zc_testing = False
         if self.world_size > 1:
             hs = int(self._lib.flexar_handle_size())
             buf = ctypes.create_string_buffer(hs)
@@ -299,8 +301,61 @@ class Communicator:
         flat schedule then reads every peer's input and output straight over IPC, with no staging copies.
         Collective: every rank registers its corresponding tensor (same byte size), in the same order.
         The communicator holds a reference until :meth:`deregister`. A "+zc" call takes tensors that lie
-        inside registrations, at the same offset on every rank (DDP buckets, FSDP flat parameters)."""
+        inside registrations, at the same offset on every rank (DDP buckets, FSDP flat parameters).
+
+        The first registration runs the zero-copy readiness check (:meth:`_zc_selftest`, like the
+        connect-time self-test of the staging protocols): if the peers' buffers do not read back exactly
+        on this node, every rank raises here and callers keep the staging schedules."""
         _require_cuda(tensor)
+        if self.world_size > 1 and self._zc_ok is None:
+            self._zc_ok = False  # (re-entry from the self-test's own registration)
+            self._zc_ok = self._zc_selftest()
+        if self.world_size > 1 and self._zc_ok is False and not self._zc_testing:
+            raise nv.FlexarError(2, "register: zero copy failed its readiness check on this node "
+                                    "(peer buffers did not read back exactly); use the staging schedules")
+        return self._register(tensor)
+
+    def _zc_selftest(self) -> bool:
+        """Exact integer allreduces over a registered scratch buffer with both zero-copy forms, three
+        consecutive calls each (the calls' hand-offs and the peers' reads of freshly written buffers are
+        what could fail across devices). Collective; True when every rank got exact sums."""
+        import torch
+
+        if os.environ.get("FLEXAR_SELFTEST", "1") == "0":
+            return True
+        n = 65536 + 77
+        buf = torch.empty(2 * n + 64, dtype=torch.int32, device=f"cuda:{self.device}")
+        x, y = buf[:n], buf[n + 64:]
+        idx = torch.arange(n, dtype=torch.int32, device=buf.device) % 1009
+        ok = True
+        self._zc_testing = True
+        rid = None
+        try:
+            rid = self._register(buf)
+            w = self.world_size
+            for spec in ("flat+zc+push", "flat+zc"):
+                for call in range(3):
+                    x.copy_(idx * (self.rank + 1) + call)
+                    self.all_reduce(x, out=y, algo=spec)
+                    want = idx * (w * (w + 1) // 2) + call * w
+                    ok = ok and bool(torch.equal(y, want))
+            self.check()
+        except nv.FlexarError:
+            ok = False
+        finally:
+            self._zc_testing = False
+        rows = self._exchange(b"1" if ok else b"0")  # also the barrier: no rank is inside a test call
+        passed = all(r == b"1" for r in rows)
+        if not passed:
+            self.clear_error()  # a timed-out test call must not fail the next production call
+        if rid is not None:
+            try:
+                self.deregister(rid)
+            except nv.FlexarError:
+                pass
+        return passed
+
+    def _register(self, tensor) -> int:
         nbytes = tensor.numel() * tensor.element_size()
         blob = ctypes.create_string_buffer(int(self._lib.flexar_reg_handle_size()))
         rc = self._lib.flexar_reg_export(self._h, tensor.data_ptr(), nbytes, blob)
