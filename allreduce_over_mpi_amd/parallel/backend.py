@@ -406,7 +406,11 @@ class FlexarHookState:
         if have is None or have[0] != buf.data_ptr() or have[1] != nbytes:
             if have is not None:
                 self.comm.deregister(have[2])
-            self._bucket_regs[key] = (buf.data_ptr(), nbytes, self.comm.register(buf))
+            try:
+                self._bucket_regs[key] = (buf.data_ptr(), nbytes, self.comm.register(buf))
+            except nv.FlexarError:  # zero copy not usable here (every rank raises together): staging
+                self.zero_copy = False
+                return self.algo
         proto = "+wt" if self.algo and "+wt" in self.algo else "+nts" if self.algo and "+nts" in self.algo else ""
         return "flat+zc+push" + proto
 
