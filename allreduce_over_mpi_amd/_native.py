@@ -74,6 +74,7 @@ def _sig(lib):
         "flexar_group_collective": (i, [c.POINTER(vp), i, i, c.POINTER(vp), c.POINTER(vp), sz, i, i, vp, cp]),
         "flexar_broadcast": (i, [vp, vp, vp, sz, i, i, vp, cp]),
         "flexar_all_to_all": (i, [vp, vp, vp, sz, i, vp]),
+        "flexar_all_to_all_ex": (i, [vp, vp, vp, sz, i, vp, cp]),
         "flexar_amax": (i, [vp, sz, i, vp, vp]),
         "flexar_quantize_fp8": (i, [vp, i, vp, sz, vp, f, vp]),
         "flexar_dequantize_fp8": (i, [vp, vp, i, sz, vp, f, vp]),

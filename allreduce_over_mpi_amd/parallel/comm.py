@@ -456,16 +456,17 @@ class Communicator:
             nv.check(rc, "all_gather")
         return output
 
-    def all_to_all(self, input, output, stream=None):
+    def all_to_all(self, input, output, stream=None, algo: Optional[str] = None):
         """Equal-split all-to-all (expert parallelism): block p of ``input`` (world_size blocks) goes to
-        rank p; block q of ``output`` comes from rank q. One direct exchange over all links."""
+        rank p; block q of ``output`` comes from rank q. One direct exchange over all links; ``algo``
+        "flat+zc" writes straight into the peers' registered ``output`` (no staging)."""
         _require_cuda(input)
         _require_cuda(output, "output")
         if input.numel() != output.numel() or input.dtype != output.dtype or input.numel() % self.world_size:
             raise nv.FlexarError(1, "input/output must have equal size (a multiple of world_size) and dtype")
-        nv.check(self._lib.flexar_all_to_all(self._h, input.data_ptr(), output.data_ptr(),
-                                             input.numel() // self.world_size, nv.dtype_code(input.dtype),
-                                             _stream_handle(stream)), "all_to_all")
+        nv.check(self._lib.flexar_all_to_all_ex(self._h, input.data_ptr(), output.data_ptr(),
+                                                input.numel() // self.world_size, nv.dtype_code(input.dtype),
+                                                _stream_handle(stream), _algo(algo)), "all_to_all")
         return output
 
     def broadcast(self, tensor, root: int = 0, out=None, algo: Optional[str] = None, stream=None):

@@ -134,6 +134,10 @@ int flexar_all_gather(flexar_comm_t comm, const void* sendbuf, void* recvbuf, si
  * block p goes to rank p; recvbuf receives nranks blocks, block q from rank q. One direct exchange. */
 int flexar_all_to_all(flexar_comm_t comm, const void* sendbuf, void* recvbuf, size_t count, int dtype,
                       void* hip_stream);
+/* Same with an algorithm spec: NULL = the direct exchange through staging, "flat+zc" = zero copy (every rank
+ * writes straight into its peers' registered recvbuf). */
+int flexar_all_to_all_ex(flexar_comm_t comm, const void* sendbuf, void* recvbuf, size_t count, int dtype,
+                         void* hip_stream, const char* algo);
 /* Broadcast `count` elements from `root`: the root reads sendbuf (NULL = recvbuf), every rank writes
  * recvbuf. algo: "oneshot" = direct multicast from the root; "flat" (or any other spec) = scatter +
  * all-gather (~2 S / N per link); NULL/"auto" = direct up to 256 KiB, scatter + all-gather above. */

@@ -48,8 +48,10 @@ struct Program {
   int wire = 0;
   uint32_t wsize = 0;
   uint32_t unit = 0;
-  // zero-copy program (AlgoSpec::zc): IN / OUT operands of other ranks address their registered buffers
+  // zero-copy program (AlgoSpec::zc): IN / OUT operands of other ranks address their registered buffers;
+  // zc_bufs = which of them the program addresses on a peer (bit BUF_IN, bit BUF_OUT)
   bool zc = false;
+  uint32_t zc_bufs = 0;
   std::string desc;
   uint32_t stg_unit() const { return unit ? unit : esize; }
   uint64_t stg_bytes() const { return stg_elems * stg_unit(); }
@@ -171,6 +173,10 @@ class Planner {
         if (count) xfer(count, {loc(BUF_IN, r, 0)}, {loc(BUF_OUT, r, 0)}, 1.0f);
         finish_channel();
         P->desc = "copy";
+      } else if (spec.zc) {
+        build_bcast_zc((uint32_t)stride);
+        P->zc = true;
+        P->desc = "bcast-zc";
       } else if (spec.kind == AlgoKind::ONESHOT || spec.kind == AlgoKind::LL) {
         build_bcast_direct((uint32_t)stride);
         P->desc = "bcast-direct";
@@ -190,10 +196,18 @@ class Planner {
     P->chan_start.push_back(0);
     stg = 0;
     const bool ring = spec.kind == AlgoKind::RING && N > 2;
+    if (spec.zc && (spec.kind == AlgoKind::RING || spec.msg)) {
+      if (err) *err = "zero-copy (+zc) collectives run the direct exchange over IPC-registered buffers";
+      return false;
+    }
     if (N == 1) {
       if (count) xfer(count, {loc(BUF_IN, r, 0)}, {loc(BUF_OUT, r, 0)}, coll == Coll::REDUCE_SCATTER ? scale : 1.0f);
       finish_channel();
       P->desc = "copy";
+    } else if (spec.zc) {
+      build_coll_zc(coll, stride);
+      P->zc = true;
+      P->desc = coll == Coll::ALL_TO_ALL ? "a2a-zc" : coll == Coll::REDUCE_SCATTER ? "rs-zc" : "ag-zc";
     } else if (coll == Coll::ALL_TO_ALL) {
       build_flat_a2a(stride);
       P->desc = "flat-a2a";
@@ -214,6 +228,14 @@ class Planner {
   // pairwise independent in local memory (no overlap between one op's local destinations and
   // another's local sources/destinations). Executed in a per-workgroup rotated order.
   static void mark_runs(Program& P, uint32_t rank) {
+    P.zc_bufs = 0;
+    for (const Op& o : P.ops)
+      if (o.kind == OP_XFER) {
+        for (int k = 0; k < o.nsrc; ++k)
+          if (o.src[k].buf != BUF_STG && o.src[k].rank != rank) P.zc_bufs |= 1u << o.src[k].buf;
+        for (int k = 0; k < o.ndst; ++k)
+          if (o.dst[k].buf != BUF_STG && o.dst[k].rank != rank) P.zc_bufs |= 1u << o.dst[k].buf;
+      }
     auto remote = [&](const Op& o) {
       for (int k = 0; k < o.nsrc; ++k) if (o.src[k].rank != rank) return true;
       for (int k = 0; k < o.ndst; ++k) if (o.dst[k].rank != rank) return true;
@@ -710,6 +732,53 @@ class Planner {
       for (uint32_t p : peers) xfer(blen(p), {loc(BUF_OUT, p, boff(p))}, {loc(BUF_OUT, r, boff(p))}, 1.0f);
       signal(peers, 2);
       wait(peers, 2);
+    }
+    finish_channel();
+  }
+
+  // Zero-copy reduce-scatter / all-gather / all-to-all over registered buffers: the direct exchange with
+  // the peers' IN / OUT as operands, no staging. Slot 0 "I have entered the call" (my IN is final, my OUT
+  // may be written), slot 1 "I have finished with your buffers" (no rank leaves while a peer still
+  // reads or writes its buffers).
+  //  reduce-scatter: pull - rank r sums block r of every rank's IN (rank order) into its OUT;
+  //  all-gather: push - rank r writes its IN into block r of every rank's OUT;
+  //  all-to-all: push - rank r writes block p of its IN into block r of rank p's OUT.
+  void build_coll_zc(Coll coll, uint64_t stride) {
+    const uint64_t m = count;
+    auto peers = rotated_peers();
+    signal(peers, 0);
+    wait(peers, 0);
+    if (coll == Coll::REDUCE_SCATTER) {
+      std::vector<Loc> srcs;
+      for (uint32_t p = 0; p < N; ++p) srcs.push_back(loc(BUF_IN, p, (uint64_t)r * stride));
+      xfer(m, srcs, {loc(BUF_OUT, r, 0)}, scale);
+    } else if (coll == Coll::ALL_GATHER) {
+      std::vector<Loc> dsts{loc(BUF_OUT, r, (uint64_t)r * stride)};
+      for (uint32_t p : peers) dsts.push_back(loc(BUF_OUT, p, (uint64_t)r * stride));
+      xfer(m, {loc(BUF_IN, r, 0)}, dsts, 1.0f);
+    } else {
+      for (uint32_t p : peers) xfer(m, {loc(BUF_IN, r, (uint64_t)p * stride)}, {loc(BUF_OUT, p, (uint64_t)r * stride)}, 1.0f);
+      xfer(m, {loc(BUF_IN, r, (uint64_t)r * stride)}, {loc(BUF_OUT, r, (uint64_t)r * stride)}, 1.0f);
+    }
+    signal(peers, 1);
+    wait(peers, 1);
+    finish_channel();
+  }
+  // Zero-copy broadcast: the root writes its IN into every rank's OUT once every rank has entered the
+  // call, then tells them it is done.
+  void build_bcast_zc(uint32_t root) {
+    std::vector<uint32_t> others;
+    for (uint32_t p = 0; p < N; ++p)
+      if (p != root) others.push_back(p);
+    if (r == root) {
+      wait(others, 0);
+      std::vector<Loc> dsts{loc(BUF_OUT, r, 0)};
+      for (uint32_t p : others) dsts.push_back(loc(BUF_OUT, p, 0));
+      xfer(count, {loc(BUF_IN, r, 0)}, dsts, 1.0f);
+      signal(others, 1);
+    } else {
+      signal({root}, 0);
+      wait({root}, 1);
     }
     finish_channel();
   }

@@ -429,13 +429,16 @@ static int proto_of(const AlgoSpec& s) { return s.wt ? PM_WT : s.nts ? PM_FENCE_
 // Zero-copy program: the peers' buffers of this call. `in` / `out` must lie inside registrations; every
 // rank passes the same offsets into its corresponding registration (the registration contract, like
 // NCCL's registered buffers), so rank p's operand is its registered base + the same offset.
-static int zc_bind(flexar_comm* c, const void* in, const void* out, uint64_t bytes, DevCtx* x) {
+static int zc_bind(flexar_comm* c, const Program& P, const void* in, uint64_t in_bytes, const void* out,
+                   uint64_t out_bytes, DevCtx* x) {
   const void* ptrs[2] = {in, out};
+  const uint64_t sizes[2] = {in_bytes, out_bytes};
   for (int b = 0; b < 2; ++b) {
+    if (!(P.zc_bufs & (1u << b))) continue;  // the program never addresses this buffer on a peer
     const char* q = (const char*)ptrs[b];
     const flexar_comm::Reg* g = nullptr;
     for (const auto& r : c->regs)
-      if (q >= r.base && q + bytes <= r.base + r.bytes) { g = &r; break; }
+      if (q >= r.base && q + sizes[b] <= r.base + r.bytes) { g = &r; break; }
     if (!g) {
       set_error(std::string("zero-copy (+zc) needs registered buffers: the ") + (b ? "output" : "input") +
                 " is not inside a registration (Communicator.register / flexar_reg_open)");
@@ -655,6 +658,11 @@ static int run_rs_ag(flexar_comm* c, Coll coll, const void* in, void* out, size_
     if ((rc = get_program(c, s, n, es, fs, &dp, coll, count))) return rc;
     DevCtx x;
     fill_ctx(c, dp, (const char*)in + off * es, (char*)out + off * es, &x);
+    if (dp->prog.zc) {  // the N-block side spans (N - 1) rank strides + this piece
+      const uint64_t wide = ((uint64_t)(c->nranks - 1) * count + n) * es;
+      const uint64_t in_b = coll == Coll::ALL_GATHER ? n * es : wide, out_b = coll == Coll::REDUCE_SCATTER ? n * es : wide;
+      if ((rc = zc_bind(c, dp->prog, (const char*)in + off * es, in_b, (char*)out + off * es, out_b, &x))) return rc;
+    }
     LaunchArgs la;
     la.kind = LAUNCH_EXEC;
     la.ctx = x;
@@ -709,6 +717,9 @@ static int run_bcast(flexar_comm* c, const void* in, void* out, size_t count, in
     if ((rc = get_program(c, s, n, es, 1.0f, &dp, Coll::BROADCAST, (uint64_t)root))) return rc;
     DevCtx x;
     fill_ctx(c, dp, (const char*)in + off * es, (char*)out + off * es, &x);
+    if (dp->prog.zc &&
+        (rc = zc_bind(c, dp->prog, (const char*)in + off * es, n * es, (char*)out + off * es, n * es, &x)))
+      return rc;
     LaunchArgs la;
     la.kind = LAUNCH_EXEC;
     la.ctx = x;
@@ -1792,7 +1803,8 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     LaunchArgs la;
     la.kind = LAUNCH_EXEC;
     fill_ctx(c, dp, in, out, &la.ctx);
-    if (dp->prog.zc && (rc = zc_bind(c, in, out, (uint64_t)count * es, &la.ctx))) return rc;
+    if (dp->prog.zc && (rc = zc_bind(c, dp->prog, in, (uint64_t)count * es, out, (uint64_t)count * es, &la.ctx)))
+      return rc;
     la.grid = hit ? m.grid : choose_grid(c, count * es, dp->prog.nchan);
     la.stream = st;
     la.proto = proto_of(s);
@@ -1824,7 +1836,9 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     if ((rc = get_program(c, s, n, es, fs, &dp))) return rc;
     DevCtx x;
     fill_ctx(c, dp, (const char*)in + off * es, (char*)out + off * es, &x);
-    if (dp->prog.zc && (rc = zc_bind(c, (const char*)in + off * es, (char*)out + off * es, n * es, &x))) break;
+    if (dp->prog.zc &&
+        (rc = zc_bind(c, dp->prog, (const char*)in + off * es, n * es, (char*)out + off * es, n * es, &x)))
+      break;
     int grid = choose_grid(c, n * es, dp->prog.nchan);
     LaunchArgs la;
     la.kind = LAUNCH_EXEC;
@@ -1964,13 +1978,18 @@ int flexar_all_gather(flexar_comm_t c, const void* in, void* out, size_t count, 
   return run_rs_ag(c, Coll::ALL_GATHER, in, out, count, dtype, FLEXAR_SUM, (hipStream_t)stream, algo, 1.0f);
 }
 
-int flexar_all_to_all(flexar_comm_t c, const void* in, void* out, size_t count, int dtype, void* stream) {
+int flexar_all_to_all_ex(flexar_comm_t c, const void* in, void* out, size_t count, int dtype, void* stream,
+                         const char* algo) {
   int rc = validate_call(c, dtype, FLEXAR_SUM, 1.0f);
   if (rc) return rc;
   if (!in || !out || in == out) { set_error("all_to_all needs distinct send/recv buffers"); return FLEXAR_ERR_INVALID; }
   if ((rc = check_err(c))) return rc;
   if (count == 0) return 0;
-  return run_rs_ag(c, Coll::ALL_TO_ALL, in, out, count, dtype, FLEXAR_SUM, (hipStream_t)stream, nullptr, 1.0f);
+  return run_rs_ag(c, Coll::ALL_TO_ALL, in, out, count, dtype, FLEXAR_SUM, (hipStream_t)stream, algo, 1.0f);
+}
+
+int flexar_all_to_all(flexar_comm_t c, const void* in, void* out, size_t count, int dtype, void* stream) {
+  return flexar_all_to_all_ex(c, in, out, count, dtype, stream, nullptr);
 }
 
 int flexar_broadcast(flexar_comm_t c, const void* in, void* out, size_t count, int dtype, int root, void* stream,
@@ -2015,6 +2034,17 @@ struct GroupCtxStage {
   bool used = false;
 };
 static thread_local GroupCtxStage g_group_ctx;
+
+// In-process group running a zero-copy program: every rank's buffers are plain device pointers.
+static void group_zc_bind(std::vector<DevCtx>& h, int nranks, const void* const* ins, void* const* outs,
+                          uint64_t off_bytes) {
+  for (int r = 0; r < nranks; ++r)
+    for (int p = 0; p < nranks; ++p) {
+      h[r].peer_io[BUF_IN][p] = (char*)(ins && ins[p] ? ins[p] : outs[p]) + off_bytes;
+      h[r].peer_io[BUF_OUT][p] = (char*)outs[p] + off_bytes;
+      if ((((uintptr_t)h[r].peer_io[BUF_IN][p]) | ((uintptr_t)h[r].peer_io[BUF_OUT][p])) & 15) h[r].vec_ok = 0;
+    }
+}
 
 static int stage_group_ctx(const std::vector<DevCtx>& h, int nranks, hipStream_t st, DevCtx** out) {
   GroupCtxStage& g = g_group_ctx;
@@ -2099,18 +2129,14 @@ static int group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
     uint64_t n = std::min<uint64_t>(piece, count - off);
     std::vector<DevCtx> h(nranks);
     int grid = 0, wire = 0;
+    bool zc = false;
     for (int r = 0; r < nranks; ++r) {
       DevProgram* dp = nullptr;
       int rc = get_program(comms[r], specs[r], n, es, fs, &dp);
       if (rc) return rc;
       const char* in = ins && ins[r] ? (const char*)ins[r] : (const char*)outs[r];
       fill_ctx(comms[r], dp, in + off * es, (char*)outs[r] + off * es, &h[r]);
-      if (dp->prog.zc)  // one process: every rank's buffers are plain device pointers, no registration
-        for (int p = 0; p < nranks; ++p) {
-          h[r].peer_io[BUF_IN][p] = (char*)(ins && ins[p] ? ins[p] : outs[p]) + off * es;
-          h[r].peer_io[BUF_OUT][p] = (char*)outs[p] + off * es;
-          if ((((uintptr_t)h[r].peer_io[BUF_IN][p]) | ((uintptr_t)h[r].peer_io[BUF_OUT][p])) & 15) h[r].vec_ok = 0;
-        }
+      zc = zc || dp->prog.zc;
       if (amax_parts) h[r].amax_parts = amax_parts[r];
       wire = dp->prog.wire;
       int g = choose_grid(comms[r], n * es, dp->prog.nchan);
@@ -2121,6 +2147,7 @@ static int group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
       set_error("group grid too large: ranks x grid must stay <= 256 co-resident workgroups");
       return FLEXAR_ERR_INVALID;
     }
+    if (zc) group_zc_bind(h, nranks, ins, outs, off * es);
     if (int e = stage_group_ctx(h, nranks, st, &d_ctx)) return e;
     LaunchArgs la;
     la.kind = LAUNCH_GROUP;
@@ -2171,6 +2198,7 @@ int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const vo
   std::vector<DevCtx> h(nranks);
   int grid = 0;
   int proto = PM_FENCE;
+  bool zc = false;
   for (int r = 0; r < nranks; ++r) {
     AlgoSpec s;
     int rc = resolve_spec(comms[r], algo, (double)count * es * nranks, &s);
@@ -2181,9 +2209,11 @@ int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const vo
     if ((rc = get_program(comms[r], s, count, es, fs, &dp, (Coll)coll, count))) return rc;
     if (dp->prog.stg_bytes() > comms[r]->exec_half) { set_error("group collective exceeds workspace"); return FLEXAR_ERR_NOMEM; }
     fill_ctx(comms[r], dp, ins[r], outs[r], &h[r]);
+    zc = zc || dp->prog.zc;
     int g = choose_grid(comms[r], count * es * nranks, dp->prog.nchan);
     grid = r == 0 ? g : grid;
   }
+  if (zc) group_zc_bind(h, nranks, ins, outs, 0);
   if (int e = stage_group_ctx(h, nranks, st, &d_ctx)) return e;
   LaunchArgs la;
   la.kind = LAUNCH_GROUP;
@@ -2214,6 +2244,7 @@ int flexar_group_broadcast(flexar_comm_t* comms, int nranks, int root, const voi
   DevCtx* d_ctx = nullptr;
   std::vector<DevCtx> h(nranks);
   int grid = 0, proto = PM_FENCE;
+  bool zc = false;
   for (int r = 0; r < nranks; ++r) {
     AlgoSpec s;
     int rc = bcast_spec(comms[r], algo, (uint64_t)count * es, &s);
@@ -2224,9 +2255,11 @@ int flexar_group_broadcast(flexar_comm_t* comms, int nranks, int root, const voi
     if (dp->prog.stg_bytes() > comms[r]->exec_half) { set_error("group broadcast exceeds workspace"); return FLEXAR_ERR_NOMEM; }
     const void* in = ins && ins[r] ? ins[r] : outs[r];
     fill_ctx(comms[r], dp, in, outs[r], &h[r]);
+    zc = zc || dp->prog.zc;
     int g = choose_grid(comms[r], count * es, dp->prog.nchan);
     grid = r == 0 ? g : grid;
   }
+  if (zc) group_zc_bind(h, nranks, ins, outs, 0);
   if (int e = stage_group_ctx(h, nranks, st, &d_ctx)) return e;
   LaunchArgs la;
   la.kind = LAUNCH_GROUP;

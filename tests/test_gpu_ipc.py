@@ -591,6 +591,30 @@ def _zc_worker(rank, world, port, q):
             errs["unregistered"] = "accepted"
         except Exception as e:  # noqa: BLE001
             errs["unregistered"] = "refused" if "registered" in str(e) else str(e)
+        # the other collectives: only the buffers a peer addresses need registering (reduce-scatter: the
+        # inputs; all-gather / all-to-all / broadcast: the outputs)
+        m = 70001
+        big = torch.empty(3 * world * m + 128, device=dev)
+        rs_in, ag_out, a2a_out = big[:world * m], big[world * m + 64:2 * world * m + 64], big[2 * world * m + 128:]
+        regs = [comm.register(t) for t in (rs_in, ag_out, a2a_out)]
+        gen = torch.Generator().manual_seed(5)
+        alls = [torch.randn(world * m, generator=gen) for _ in range(world)]
+        rs_in.copy_(alls[rank].to(dev))
+        rs_out = torch.empty(m, device=dev)
+        comm.reduce_scatter(rs_in, rs_out, algo="flat+zc")
+        ag_in = alls[rank][:m].to(dev)
+        comm.all_gather(ag_in, ag_out, algo="flat+zc")
+        comm.all_to_all(rs_in, a2a_out, algo="flat+zc")
+        bsrc = alls[0][:m].to(dev) if rank == 0 else None
+        comm.broadcast(bsrc if rank == 0 else ag_out[:m], root=0, out=ag_out[:m], algo="flat+zc")
+        torch.cuda.synchronize()
+        total = torch.stack(alls).sum(0)
+        errs["rs"] = (rs_out.cpu() - total[rank * m:(rank + 1) * m]).abs().max().item()
+        errs["a2a"] = (a2a_out.cpu() - torch.cat([alls[q][rank * m:(rank + 1) * m] for q in range(world)])).abs().max().item()
+        errs["ag_tail"] = (ag_out[m:].cpu() - torch.cat([alls[q][:m] for q in range(1, world)])).abs().max().item()
+        errs["bcast"] = (ag_out[:m].cpu() - alls[0][:m]).abs().max().item()
+        for rid in regs:
+            comm.deregister(rid)
         comm.deregister(rx)
         comm.deregister(ry)
         errs["regs_left"] = comm._lib.flexar_reg_count(comm._h)

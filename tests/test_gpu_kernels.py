@@ -340,7 +340,7 @@ def test_group_ll_protocol(cuda, groups, dtype, n):
 
 
 @pytest.mark.parametrize("n", [2, 4, 8])
-@pytest.mark.parametrize("spec", ["flat", "ring", "flat+nts", "flat+wt", "ring+wt"])
+@pytest.mark.parametrize("spec", ["flat", "ring", "flat+nts", "flat+wt", "ring+wt", "flat+zc", "flat+zc+wt"])
 def test_group_reduce_scatter_all_gather(cuda, groups, n, spec):
     grp = groups[n]
     g = torch.Generator(device=cuda).manual_seed(41)
@@ -417,7 +417,7 @@ def test_group_broadcast(cuda, groups, n):
     g = torch.Generator(device=cuda).manual_seed(51)
     for dtype in (torch.float32, torch.bfloat16):
         for size in (3, 4099, 300007):
-            for spec in (None, "oneshot", "flat", "flat+wt"):
+            for spec in (None, "oneshot", "flat", "flat+wt", "flat+zc"):
                 for root in range(n):
                     src = torch.randn(size, device=cuda, generator=g).to(dtype)
                     ins = [src if r == root else torch.zeros_like(src) for r in range(n)]
@@ -463,10 +463,11 @@ def test_group_all_to_all(cuda, groups, n):
                     ins = [torch.randint(-100, 100, (n * m,), device=cuda, generator=g, dtype=dtype) for _ in range(n)]
                 else:
                     ins = [torch.randn(n * m, device=cuda, generator=g).to(dtype) for _ in range(n)]
-                outs = [torch.empty_like(x) for x in ins]
-                grp.collective("all_to_all", ins, outs)
-                torch.cuda.synchronize()
-                for p in range(n):
-                    want = torch.cat([ins[r][p * m:(p + 1) * m] for r in range(n)])
-                    assert torch.equal(outs[p], want), (dtype, m, p)
+                for spec in (None, "flat+zc"):  # staging exchange, zero copy into the peers' outputs
+                    outs = [torch.empty_like(x) for x in ins]
+                    grp.collective("all_to_all", ins, outs, algo=spec)
+                    torch.cuda.synchronize()
+                    for p in range(n):
+                        want = torch.cat([ins[r][p * m:(p + 1) * m] for r in range(n)])
+                        assert torch.equal(outs[p], want), (spec, dtype, m, p)
     grp.check()

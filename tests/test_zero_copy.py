@@ -56,3 +56,31 @@ def test_zero_copy_refused_outside_flat():
     for spec in ("ring+zc", "rhd+zc", "tree:2,2+zc"):
         with pytest.raises(nv.FlexarError):
             nv.simulate(spec, ins)
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 8, 12])
+def test_zero_copy_collectives(n):
+    """Reduce-scatter (pull), all-gather (push), all-to-all (push) and broadcast (root push) straight over
+    the peers' registered buffers."""
+    m = 1001
+    ins = [np.random.default_rng(r).integers(-50, 50, n * m).astype(np.int32) for r in range(n)]
+    tot = np.sum(ins, axis=0)
+    rs = nv.simulate_coll("reduce_scatter", "flat+zc", ins, m, dtype="int32", ncalls=3)
+    for r in range(n):
+        np.testing.assert_array_equal(rs[r], tot[r * m:(r + 1) * m])
+    ag_in = [np.random.default_rng(10 + r).integers(-50, 50, m).astype(np.int32) for r in range(n)]
+    for o in nv.simulate_coll("all_gather", "flat+zc", ag_in, m, dtype="int32", ncalls=3):
+        np.testing.assert_array_equal(o, np.concatenate(ag_in))
+    a2a = nv.simulate_coll("all_to_all", "flat+zc", ins, m, dtype="int32", ncalls=3)
+    for r in range(n):
+        np.testing.assert_array_equal(a2a[r], np.concatenate([ins[q][r * m:(r + 1) * m] for q in range(n)]))
+    data = np.arange(5003, dtype=np.float32)
+    for root in (0, n - 1):
+        for o in nv.simulate_bcast("flat+zc", data, n, root=root):
+            np.testing.assert_array_equal(o, data)
+
+
+def test_zero_copy_collectives_refuse_ring():
+    ins = [np.zeros(4 * 64, np.int32) for _ in range(4)]
+    with pytest.raises(nv.FlexarError):
+        nv.simulate_coll("reduce_scatter", "ring+zc", ins, 64, dtype="int32")
