@@ -258,6 +258,7 @@ struct flexar_comm {
   std::vector<Reg> regs;
   int next_reg = 1;
   std::map<std::string, std::pair<char*, int>> ipc_maps;  // (peer, handle) -> mapped base, references
+  bool zc_auto = true;  // FLEXAR_ZC_AUTO=0: automatic choices never switch to zero copy
   int* st_buf = nullptr;        // self-test buffers (device)
   uint32_t* st_bad = nullptr;   // self-test mismatch counter (host-mapped)
   uint32_t* st_bad_dev = nullptr;
@@ -491,6 +492,16 @@ static void fill_ctx(flexar_comm* c, DevProgram* dp, const void* in, void* out, 
   x->fi_kind = c->fi_kind;
   x->fi_slot = c->fi_slot;
   x->fi_ticks = c->fi_ticks;
+}
+
+// Both buffers of an allreduce inside registrations (what a zero-copy choice needs).
+static bool zc_registered(flexar_comm* c, const void* in, const void* out, uint64_t bytes) {
+  auto inside = [&](const void* p) {
+    for (const auto& r : c->regs)
+      if ((const char*)p >= r.base && (const char*)p + bytes <= r.base + r.bytes) return true;
+    return false;
+  };
+  return inside(in) && inside(out);
 }
 
 // ---- message transport (msg_plan.hpp over RCCL) ----------------------------------------------------
@@ -1045,6 +1056,7 @@ static void init_defaults(flexar_comm* c) {
   if (const char* m = getenv("FLEXAR_MODEL")) c->links_from_env = std::count(m, m + strlen(m), ',') >= 4;
   c->have_tune = c->tune.load(getenv("FLEXAR_TUNE_FILE"));
   c->timeout_ticks = env_u64("FLEXAR_TIMEOUT_MS", 20000) * 100000ull;  // 100 MHz s_memrealtime
+  c->zc_auto = env_u64("FLEXAR_ZC_AUTO", 1) != 0;
   c->max_grid = (int)env_u64("FLEXAR_MAX_GRID", 256);
   if (c->max_grid < 1) c->max_grid = 1;
   if (c->max_grid > (int)kMaxGridBlocks) c->max_grid = kMaxGridBlocks;
@@ -1719,8 +1731,8 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
   memcpy(&fsb, &fs, 4);
   const char* akey = algo ? algo : "";
   flexar_comm::CallMemo& m = c->memo[((uint64_t)count * 0x9E3779B97F4A7C15ull + (uint64_t)dtype * 31u + (uint64_t)op) >> 60];
-  const bool hit = m.gen == c->memo_gen && m.count == count && m.dtype == dtype && m.op == op && m.fsb == fsb &&
-                   m.algo == akey;
+  bool hit = m.gen == c->memo_gen && m.count == count && m.dtype == dtype && m.op == op && m.fsb == fsb &&
+             m.algo == akey;
   AlgoSpec s;
   if (hit) {
     s = m.s;
@@ -1739,6 +1751,37 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     if ((rc = executor_proto(c, &s))) return rc;
   }
   if (s.msg) s.wire = 0;  // the message transport runs the schedule untyped
+  // Registered buffers (flexar_reg_*): a flat schedule the call did not name explicitly - the cost model's
+  // or the tune table's choice - runs zero copy ("+zc+push": no staging), and a zero-copy choice from a
+  // tune table falls back to the staging schedule for buffers that are not registered. Registration is
+  // collective, so every rank decides alike. An explicit "+zc" on unregistered buffers stays an error.
+  if (!c->regs.empty() || s.zc) {
+    const bool named = algo && *algo && strcmp(algo, "auto") != 0;
+    const bool from_auto = !named && c->spec.kind == AlgoKind::AUTO;
+    const bool flat = s.kind == AlgoKind::TREE && s.widths.size() == 1 && !s.msg && s.wire == 0 && c->nranks > 1;
+    const bool reg = c->nranks > 1 && !s.msg && s.wire == 0 && zc_registered(c, in, out, (uint64_t)count * es);
+    if (reg && !s.zc && from_auto && c->zc_auto && s.kind != AlgoKind::DMA) {
+      // the flat schedule always gains; another model choice (oneshot, LL, ring, trees) only when the cost
+      // model prices the zero-copy push form lower (a tune table's measured choice is kept)
+      AlgoSpec z;
+      z.kind = AlgoKind::TREE;
+      z.widths = {c->nranks};
+      z.ag = AgMode::PUSH;
+      z.zc = true;
+      z.wt = s.wt;
+      z.nts = s.nts;
+      const double bytes = (double)count * es;
+      if (c->disabled & proto_family(z)) {
+        // the zero-copy form's protocol family failed the connect-time self-test: keep the verified choice
+      } else if (flat || (!c->have_tune && c->model.cost_us(z, c->nranks, bytes) < c->model.cost_us(s, c->nranks, bytes))) {
+        s = z;
+        hit = hit && m.s.zc;
+      }
+    } else if (flat && s.zc && !reg && !named) {
+      s.zc = false;
+      hit = hit && !m.s.zc;
+    }
+  }
   auto remember = [&](uint64_t piece, DevProgram* dp, int grid) {
     if (hit) return;
     m.gen = c->memo_gen;

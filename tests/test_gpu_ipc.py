@@ -551,7 +551,7 @@ def test_ipc_connect_readiness_gate(cuda, fault):
 def _zc_worker(rank, world, port, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
-                          FLEXAR_TIMEOUT_MS="20000")
+                          FLEXAR_TIMEOUT_MS="20000", FLEXAR_PROFILE="1")
         import torch.distributed as dist
 
         torch.cuda.set_device(0)
@@ -615,6 +615,18 @@ def _zc_worker(rank, world, port, q):
         errs["bcast"] = (ag_out[:m].cpu() - alls[0][:m]).abs().max().item()
         for rid in regs:
             comm.deregister(rid)
+        # automatic choice (no spec): registered buffers run zero copy, unregistered ones the staging path,
+        # and both give exact sums
+        x.fill_(1.0)
+        comm.all_reduce(x, out=y)
+        z = torch.ones(n, device=dev)
+        comm.all_reduce(z)
+        torch.cuda.synchronize()
+        errs["auto_registered"] = (y - world).abs().max().item()
+        errs["auto_unregistered"] = (z - world).abs().max().item()
+        prof = comm.stats()["profile"]
+        errs["auto_used_zc"] = 0.0 if any("+zc" in k for k in prof) else 1.0
+        errs["auto_used_staging"] = 0.0 if any("+zc" not in k for k in prof) else 1.0
         comm.deregister(rx)
         comm.deregister(ry)
         errs["regs_left"] = comm._lib.flexar_reg_count(comm._h)
