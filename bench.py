@@ -190,7 +190,7 @@ def main():
             log(rank, f"zero-copy candidates skipped: {e}")
             return False
 
-    zc = register_buffers(comm)
+    zc = False  # registered after the cost-model measurement (which runs the unregistered, staging path)
 
     def max_over_ranks(v: float) -> float:
         if world == 1:
@@ -268,6 +268,18 @@ def main():
             log(rank, f"cost model: {choice} predicted {model['predicted_us']} us, measured {model['measured_us']} us")
         except nv.FlexarError as e:
             model = {"error": str(e)}
+    zc = register_buffers(comm)
+    if model and "error" not in model and zc:
+        # the same automatic choice once the buffers are registered: the flat schedule (or any choice the
+        # model prices higher than the zero-copy push form) runs "+zc+push" (comm.hip, FLEXAR_ZC_AUTO)
+        try:
+            ok1, _ = check("auto")
+            t1 = timed("auto", 5) if max_over_ranks(0.0 if ok1 else 1.0) == 0.0 else None
+            model["registered_measured_us"] = round(t1 * 1e6, 1) if t1 else None
+            model["registered_busbw_GBps"] = round(busbw_gbps(nbytes, t1, world), 2) if t1 else None
+            model["registered_correct"] = ok1
+        except nv.FlexarError as e:
+            model["registered_error"] = str(e)
 
     # ---------------------------------------------------------------- start-up tuner
     algo = args.algo
