@@ -102,6 +102,7 @@ def _sig(lib):
         "flexar_reg_close": (i, [vp, i]),
         "flexar_reg_count": (i, [vp]),
         "flexar_reg_find": (i, [vp, vp, sz]),
+        "flexar_reg_ids": (i, [vp, c.POINTER(i), i]),
         "flexar_model_features": (i, [cp, i, d, i, c.POINTER(d)]),
         "flexar_kernel_info": (i, [i, i, i, i, c.POINTER(i), c.POINTER(i)]),
         "flexar_downgrade_spec": (i, [cp, i, u32, i, cp, sz]),

@@ -375,6 +375,12 @@ class Communicator:
                 self._lib.flexar_reg_close(self._h, rid.value)
             raise nv.FlexarError(rc or 1, "register: " + "; ".join(bad))
         self._regs[rid.value] = tensor
+        # a registration this one replaced (contained in it) is gone on the native side: drop its reference
+        ids = (ctypes.c_int * 4096)()
+        k = self._lib.flexar_reg_ids(self._h, ids, 4096)
+        live = set(ids[:min(k, 4096)])
+        for old in [r for r in self._regs if r not in live]:
+            del self._regs[old]
         return rid.value
 
     def deregister(self, rid: int):

@@ -173,8 +173,9 @@ int flexar_reg_export(flexar_comm_t comm, const void* ptr, size_t bytes, void* o
 int flexar_reg_open(flexar_comm_t comm, const void* ptr, size_t bytes, const void* all_blobs, int* id_out);
 int flexar_reg_close(flexar_comm_t comm, int id);
 int flexar_reg_count(flexar_comm_t comm);
+int flexar_reg_ids(flexar_comm_t comm, int* ids_out, int max); /* current registration ids; returns the count */
 /* Registration holding [ptr, ptr + bytes): its id, 0 if none, -1 if its allocation was freed and the address
- * reused (stale peer mappings). A new registration overlapping old ones replaces them. */
+ * reused (stale peer mappings). A new registration replaces the old ones it contains or that are stale. */
 int flexar_reg_find(flexar_comm_t comm, const void* ptr, size_t bytes);
 /* JSON: per-peer PCI bus id, device ordinal, link class (same-device / xgmi / pcie / unknown) and hop
  * count from the connect-time probe; links used by the cost model; self-test state. */

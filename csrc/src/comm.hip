@@ -1443,12 +1443,16 @@ int flexar_reg_open(flexar_comm_t c, const void* ptr, size_t bytes, const void* 
   }
   std::lock_guard<std::mutex> lk(c->mu);
   FX_HIP(hipSetDevice(c->device));
-  // a new registration of (part of) a registered range replaces the old one (the buffer was freed and its
-  // address reused, or a call outgrew it): every rank registers together, so every rank drops it
+  // a new registration replaces an overlapping old one whose allocation is gone (freed, address reused:
+  // stale peer mappings) or which it contains (a call outgrew it); every rank registers together, so
+  // every rank drops it. Other overlaps (a tensor inside a registered arena) coexist.
   bool synced = false;
   for (size_t i = c->regs.size(); i-- > 0;) {
     const flexar_comm::Reg& o = c->regs[i];
-    if ((const char*)ptr < o.base + o.bytes && o.base < (const char*)ptr + bytes) {
+    const bool overlap = (const char*)ptr < o.base + o.bytes && o.base < (const char*)ptr + bytes;
+    const bool contains = (const char*)ptr <= o.base && o.base + o.bytes <= (const char*)ptr + bytes;
+    const bool stale = o.bufid && buffer_id(o.base) != o.bufid;
+    if (overlap && (contains || stale)) {
       if (!synced) FX_HIP(hipDeviceSynchronize());
       synced = true;
       reg_drop(c, i);
@@ -1541,6 +1545,15 @@ int flexar_reg_find(flexar_comm_t c, const void* p, size_t bytes) {
 }
 
 int flexar_reg_count(flexar_comm_t c) { return c ? (int)c->regs.size() : -1; }
+
+int flexar_reg_ids(flexar_comm_t c, int* out, int max) {
+  if (!c) return -1;
+  std::lock_guard<std::mutex> lk(c->mu);
+  int n = 0;
+  for (const auto& r : c->regs)
+    if (n < max && out) out[n++] = r.id;
+  return (int)c->regs.size();
+}
 
 int flexar_comm_set_model(flexar_comm_t c, double alpha_launch_us, double alpha_sync_us, double link_gbps,
                           double hbm_gbps, int links) {
