@@ -296,7 +296,7 @@ def main():
         if comm.topology().get("rccl"):  # the schedules over RCCL send/recv as well
             cands += ["flat+rccl", "ring+rccl"] + (["rhd+rccl"] if world > 2 and not world & (world - 1) else [])
         if zc:  # registered buffers: the flat schedule straight from / to the peers' x and y
-            cands += ["flat+zc", "flat+zc+nts", "flat+zc+wt", "flat+zc+push", "flat+zc+push+wt"]
+            cands += ["flat+zc", "flat+zc+nts", "flat+zc+wt", "flat+zc+push", "flat+zc+push+nts", "flat+zc+push+wt"]
         timings = {}
         for spec in cands:
             failed = 0.0
