@@ -323,10 +323,11 @@ def _captured_worker(rank, world, port, q):
         from allreduce_over_mpi_amd.parallel import CapturedAllReduce, Communicator
 
         comm = Communicator(workspace_bytes=64 << 20)
-        sizes = [64, 16384, 1 << 18]
+        sizes = [64, 16384, 1 << 18, 300001]
         bufs = [torch.empty(n, device="cuda") for n in sizes]
-        outs = [None, torch.empty(sizes[1], device="cuda"), None]
-        cap = CapturedAllReduce(comm, bufs, outs=outs, algo=[None, "oneshot", "dma"])
+        outs = [None, torch.empty(sizes[1], device="cuda"), None, None]
+        comm.register(bufs[3])  # zero copy replays from a graph too (the peers' pointers are bound at capture)
+        cap = CapturedAllReduce(comm, bufs, outs=outs, algo=[None, "oneshot", "dma", "flat+zc+push"])
         errs = []
         for it in range(5):
             xs = [[torch.randn(n, generator=torch.Generator().manual_seed(1000 * it + 10 * r + k))
@@ -356,8 +357,8 @@ def _captured_worker(rank, world, port, q):
 
 
 def test_captured_allreduce_replays(cuda):
-    """CapturedAllReduce: LL / oneshot / dma-requested calls captured in one graph, replayed with new inputs;
-    eager calls (dma included) stay correct afterwards."""
+    """CapturedAllReduce: LL / oneshot / dma-requested / zero-copy calls captured in one graph, replayed with
+    new inputs; eager calls (dma included) stay correct afterwards."""
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
@@ -371,7 +372,7 @@ def test_captured_allreduce_replays(cuda):
         p.join(timeout=60)
     for rank, errs, tb in res:
         assert tb is None, tb
-        assert len(errs) == 18 and max(errs) < 1e-4, errs
+        assert len(errs) == 23 and max(errs) < 1e-4, errs
 
 
 def _stress_worker(rank, world, port, calls, q, fault=""):
