@@ -392,6 +392,7 @@ class FlexarHookState:
             zero_copy = os.environ.get("FLEXAR_HOOK_ZC", "0") == "1"
         self.zero_copy = bool(zero_copy) and self.comm.world_size > 1 and hasattr(self.comm, "register")
         self._bucket_regs = {}  # bucket index -> (data_ptr, nbytes, registration id)
+        self.registrations = 0  # buckets registered so far (first sight + DDP's one bucket rebuild)
         grid = grid if grid is not None else int(os.environ.get("FLEXAR_HOOK_GRID", "0") or 0)
         if grid and hasattr(self.comm, "set_grid"):
             self.comm.set_grid(grid)
@@ -408,6 +409,7 @@ class FlexarHookState:
                 self.comm.deregister(have[2])
             try:
                 self._bucket_regs[key] = (buf.data_ptr(), nbytes, self.comm.register(buf))
+                self.registrations += 1
             except nv.FlexarError:  # zero copy not usable here (every rank raises together): staging
                 self.zero_copy = False
                 return self.algo
