@@ -105,6 +105,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("FLEXAR_BENCH_TRACEBACK_S"):  # debugging aid: every rank's Python stacks, periodically
+        import faulthandler
+
+        faulthandler.dump_traceback_later(int(os.environ["FLEXAR_BENCH_TRACEBACK_S"]), repeat=True)
 
     import torch
     import torch.distributed as dist
@@ -165,14 +169,18 @@ def main():
     comm = make_comm()
     if comm is None:
         comm, fallback = RcclOnly(dist), "flexar communicator could not be created"
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(1234 + rank)
-    x = torch.randn(count, device=dev, dtype=torch.float32, generator=gen)
-    if dtype == torch.float8_e4m3fn:
-        x = x * 8  # fp8 e4m3 range: |x| <= 448
-    x = x.to(dtype)
+    # the three buffers first, each its own allocation (registration maps whole allocations into the peers;
+    # a temporary freed first would leave a larger block the allocator carves them from)
+    x = torch.empty(count, device=dev, dtype=dtype)
     y = torch.empty_like(x)
     xs = torch.empty_like(x)  # scaled copies of x for the stale-staging check
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + rank)
+    x0 = torch.randn(count, device=dev, dtype=torch.float32, generator=gen)
+    if dtype == torch.float8_e4m3fn:
+        x0 = x0 * 8  # fp8 e4m3 range: |x| <= 448
+    x.copy_(x0.to(dtype))
+    del x0
     zc_note = None
 
     def register_buffers(cm):

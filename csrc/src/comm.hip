@@ -1421,8 +1421,20 @@ int flexar_reg_export(flexar_comm_t c, const void* ptr, size_t bytes, void* out)
       set_error("registered range exceeds its allocation");
       return FLEXAR_ERR_INVALID;
     }
+    // Importing a peer allocation larger than ~1 GiB through HIP IPC after other imports hangs in
+    // hipIpcOpenMemHandle on this platform (ROCm 7, dmabuf IPC; reproduced with hipMalloc'd and torch
+    // allocations of 2 GiB+, bench/reg_repro.py), so such allocations are refused up front instead
+    // (every rank then keeps the staging schedules). FLEXAR_REG_MAX_ALLOC overrides the cap.
+    const uint64_t cap = env_u64("FLEXAR_REG_MAX_ALLOC", 1ull << 30);
+    if (size > cap) {
+      set_error("registering: the buffer lies in an allocation of " + std::to_string(size) + " bytes, above the " +
+                std::to_string(cap) + "-byte cap for IPC-mapped registrations (allocate it on its own)");
+      return FLEXAR_ERR_UNSUPPORTED;
+    }
     FX_HIP(hipIpcGetMemHandle(&b.h, base));
     b.offset = (uint64_t)((const char*)ptr - (const char*)base);
+    logf(LOG_DEBUG, c->rank, "registering: buffer %p (%zu bytes) lies in allocation %p (%zu bytes) at +%llu", ptr,
+         bytes, base, size, (unsigned long long)b.offset);
   }
   b.bytes = bytes;
   b.device = c->device;
@@ -1446,6 +1458,7 @@ int flexar_reg_open(flexar_comm_t c, const void* ptr, size_t bytes, const void* 
   // a new registration replaces an overlapping old one whose allocation is gone (freed, address reused:
   // stale peer mappings) or which it contains (a call outgrew it); every rank registers together, so
   // every rank drops it. Other overlaps (a tensor inside a registered arena) coexist.
+  logf(LOG_DEBUG, c->rank, "registering %zu bytes at %p (%zu registrations)", bytes, ptr, c->regs.size());
   bool synced = false;
   for (size_t i = c->regs.size(); i-- > 0;) {
     const flexar_comm::Reg& o = c->regs[i];
@@ -1494,7 +1507,10 @@ int flexar_reg_open(flexar_comm_t c, const void* ptr, size_t bytes, const void* 
       it->second.second++;
     } else {
       void* q = nullptr;
+      logf(LOG_DEBUG, c->rank, "registering: opening rank %d's allocation (buffer at +%llu, %zu bytes)", p,
+           (unsigned long long)b.offset, bytes);
       hipError_t e = hipIpcOpenMemHandle(&q, b.h, hipIpcMemLazyEnablePeerAccess);
+      logf(LOG_DEBUG, c->rank, "registering: rank %d's allocation mapped (%s)", p, hipGetErrorString(e));
       if (e != hipSuccess) {
         undo();
         set_error("registering: mapping rank " + std::to_string(p) + "'s buffer failed: hipIpcOpenMemHandle: " +
