@@ -189,6 +189,9 @@ def main():
         nonlocal zc_note
         if world == 1 or not isinstance(cm, Communicator):
             return False
+        if os.environ.get("FLEXAR_BENCH_ZC", "1") == "0":
+            zc_note = "disabled (FLEXAR_BENCH_ZC=0)"
+            return False
         try:
             for t in (x, xs, y):
                 cm.register(t)
