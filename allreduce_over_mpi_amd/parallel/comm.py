@@ -142,8 +142,10 @@ class Communicator:
             # a rank that failed to map a peer must not leave the others waiting in a later collective
             msg = b"" if rc == 0 else f"{rc}:rank {self.rank}: {nv.last_error()}".encode()
             bad = [m.decode(errors="replace") for m in exchange(msg) if m]
-            # only a failed peer mapping (HIP error) falls back; settings mismatches etc. stay errors
-            mapping_only = bool(bad) and all(b.split(":", 1)[0] == "3" for b in bad)
+            # no peer memory (a failed peer mapping = HIP error 3; no P2P path between the GPUs or ranks on
+            # different hosts = unsupported 2) falls back to the message transport; settings mismatches
+            # (invalid 1) stay errors
+            mapping_only = bool(bad) and all(b.split(":", 1)[0] in ("2", "3") for b in bad)
             fallback = bool(bad) and transport == "auto" and mapping_only and self._lib.flexar_rccl_available()
             if bad and not fallback:
                 self.close()
