@@ -392,6 +392,12 @@ def _stress_worker(rank, world, port, calls, q, fault=""):
         comm = Communicator(workspace_bytes=32 << 20)
         specs = ["flat", "flat+push", "flat+wt", "flat+push+nts", "ring", "ring+wt", "oneshot", "ll", "dma",
                  "rhd", "tree:2,2+push"] if world == 4 else ["flat", "flat+push+wt", "ring", "oneshot", "ll", "dma"]
+        specs += ["flat+zc", "flat+zc+push"]
+        # zero-copy calls run on registered arenas (the same offsets on every rank: the same call sequence)
+        arena_in = torch.empty(world * 2_000_003 + 64, device="cuda")
+        arena_out = torch.empty(world * 2_000_003 + 64, device="cuda")
+        comm.register(arena_in)
+        comm.register(arena_out)
         rnd = random.Random(1234)  # same call sequence on every rank
         side = torch.cuda.Stream()
         main = torch.cuda.current_stream()
@@ -426,21 +432,33 @@ def _stress_worker(rank, world, port, calls, q, fault=""):
                 x = allx[rank][:m].to("cuda")
                 out = torch.empty(m * world, device="cuda")
                 want = allx[:, :m].reshape(-1)
+            zc = "zc" in spec
+            if zc:  # move the operands into the arenas once every earlier call on either stream is done
+                main.wait_stream(side)
+                off = it % 64  # a different (same-on-every-rank) offset each time
+                ax = arena_in[off:off + x.numel()]
+                ax.copy_(x)
+                x = ax
+                ao = arena_out[off:off + (out.numel() if out is not None else x.numel())]
+                out = ao if out is not None else None
             stream.wait_stream(main)  # x and out were made on the main stream
             # NO host synchronisation between calls: consecutive calls on different streams must still be
             # serialised by the communicator (every collective shares the epochs and staging halves)
             with torch.cuda.stream(stream):
                 busy = torch.randn(1 << 20, device="cuda").square_().sum()  # compute sharing the GPU
+                calgo = "flat+zc" if zc else ("ring" if "ring" in spec else None)
                 if coll == "allreduce":
                     y = comm.all_reduce(x, out=out, algo=spec)
                 elif coll == "broadcast":
-                    y = comm.broadcast(x, root=root, out=out)
+                    y = comm.broadcast(x, root=root, out=out, algo="flat+zc" if zc else None)
                 elif coll == "all_to_all":
-                    y = comm.all_to_all(x, out)
+                    y = comm.all_to_all(x, out, algo="flat+zc" if zc else None)
                 elif coll == "reduce_scatter":
-                    y = comm.reduce_scatter(x, out, algo="ring" if "ring" in spec else None)
+                    y = comm.reduce_scatter(x, out, algo=calgo)
                 else:
-                    y = comm.all_gather(x, out, algo="ring" if "ring" in spec else None)
+                    y = comm.all_gather(x, out, algo=calgo)
+                if zc:
+                    y = y.clone()  # the arenas are reused by later calls
             # keep x alive until the end: freed now, the caching allocator would hand its block to the next
             # iteration (main stream) while this call may still read it on the side stream
             pending.append((it, coll + ":" + spec, n, in_place, use_side, y, want, (x, busy)))
