@@ -385,6 +385,48 @@ class Communicator:
             del self._regs[old]
         return rid.value
 
+    def register_many(self, tensors) -> list:
+        """:meth:`register` for several tensors with one handle exchange and one agreement round (every
+        rank passes its corresponding tensors in the same order). Returns the registration ids."""
+        tensors = list(tensors)
+        if self.world_size == 1 or not tensors:
+            return [self.register(t) for t in tensors]
+        if self._zc_ok is None:
+            self._zc_ok = False
+            self._zc_ok = self._zc_selftest()
+        if self._zc_ok is False:
+            raise nv.FlexarError(2, "register: zero copy failed its readiness check on this node "
+                                    "(peer buffers did not read back exactly); use the staging schedules")
+        hs = int(self._lib.flexar_reg_handle_size())
+        blobs, err = [], ""
+        for t in tensors:
+            _require_cuda(t)
+            b = ctypes.create_string_buffer(hs)
+            if self._lib.flexar_reg_export(self._h, t.data_ptr(), t.numel() * t.element_size(), b):
+                err = nv.last_error()
+                break
+            blobs.append(bytes(b.raw))
+        rows = self._exchange(b"".join(blobs) if not err else b"")
+        if any(len(r) != hs * len(tensors) for r in rows):
+            raise nv.FlexarError(1, f"register: export failed on rank(s) "
+                                    f"{[i for i, r in enumerate(rows) if len(r) != hs * len(tensors)]} {err}".rstrip())
+        ids, msg = [], b""
+        for k, t in enumerate(tensors):
+            all_k = b"".join(r[k * hs:(k + 1) * hs] for r in rows)
+            rid = ctypes.c_int(0)
+            if self._lib.flexar_reg_open(self._h, t.data_ptr(), t.numel() * t.element_size(), all_k, ctypes.byref(rid)):
+                msg = f"rank {self.rank}: {nv.last_error()}".encode()
+                break
+            ids.append(rid.value)
+        bad = [m.decode(errors="replace") for m in self._exchange(msg) if m]
+        if bad:
+            for rid in ids:
+                self._lib.flexar_reg_close(self._h, rid)
+            raise nv.FlexarError(1, "register: " + "; ".join(bad))
+        for rid, t in zip(ids, tensors):
+            self._regs[rid] = t
+        return ids
+
     def deregister(self, rid: int):
         """Drop a registration (every rank, once the calls using it have completed)."""
         nv.check(self._lib.flexar_reg_close(self._h, int(rid)), "deregister")

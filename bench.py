@@ -193,8 +193,7 @@ def main():
             zc_note = "disabled (FLEXAR_BENCH_ZC=0)"
             return False
         try:
-            for t in (x, xs, y):
-                cm.register(t)
+            cm.register_many([x, xs, y])
             return True
         except nv.FlexarError as e:
             zc_note = f"registration failed: {e}"

@@ -615,7 +615,7 @@ def _zc_worker(rank, world, port, q):
         m = 70001
         big = torch.empty(3 * world * m + 128, device=dev)
         rs_in, ag_out, a2a_out = big[:world * m], big[world * m + 64:2 * world * m + 64], big[2 * world * m + 128:]
-        regs = [comm.register(t) for t in (rs_in, ag_out, a2a_out)]
+        regs = comm.register_many([rs_in, ag_out, a2a_out])  # one exchange for the three
         gen = torch.Generator().manual_seed(5)
         alls = [torch.randn(world * m, generator=gen) for _ in range(world)]
         rs_in.copy_(alls[rank].to(dev))
