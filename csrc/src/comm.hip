@@ -654,6 +654,17 @@ static int run_rs_ag(flexar_comm* c, Coll coll, const void* in, void* out, size_
   if (s.kind != AlgoKind::RING) s.kind = AlgoKind::TREE, s.widths = {c->nranks}, s.ag = AgMode::PUSH;
   if ((rc = executor_proto(c, &s))) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
+  // registered buffers and no named spec: the direct exchange runs zero copy (the buffer the peers address
+  // - reduce-scatter: the input, all-gather / all-to-all: the output - must lie inside a registration)
+  if (!c->regs.empty() && !s.zc && !s.msg && c->zc_auto && s.kind == AlgoKind::TREE && c->nranks > 1 &&
+      !(algo && *algo && strcmp(algo, "auto") != 0) && c->spec.kind == AlgoKind::AUTO &&
+      !(c->disabled & proto_family(s))) {
+    const uint64_t wide = (uint64_t)c->nranks * count * es;
+    const bool rs = coll == Coll::REDUCE_SCATTER;
+    const void* p = rs ? in : out;
+    for (const auto& r : c->regs)
+      if ((const char*)p >= r.base && (const char*)p + wide <= r.base + r.bytes) { s.zc = true; break; }
+  }
   if ((rc = order_call(c, st))) return rc;
   if (s.msg) {
     s.wire = 0;

@@ -619,19 +619,21 @@ def _zc_worker(rank, world, port, q):
         gen = torch.Generator().manual_seed(5)
         alls = [torch.randn(world * m, generator=gen) for _ in range(world)]
         rs_in.copy_(alls[rank].to(dev))
-        rs_out = torch.empty(m, device=dev)
-        comm.reduce_scatter(rs_in, rs_out, algo="flat+zc")
-        ag_in = alls[rank][:m].to(dev)
-        comm.all_gather(ag_in, ag_out, algo="flat+zc")
-        comm.all_to_all(rs_in, a2a_out, algo="flat+zc")
-        bsrc = alls[0][:m].to(dev) if rank == 0 else None
-        comm.broadcast(bsrc if rank == 0 else ag_out[:m], root=0, out=ag_out[:m], algo="flat+zc")
-        torch.cuda.synchronize()
         total = torch.stack(alls).sum(0)
-        errs["rs"] = (rs_out.cpu() - total[rank * m:(rank + 1) * m]).abs().max().item()
-        errs["a2a"] = (a2a_out.cpu() - torch.cat([alls[q][rank * m:(rank + 1) * m] for q in range(world)])).abs().max().item()
-        errs["ag_tail"] = (ag_out[m:].cpu() - torch.cat([alls[q][:m] for q in range(1, world)])).abs().max().item()
-        errs["bcast"] = (ag_out[:m].cpu() - alls[0][:m]).abs().max().item()
+        for calgo in ("flat+zc", None):  # explicit, and the automatic switch on registered buffers
+            rs_out = torch.empty(m, device=dev)
+            comm.reduce_scatter(rs_in, rs_out, algo=calgo)
+            ag_in = alls[rank][:m].to(dev)
+            comm.all_gather(ag_in, ag_out, algo=calgo)
+            comm.all_to_all(rs_in, a2a_out, algo=calgo)
+            bsrc = alls[0][:m].to(dev) if rank == 0 else None
+            comm.broadcast(bsrc if rank == 0 else ag_out[:m], root=0, out=ag_out[:m], algo="flat+zc")
+            torch.cuda.synchronize()
+            errs[f"rs_{calgo}"] = (rs_out.cpu() - total[rank * m:(rank + 1) * m]).abs().max().item()
+            errs[f"a2a_{calgo}"] = (a2a_out.cpu() - torch.cat([alls[q][rank * m:(rank + 1) * m]
+                                                               for q in range(world)])).abs().max().item()
+            errs[f"ag_tail_{calgo}"] = (ag_out[m:].cpu() - torch.cat([alls[q][:m] for q in range(1, world)])).abs().max().item()
+            errs[f"bcast_{calgo}"] = (ag_out[:m].cpu() - alls[0][:m]).abs().max().item()
         for rid in regs:
             comm.deregister(rid)
         # automatic choice (no spec): registered buffers run zero copy, unregistered ones the staging path,
