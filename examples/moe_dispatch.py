@@ -2,10 +2,13 @@
 """Expert-parallel MoE token dispatch / combine with equal-capacity all-to-all on the "flexar" backend.
 
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 examples/moe_dispatch.py
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 examples/moe_dispatch.py --zero-copy
 
 Every rank hosts one expert. Tokens are routed top-1 with a fixed capacity per (source rank, expert),
 so dispatch and combine are equal-split ``dist.all_to_all_single`` calls, which flexar runs as one
-direct exchange over all xGMI links. The result is checked against running every expert locally.
+direct exchange over all xGMI links. With ``--zero-copy`` the receive buffers are registered once with a
+flexar Communicator and every rank writes its tokens straight into the peers' buffers (no staging). The
+result is checked against running every expert locally.
 """
 from __future__ import annotations
 
@@ -16,8 +19,14 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
+    import argparse
+
     import torch
     import torch.distributed as dist
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--zero-copy", action="store_true", help="registered receive buffers, zero-copy all-to-all")
+    args = ap.parse_args()
 
     from allreduce_over_mpi_amd.parallel import backend as _fb  # noqa: F401
 
@@ -41,11 +50,19 @@ def main():
         send[e, :len(idx)] = x[idx]
         kept[e, :len(idx)] = idx
     recv = torch.empty_like(send)
-    dist.all_to_all_single(recv.view(-1), send.view(-1))          # dispatch
+    back = torch.empty_like(send)
+    if args.zero_copy:  # persistent dispatch / combine buffers, registered once (collective)
+        from allreduce_over_mpi_amd.parallel import Communicator
+
+        comm = Communicator()
+        comm.register_many([recv, back])
+        a2a = lambda out, inp: comm.all_to_all(inp, out)  # noqa: E731 - registered out: zero copy
+    else:
+        a2a = lambda out, inp: dist.all_to_all_single(out, inp)  # noqa: E731
+    a2a(recv.view(-1), send.view(-1))                              # dispatch
     with torch.no_grad():
         out = experts[rank](recv.view(-1, d)).view(world, cap, d)  # this rank's expert on every source
-    back = torch.empty_like(out)
-    dist.all_to_all_single(back.view(-1), out.contiguous().view(-1))  # combine
+    a2a(back.view(-1), out.contiguous().view(-1))                  # combine
     y = torch.zeros_like(x)
     with torch.no_grad():
         for e in range(world):
@@ -54,7 +71,7 @@ def main():
             ref = experts[e](x[kept[e][m]])
             assert torch.allclose(back[e][m], ref, atol=1e-4), "all-to-all dispatch/combine mismatch"
     if rank == 0:
-        print(f"moe dispatch/combine ok: {world} experts, capacity {cap}, d={d}")
+        print(f"moe dispatch/combine ok: {world} experts, capacity {cap}, d={d}, zero copy {args.zero_copy}")
     dist.destroy_process_group()
 
 
