@@ -307,7 +307,12 @@ class Communicator:
 
         The first registration runs the zero-copy readiness check (:meth:`_zc_selftest`, like the
         connect-time self-test of the staging protocols): if the peers' buffers do not read back exactly
-        on this node, every rank raises here and callers keep the staging schedules."""
+        on this node, every rank raises here and callers keep the staging schedules. The peers map the
+        whole allocation holding the tensor; allocations above 1 GiB are refused (FLEXAR_REG_MAX_ALLOC;
+        docs/DESIGN.md §17), so allocate large registered buffers on their own.
+
+        Once registered, calls with no named spec switch to zero copy by themselves (FLEXAR_ZC_AUTO):
+        allreduce when the cost model prefers it, reduce-scatter / all-gather / all-to-all always."""
         _require_cuda(tensor)
         if self.world_size > 1 and self._zc_ok is None:
             self._zc_ok = False  # (re-entry from the self-test's own registration)
