@@ -60,6 +60,22 @@ def _worker(rank, world, port, specs, q, transport="rccl", no_ipc=False):
                             err = ((y.double().cpu() - want).abs().max() / (want.abs().max() + 1e-12)).item()
                             worst = max(worst, err)
                         results[(spec, str(dtype), size, op)] = worst
+        if not no_ipc:  # zero copy across devices: peers read / write registered buffers over xGMI
+            for dtype in (torch.float32, torch.bfloat16):
+                arena = torch.empty(1000003, device=dev, dtype=dtype)
+                out = torch.empty_like(arena)
+                comm.register_many([arena, out])
+                for spec in ("flat+zc", "flat+zc+push", "flat+zc+push+wt"):
+                    for size in (5, 4096, 1000003):
+                        xs = [torch.randn(size, generator=torch.Generator().manual_seed(7 * r + size)).to(dtype)
+                              for r in range(world)]
+                        ref = torch.stack([x.double() for x in xs]).sum(0)
+                        for call in range(3):  # consecutive calls: the closing hand-off
+                            arena[:size].copy_(xs[rank].to(dev))
+                            comm.all_reduce(arena[:size], out=out[:size], algo=spec)
+                        torch.cuda.synchronize()
+                        err = ((out[:size].double().cpu() - ref).abs().max() / (ref.abs().max() + 1e-12)).item()
+                        results[(spec, str(dtype), size, "sum")] = err
         comm.check()
         results["readiness"] = (comm.topology(), list(comm.selftest_failed))
         comm.close()
