@@ -126,7 +126,9 @@ def lib():
             except Exception:
                 pass
             path = _build.LIB_PATH
-            if _build.needs_build() and os.environ.get("FLEXAR_NO_BUILD") != "1":
+            if os.environ.get("FLEXAR_LIB_PATH"):  # A/B experiments: another build of the library
+                path = os.environ["FLEXAR_LIB_PATH"]
+            elif _build.needs_build() and os.environ.get("FLEXAR_NO_BUILD") != "1":
                 path = _build.build()
             if not os.path.exists(path):
                 raise FlexarError(5, f"native library missing: {path} (run __graft_entry__.build())")

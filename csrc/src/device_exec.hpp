@@ -186,7 +186,10 @@ __device__ FX_INLINE void xfer_k(const char* const (&s)[kMaxSrc], char* const (&
                                  float scale, bool vec) {
   using A = typename Elem<T>::acc;
   constexpr int E = 16 / sizeof(T);
-  constexpr int U = (K <= 2) ? 4 : ((K <= 4) ? 2 : 1);  // 16-B loads in flight per lane ~ 4..8
+#ifndef FLEXAR_UNROLL_WIDE
+#define FLEXAR_UNROLL_WIDE 1
+#endif
+  constexpr int U = (K <= 2) ? 4 : ((K <= 4) ? 2 : FLEXAR_UNROLL_WIDE);  // 16-B loads in flight per lane
   constexpr bool WT = PM == PM_WT;
   constexpr bool NTS = PM == PM_FENCE_NTS;
   const bool sc = Elem<T>::is_float && scale != 1.0f;
