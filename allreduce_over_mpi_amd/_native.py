@@ -103,6 +103,7 @@ def _sig(lib):
         "flexar_reg_count": (i, [vp]),
         "flexar_reg_find": (i, [vp, vp, sz]),
         "flexar_reg_ids": (i, [vp, c.POINTER(i), i]),
+        "flexar_zc_decide": (i, [cp, i, d, i, u32, c.POINTER(i), cp, sz]),
         "flexar_model_features": (i, [cp, i, d, i, c.POINTER(d)]),
         "flexar_kernel_info": (i, [i, i, i, i, c.POINTER(i), c.POINTER(i)]),
         "flexar_downgrade_spec": (i, [cp, i, u32, i, cp, sz]),
@@ -233,6 +234,19 @@ def model_features(spec: str, nranks: int, nbytes: float, links: int = 0):
         return None
     check(rc, "model_features")
     return list(out)
+
+
+def zc_decide(spec: str, nranks: int, nbytes: float, registered=True, named=False, auto=True, zc_auto=True,
+              have_tune=False, disabled: int = 0):
+    """The zero-copy policy on a concrete spec: (decision, spec) with decision 1 = switched to zero copy,
+    -1 = fell back to staging, 0 = unchanged (csrc/include/flexar/zc_policy.hpp)."""
+    flags = (1 if registered else 0) | (2 if named else 0) | (4 if auto else 0) | (8 if zc_auto else 0) | \
+            (16 if have_tune else 0)
+    dec = ctypes.c_int(0)
+    b = _strbuf(256)
+    check(lib().flexar_zc_decide(spec.encode(), nranks, float(nbytes), flags, disabled, ctypes.byref(dec), b, 256),
+          "zc_decide")
+    return dec.value, b.value.decode()
 
 
 def select_plan(nranks: int, nbytes: float) -> str:

@@ -177,6 +177,11 @@ int flexar_reg_ids(flexar_comm_t comm, int* ids_out, int max); /* current regist
 /* Registration holding [ptr, ptr + bytes): its id, 0 if none, -1 if its allocation was freed and the address
  * reused (stale peer mappings). A new registration replaces the old ones it contains or that are stale. */
 int flexar_reg_find(flexar_comm_t comm, const void* ptr, size_t bytes);
+/* The zero-copy policy (zc_policy.hpp) applied to a concrete spec, for tests and tools: writes the spec a call
+ * runs and sets *decision (1 switched to "+zc+push", -1 fell back to staging, 0 unchanged). flags: 1 buffers
+ * registered, 2 the call named the spec, 4 automatic choice, 8 FLEXAR_ZC_AUTO, 16 a tune table is installed. */
+int flexar_zc_decide(const char* spec, int nranks, double bytes, int flags, uint32_t disabled, int* decision,
+                     char* out, size_t outlen);
 /* JSON: per-peer PCI bus id, device ordinal, link class (same-device / xgmi / pcie / unknown) and hop
  * count from the connect-time probe; links used by the cost model; self-test state. */
 int flexar_comm_topology(flexar_comm_t comm, char* buf, size_t buflen);

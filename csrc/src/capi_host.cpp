@@ -18,6 +18,7 @@
 #include "flexar/msg_plan.hpp"
 #include "flexar/planner.hpp"
 #include "flexar/readiness.hpp"
+#include "flexar/zc_policy.hpp"
 #include "internal.hpp"
 
 namespace flexar {
@@ -439,6 +440,31 @@ int flexar_downgrade_spec(const char* spec, int nranks, uint32_t disabled, int a
   if (nranks < 1 || !parse_algo(spec ? spec : "auto", nranks, &s, &err)) { set_error(err.empty() ? "bad arguments" : err); return FLEXAR_ERR_INVALID; }
   if (s.kind == AlgoKind::AUTO) { set_error("downgrade needs a concrete spec"); return FLEXAR_ERR_INVALID; }
   if (!downgrade_spec(&s, nranks, disabled, allow_dma != 0, &err)) { set_error(err); return FLEXAR_ERR_UNSUPPORTED; }
+  return copy_out(s.str(), out, outlen);
+}
+
+// Zero-copy policy (zc_policy.hpp) on a resolved spec: the spec a call runs and the decision (1 = switched
+// to zero copy, -1 = fell back to staging, 0 = unchanged) in *decision. flags: 1 registered, 2 named,
+// 4 from_auto, 8 zc_auto, 16 have_tune. Default cost model (FLEXAR_MODEL applies).
+int flexar_zc_decide(const char* spec, int nranks, double bytes, int flags, uint32_t disabled, int* decision,
+                     char* out, size_t outlen) {
+  AlgoSpec s;
+  std::string err;
+  if (nranks < 1 || !decision || !parse_algo(spec ? spec : "", nranks, &s, &err) || s.kind == AlgoKind::AUTO) {
+    set_error(err.empty() ? "zc_decide needs a concrete spec" : err);
+    return FLEXAR_ERR_INVALID;
+  }
+  if (s.kind == AlgoKind::TREE && s.ag == AgMode::AUTO) s.ag = AgMode::PULL;
+  ZcFacts f;
+  f.nranks = nranks;
+  f.bytes = bytes;
+  f.registered = flags & 1;
+  f.named = flags & 2;
+  f.from_auto = flags & 4;
+  f.zc_auto = flags & 8;
+  f.have_tune = flags & 16;
+  f.disabled = disabled;
+  *decision = zc_decide(&s, f, XgmiModel::from_env());
   return copy_out(s.str(), out, outlen);
 }
 

@@ -32,6 +32,7 @@
 #include "flexar/flexar.h"
 #include "flexar/log.hpp"
 #include "flexar/msg_plan.hpp"
+#include "flexar/zc_policy.hpp"
 #include "flexar/planner.hpp"
 #include "flexar/readiness.hpp"
 #include "flexar/timer.hpp"
@@ -1791,36 +1792,20 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     if ((rc = executor_proto(c, &s))) return rc;
   }
   if (s.msg) s.wire = 0;  // the message transport runs the schedule untyped
-  // Registered buffers (flexar_reg_*): a flat schedule the call did not name explicitly - the cost model's
-  // or the tune table's choice - runs zero copy ("+zc+push": no staging), and a zero-copy choice from a
-  // tune table falls back to the staging schedule for buffers that are not registered. Registration is
-  // collective, so every rank decides alike. An explicit "+zc" on unregistered buffers stays an error.
+  // Registered buffers (flexar_reg_*): zero copy or staging for this call (zc_policy.hpp)
   if (!c->regs.empty() || s.zc) {
-    const bool named = algo && *algo && strcmp(algo, "auto") != 0;
-    const bool from_auto = !named && c->spec.kind == AlgoKind::AUTO;
-    const bool flat = s.kind == AlgoKind::TREE && s.widths.size() == 1 && !s.msg && s.wire == 0 && c->nranks > 1;
-    const bool reg = c->nranks > 1 && !s.msg && s.wire == 0 && zc_registered(c, in, out, (uint64_t)count * es);
-    if (reg && !s.zc && from_auto && c->zc_auto && s.kind != AlgoKind::DMA) {
-      // the flat schedule always gains; another model choice (oneshot, LL, ring, trees) only when the cost
-      // model prices the zero-copy push form lower (a tune table's measured choice is kept)
-      AlgoSpec z;
-      z.kind = AlgoKind::TREE;
-      z.widths = {c->nranks};
-      z.ag = AgMode::PUSH;
-      z.zc = true;
-      z.wt = s.wt;
-      z.nts = s.nts;
-      const double bytes = (double)count * es;
-      if (c->disabled & proto_family(z)) {
-        // the zero-copy form's protocol family failed the connect-time self-test: keep the verified choice
-      } else if (flat || (!c->have_tune && c->model.cost_us(z, c->nranks, bytes) < c->model.cost_us(s, c->nranks, bytes))) {
-        s = z;
-        hit = hit && m.s.zc;
-      }
-    } else if (flat && s.zc && !reg && !named) {
-      s.zc = false;
-      hit = hit && !m.s.zc;
-    }
+    ZcFacts f;
+    f.nranks = c->nranks;
+    f.bytes = (double)count * es;
+    f.named = algo && *algo && strcmp(algo, "auto") != 0;
+    f.from_auto = !f.named && c->spec.kind == AlgoKind::AUTO;
+    f.zc_auto = c->zc_auto;
+    f.have_tune = c->have_tune;
+    f.disabled = c->disabled;
+    f.registered = !s.msg && s.wire == 0 && zc_registered(c, in, out, (uint64_t)count * es);
+    const int d = zc_decide(&s, f, c->model);
+    if (d > 0) hit = hit && m.s.zc;
+    if (d < 0) hit = hit && !m.s.zc;
   }
   auto remember = [&](uint64_t piece, DevProgram* dp, int grid) {
     if (hit) return;

@@ -84,3 +84,32 @@ def test_zero_copy_collectives_refuse_ring():
     ins = [np.zeros(4 * 64, np.int32) for _ in range(4)]
     with pytest.raises(nv.FlexarError):
         nv.simulate_coll("reduce_scatter", "ring+zc", ins, 64, dtype="int32")
+
+
+def test_zero_copy_policy():
+    """The automatic zero-copy switch (csrc/include/flexar/zc_policy.hpp, applied by comm.hip per call)."""
+    big, small = float(1 << 28), 8192.0
+    # registered buffers, automatic choice: the flat schedule always switches, keeping its protocol
+    assert nv.zc_decide("flat+pull", 8, big) == (1, "tree:8+push+zc")
+    assert nv.zc_decide("flat+pull+wt", 8, big) == (1, "tree:8+push+wt+zc")
+    # another model choice only when the model prices the push form lower: large oneshot yes, small LL no
+    assert nv.zc_decide("oneshot", 2, big)[0] == 1
+    assert nv.zc_decide("ll", 8, small) == (0, "ll")
+    # a tune table's measured non-flat choice is kept; its flat choice still switches
+    assert nv.zc_decide("ring", 8, big, have_tune=True) == (0, "ring")
+    assert nv.zc_decide("flat+pull", 8, big, have_tune=True)[0] == 1
+    # never: unregistered, a named spec, FLEXAR_ZC_AUTO=0, one rank, copy engines, typed / message transport
+    assert nv.zc_decide("flat+pull", 8, big, registered=False)[0] == 0
+    assert nv.zc_decide("flat+pull", 8, big, named=True, auto=False)[0] == 0
+    assert nv.zc_decide("flat+pull", 8, big, zc_auto=False)[0] == 0
+    assert nv.zc_decide("flat+pull", 1, big)[0] == 0
+    assert nv.zc_decide("dma", 8, big)[0] == 0
+    assert nv.zc_decide("flat+rccl", 8, big)[0] == 0
+    # a protocol family that failed the connect-time self-test is never picked by the switch
+    fence = nv.FAMILIES["fence"]
+    assert nv.zc_decide("flat+pull", 8, big, disabled=fence)[0] == 0
+    assert nv.zc_decide("flat+pull+wt", 8, big, disabled=fence)[0] == 1
+    # a zero-copy choice nobody named (tune table, default spec) falls back for unregistered buffers; a named
+    # one stays (and is refused at the call with an error)
+    assert nv.zc_decide("flat+zc+push", 8, big, registered=False, auto=False) == (-1, "tree:8+push")
+    assert nv.zc_decide("flat+zc+push", 8, big, registered=False, named=True, auto=False) == (0, "tree:8+push+zc")
