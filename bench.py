@@ -105,10 +105,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if os.environ.get("FLEXAR_BENCH_TRACEBACK_S"):  # debugging aid: every rank's Python stacks, periodically
+    # every rank's Python stacks on stderr if the run is still going after this long (the bench takes about a
+    # minute; a stuck collective then names itself in the log); FLEXAR_BENCH_TRACEBACK_S=0 disables it
+    tb_s = int(os.environ.get("FLEXAR_BENCH_TRACEBACK_S", "600" if world > 1 else "0"))
+    if tb_s > 0:
         import faulthandler
 
-        faulthandler.dump_traceback_later(int(os.environ["FLEXAR_BENCH_TRACEBACK_S"]), repeat=True)
+        faulthandler.dump_traceback_later(tb_s, repeat=True)
 
     import torch
     import torch.distributed as dist
