@@ -117,18 +117,28 @@ def main():
     import torch.distributed as dist
 
     # FLEXAR_BENCH_SHARED_GPU=1: rehearsal of the multi-rank flow with every rank on device 0 (a 1-GPU
-    # box). RCCL refuses two ranks on one GPU, so the reference result and barriers use gloo and the RCCL
-    # comparison is skipped; the numbers measure one shared HBM, not xGMI.
+    # box). By default the reference result and barriers use gloo and the RCCL comparison is skipped; the
+    # numbers measure one shared HBM, not xGMI.
     shared = os.environ.get("FLEXAR_BENCH_SHARED_GPU", "0") == "1"
+    # FLEXAR_BENCH_SHARED_RCCL=1 (with SHARED_GPU): the driver's own flow on one GPU - "nccl" process group,
+    # RCCL reference and comparator, the '+rccl' message-transport candidates. RCCL refuses two ranks on one
+    # GPU of one host, so every rank gets its own NCCL_HOSTID: RCCL then treats the ranks as separate hosts
+    # and carries their messages over its socket transport on loopback (RCCL numbers are not xGMI figures).
+    shared_rccl = shared and world > 1 and os.environ.get("FLEXAR_BENCH_SHARED_RCCL", "0") == "1"
+    host_ref = shared and not shared_rccl  # gloo process group: references and reductions on the host
+    if shared_rccl:
+        os.environ["NCCL_HOSTID"] = f"flexar-bench-rank{rank}"  # must differ per rank
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
     if shared:
         local = 0
-        args.no_rccl = True
+        args.no_rccl = args.no_rccl or not shared_rccl
         # every rank's workgroups must be co-resident on the one GPU (they spin on each other)
         os.environ.setdefault("FLEXAR_MAX_GRID", str(max(8, 256 // (2 * world))))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        if shared:
+        if host_ref:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
@@ -153,7 +163,7 @@ def main():
 
     # one rank per GPU: IPC plus the RCCL message transport, so the tuner also measures the FlexTree / ring /
     # RHD schedules over ncclSend/ncclRecv ("+rccl"); if RCCL cannot be set up, IPC alone
-    transports = ["ipc"] if (world == 1 or shared) else [args.transport, "ipc"] if args.transport != "ipc" else ["ipc"]
+    transports = ["ipc"] if (world == 1 or host_ref) else [args.transport, "ipc"] if args.transport != "ipc" else ["ipc"]
 
     def make_comm():
         err = None
@@ -208,18 +218,18 @@ def main():
     def max_over_ranks(v: float) -> float:
         if world == 1:
             return v
-        t = torch.tensor([v], device="cpu" if shared else dev, dtype=torch.float64)
+        t = torch.tensor([v], device="cpu" if host_ref else dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
     # ---------------------------------------------------------------- correctness vs RCCL
     op = args.op
-    if dtype == torch.float8_e4m3fn and not shared:  # RCCL reference computed in fp32 from the same fp8 inputs
+    if dtype == torch.float8_e4m3fn and not host_ref:  # RCCL reference computed in fp32 from the same fp8 inputs
         ref = x.float()
         if world > 1:
             dist.all_reduce(ref)
         ref = (ref / world if op == "avg" else ref).to(dtype)
-    elif shared:  # gloo: reference on the host
+    elif host_ref:  # gloo: reference on the host
         ref = x.float().cpu()
         if world > 1:
             dist.all_reduce(ref)
@@ -447,7 +457,7 @@ def main():
             return round(max_over_ranks(time.perf_counter() - t2) / iters * 1e6, 2)
 
         small = {"flexar": per_call(lambda: comm.all_reduce(xs, out=ys))}
-        if not args.no_rccl and not shared:
+        if not args.no_rccl and not host_ref:
             small["rccl"] = per_call(lambda: dist.all_reduce(xs))
 
     algbw = algbw_gbps(nbytes, t_step)
@@ -471,7 +481,9 @@ def main():
         "vs_baseline": round(busbw / BASELINE_BUSBW_256MIB, 2) if (world > 1 and args.size_mb == 256.0) else None,
         "dtype": {"float32": "fp32", "bfloat16": "bf16", "float16": "fp16", "float8_e4m3fn": "fp8_e4m3"}[args.dtype],
         "data": "synthetic (torch.randn per rank, seeded); results checked against RCCL before and after timing"
-                + ("; REHEARSAL: all ranks share one GPU (gloo reference), not an xGMI measurement" if shared else ""),
+                + ("; REHEARSAL: all ranks share one GPU ("
+                   + ("RCCL over loopback sockets" if shared_rccl else "gloo reference")
+                   + "), not an xGMI measurement" if shared else ""),
         "config": {
             "model": f"allreduce {args.dtype} {args.size_mb:g}MiB buffer per rank"
                      + (" (BASELINE config #2)" if args.dtype == "float32" and args.size_mb == 256 else ""),

@@ -1,8 +1,9 @@
 """Message transport on the GPU box: RCCL is resolved at run time (dlopen of the process's librccl) and the
 device side of a message plan (local executor segments, arena, grouped ncclSend/ncclRecv) runs. A 1-GPU
-box allows one RCCL rank per GPU, so the multi-rank transport runs in tests/test_gpu_multidevice.py (2+
-GPUs: "+rccl" specs and the IPC-unavailable fallback); the message plans themselves are validated on the
-CPU (tests/test_msg_plan.py)."""
+box allows one RCCL rank per GPU and host, so the multi-rank transport runs in
+tests/test_gpu_msg_shared.py (ranks on one GPU posing as separate hosts through NCCL_HOSTID) and
+tests/test_gpu_multidevice.py (2+ GPUs); the message plans themselves are validated on the CPU
+(tests/test_msg_plan.py)."""
 import pytest
 import torch
 
