@@ -1,7 +1,12 @@
 """The "flexar" c10d backend + DDP on a real MI355X: two training processes on
 one GPU (IPC between processes on one device), gradient allreduce through the
 flexar executor kernel, compared against full-batch single-process training of
-the same model. Also the DDP comm-hook path over a gloo process group."""
+the same model. Also the DDP comm-hook path over a gloo process group.
+
+The backend's default fallback group is RCCL (FLEXAR_PG_FALLBACK=nccl), which refuses two ranks on one GPU
+of one host; the "+nccl" cases give every process its own NCCL_HOSTID so RCCL treats the ranks as separate
+hosts (loopback sockets) and the production defaults run: RCCL fallback group, ProcessGroupNCCL cross-node
+group of the hierarchical communicator, and DDP on the plain "nccl" backend as the reference trajectory."""
 import os
 import socket
 
@@ -19,10 +24,20 @@ def _port():
     return p
 
 
-def _train(rank, world, port, mode, q, model_kind="mlp"):
+def _fallback_env(rank, fallback):
+    """gloo fallback group, or RCCL's (the default) with one NCCL_HOSTID per rank on the shared GPU."""
+    if fallback == "gloo":
+        os.environ["FLEXAR_PG_FALLBACK"] = "gloo"
+    else:
+        os.environ.pop("FLEXAR_PG_FALLBACK", None)
+        os.environ.update(NCCL_HOSTID=f"flexar-test-rank{rank}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+
+
+def _train(rank, world, port, q, mode, model_kind="mlp", fallback="gloo"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
-                          FLEXAR_PG_FALLBACK="gloo", FLEXAR_TIMEOUT_MS="20000")
+                          FLEXAR_TIMEOUT_MS="20000")
+        _fallback_env(rank, fallback)
         import torch.distributed as dist
         import torch.nn as nn
         from torch.nn.parallel import DistributedDataParallel as DDP
@@ -32,7 +47,11 @@ def _train(rank, world, port, mode, q, model_kind="mlp"):
 
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
-        dist.init_process_group("flexar" if mode == "backend" else "gloo", rank=rank, world_size=world)
+        pg_kind = {"backend": "flexar", "nccl": "nccl"}.get(mode, "gloo")
+        if pg_kind == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group(pg_kind, rank=rank, world_size=world)
         from allreduce_over_mpi_amd.models.gpt import GPT, PRESETS
 
         torch.manual_seed(0)
@@ -73,32 +92,50 @@ def _train(rank, world, port, mode, q, model_kind="mlp"):
         torch.cuda.synchronize()
         err = max((a - b).abs().max().item() for a, b in zip(model.parameters(), ref.parameters()))
         pg = dist.group.WORLD
-        used = getattr(pg, "stats", {}).get("flexar_allreduce", 0) if mode == "backend" else state.calls
+        used = (getattr(pg, "stats", {}).get("flexar_allreduce", 0) if mode == "backend" else
+                1 if mode == "nccl" else state.calls)
         if mode == "zchook" and not state._bucket_regs:
             used = 0  # the zero-copy path must actually have registered the buckets
         dist.destroy_process_group()
-        q.put((rank, err, used, None))
+        # numpy arrays travel by value (a torch CPU tensor would be shared through a descriptor of this exiting process)
+        q.put((rank, err, used, None, [p.detach().cpu().numpy() for p in model.parameters()]))
     except Exception:
         import traceback
 
-        q.put((rank, None, None, traceback.format_exc()))
+        q.put((rank, None, None, traceback.format_exc(), None))
 
 
-@pytest.mark.parametrize("mode,model_kind", [("backend", "mlp"), ("hook", "mlp"), ("backend", "gpt"), ("hook", "gpt"),
-                                             ("fp8hook", "mlp"), ("zchook", "mlp"), ("zchook", "gpt")])
-def test_ddp_over_flexar(cuda, mode, model_kind):
+def _spawn(target, world, *args, timeout=300):
+    """Run ``target(rank, world, port, q, *args)`` in ``world`` spawned processes; the results by rank.
+    A rank that hangs is killed (it must not outlive the test on the GPU)."""
+    import queue
+
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_train, args=(r, 2, port, mode, q, model_kind)) for r in range(2)]
+    ps = [ctx.Process(target=target, args=(r, world, port, q, *args)) for r in range(world)]
     for p in ps:
         p.start()
-    res = [q.get(timeout=300) for _ in range(2)]
-    for p in ps:
-        p.join(60)
-    for rank, err, used, tb in res:
+    try:
+        res = [q.get(timeout=timeout) for _ in range(world)]
+    except queue.Empty:
+        pytest.fail(f"{target.__name__}: a rank did not finish within {timeout} s")
+    finally:
+        for p in ps:
+            p.join(60)
+            if p.is_alive():
+                p.kill()
+    return res
+
+
+@pytest.mark.parametrize("mode,model_kind,fallback", [
+    ("backend", "mlp", "gloo"), ("hook", "mlp", "gloo"), ("backend", "gpt", "gloo"), ("hook", "gpt", "gloo"),
+    ("fp8hook", "mlp", "gloo"), ("zchook", "mlp", "gloo"), ("zchook", "gpt", "gloo"), ("backend", "gpt", "nccl")])
+def test_ddp_over_flexar(cuda, mode, model_kind, fallback):
+    res = _spawn(_train, 2, mode, model_kind, fallback)
+    for rank, err, used, tb, _ in res:
         assert tb is None, tb
         assert used and used > 0, "flexar path was not used"
         # fp8 on the wire: e4m3's 2^-4 relative step of each bucket's largest gradient, over 4 SGD steps
@@ -106,10 +143,23 @@ def test_ddp_over_flexar(cuda, mode, model_kind):
         assert err < tol, (mode, model_kind, rank, err)
 
 
-def _colls(rank, world, port, q):
+def test_ddp_flexar_backend_matches_rccl_ddp(cuda):
+    """SURVEY.md section 7.4's criterion: DDP on the "flexar" backend (default RCCL fallback group) follows the
+    same trajectory as DDP on the plain "nccl" backend. Two ranks: every gradient element is a sum of two
+    addends, the same in any order, so the parameters agree exactly."""
+    ours = {r: params for r, _, _, tb, params in _spawn(_train, 2, "backend", "gpt", "nccl") if tb is None}
+    rccl = {r: params for r, _, _, tb, params in _spawn(_train, 2, "nccl", "gpt", "nccl") if tb is None}
+    assert len(ours) == 2 and len(rccl) == 2
+    for r in range(2):
+        for a, b in zip(ours[r], rccl[r]):
+            assert (a == b).all(), (r, abs(a - b).max())
+
+
+def _colls(rank, world, port, q, fallback="gloo"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
-                          FLEXAR_PG_FALLBACK="gloo", FLEXAR_TIMEOUT_MS="20000")
+                          FLEXAR_TIMEOUT_MS="20000")
+        _fallback_env(rank, fallback)
         import torch.distributed as dist
 
         from allreduce_over_mpi_amd.parallel import backend as fb  # noqa: F401
@@ -158,28 +208,28 @@ def _colls(rank, world, port, q):
         dist.broadcast(bc, src=1)
         e8 = (bc - torch.arange(100003, device=dev).float() * 2).abs().max().item()
         torch.cuda.synchronize()
+        e10 = 0.0
+        if fallback == "nccl":  # point-to-point (pipeline stages) has no flexar program: RCCL by default
+            pp = torch.full((4099,), float(rank + 1), device=dev)
+            if rank == 0:
+                dist.send(pp, dst=1)
+            elif rank == 1:
+                dist.recv(pp, src=0)
+            e10 = (pp - (1.0 if rank <= 1 else rank + 1.0)).abs().max().item()
+            e10 = e10 if dist.group.WORLD.stats["fallback"] > 0 else 1.0
+        dist.barrier()
         used = dist.group.WORLD.stats["flexar_allreduce"]
         dist.destroy_process_group()
-        q.put((rank, max(e1, e2, e3, e4, e5, e6, e7, e8, e9), used, None))
+        q.put((rank, max(e1, e2, e3, e4, e5, e6, e7, e8, e9, e10), used, None))
     except Exception:
         import traceback
 
         q.put((rank, None, None, traceback.format_exc()))
 
 
-def test_backend_reduce_scatter_all_gather(cuda):
-    import torch.multiprocessing as mp
-
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _port()
-    ps = [ctx.Process(target=_colls, args=(r, 2, port, q)) for r in range(2)]
-    for p in ps:
-        p.start()
-    res = [q.get(timeout=300) for _ in range(2)]
-    for p in ps:
-        p.join(60)
-    for rank, err, used, tb in res:
+@pytest.mark.parametrize("fallback", ["gloo", "nccl"])
+def test_backend_reduce_scatter_all_gather(cuda, fallback):
+    for rank, err, used, tb in _spawn(_colls, 2, fallback):
         assert tb is None, tb
         assert err == 0.0 and used >= 9, (rank, err, used)
 
@@ -217,10 +267,11 @@ print("rccl routing ok")
     assert r.returncode == 0 and "rccl routing ok" in r.stdout, r.stdout + r.stderr
 
 
-def _hier_backend(rank, world, port, q):
+def _hier_backend(rank, world, port, q, fallback="gloo"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
-                          FLEXAR_PG_FALLBACK="gloo", FLEXAR_TIMEOUT_MS="20000", FLEXAR_NODE_SIZE="2")
+                          FLEXAR_TIMEOUT_MS="20000", FLEXAR_NODE_SIZE="2")
+        _fallback_env(rank, fallback)
         import torch.distributed as dist
 
         from allreduce_over_mpi_amd.parallel import backend as fb  # noqa: F401
@@ -250,21 +301,12 @@ def _hier_backend(rank, world, port, q):
         q.put((rank, None, None, traceback.format_exc()))
 
 
-def test_backend_hierarchical_virtual_nodes(cuda):
+@pytest.mark.parametrize("fallback", ["gloo", "nccl"])
+def test_backend_hierarchical_virtual_nodes(cuda, fallback):
     """init_process_group("flexar") over 2 virtual nodes x 2 ranks: dist.all_reduce runs intra-node flexar
-    reduce-scatter / all-gather around a cross-node allreduce of the shards."""
-    import torch.multiprocessing as mp
-
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _port()
-    ps = [ctx.Process(target=_hier_backend, args=(r, 4, port, q)) for r in range(4)]
-    for p in ps:
-        p.start()
-    res = [q.get(timeout=300) for _ in range(4)]
-    for p in ps:
-        p.join(60)
-    for rank, err, ok, tb in res:
+    reduce-scatter / all-gather around a cross-node allreduce of the shards ("nccl": the production
+    ProcessGroupNCCL cross-node group, one NCCL_HOSTID per rank)."""
+    for rank, err, ok, tb in _spawn(_hier_backend, 4, fallback):
         assert tb is None, tb
         assert err == 0.0 and ok, (rank, err, ok)
 
