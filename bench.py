@@ -318,8 +318,9 @@ def main():
         cands = default_candidates(world, nbytes)
         if comm.topology().get("rccl"):  # the schedules over RCCL send/recv as well
             cands += ["flat+rccl", "ring+rccl"] + (["rhd+rccl"] if world > 2 and not world & (world - 1) else [])
-        if zc:  # registered buffers: the flat schedule straight from / to the peers' x and y
-            cands += ["flat+zc", "flat+zc+nts", "flat+zc+wt", "flat+zc+push", "flat+zc+push+nts", "flat+zc+push+wt"]
+        if zc:  # registered buffers: the flat schedule straight from / to the peers' x and y (put: remote writes only)
+            cands += ["flat+zc", "flat+zc+nts", "flat+zc+wt", "flat+zc+push", "flat+zc+push+nts", "flat+zc+push+wt",
+                      "flat+zc+put", "flat+zc+put+nts", "flat+zc+put+wt"]
         timings = {}
         for spec in cands:
             failed = 0.0

@@ -3,7 +3,8 @@
 staging flat schedules, N ranks in one launch on one GPU (LocalGroup: every rank's buffers are plain
 device pointers, so no registration is needed). One JSON line per (ranks, spec): kernel time per call,
 busbw and the HBM bytes per rank the schedule moves (model: staging flat pull = 2(N-1)/N S + (N+2)/N S +
-2(N-1)/N S; zero copy = (N+1)/N S + 2(N-1)/N S), so the time ratio can be read against the byte ratio.
+2(N-1)/N S; zero copy = (N+1)/N S + 2(N-1)/N S; push 2 S; put 2 S + 2(N-1)/N S through the owners'
+staging), so the time ratio can be read against the byte ratio.
 
     python bench/zc_bench.py                      # N = 2, 4, 8 at 64 MiB fp32 per rank
     ZCB_MIB=256 ZCB_RANKS=2 python bench/zc_bench.py
@@ -23,7 +24,8 @@ def main():
 
     mib = int(os.environ.get("ZCB_MIB", "64"))
     ranks = [int(v) for v in os.environ.get("ZCB_RANKS", "2,4,8").split(",")]
-    specs = os.environ.get("ZCB_SPECS", "flat+pull,flat+pull+nts,flat+zc,flat+zc+nts,flat+zc+wt,flat+zc+push,flat+zc+push+wt").split(",")
+    specs = os.environ.get("ZCB_SPECS", "flat+pull,flat+pull+nts,flat+zc,flat+zc+nts,flat+zc+wt,flat+zc+push,flat+zc+push+wt,"
+                           "flat+zc+put,flat+zc+put+nts").split(",")
     count = (mib << 20) // 4
     for n in ranks:
         grp = LocalGroup(n, workspace_bytes=(4 * mib + 64) << 20)
@@ -44,7 +46,8 @@ def main():
             torch.cuda.synchronize()
             ms = a.elapsed_time(b) / iters
             S = count * 4
-            hbm = (S * (1 + 1) if "zc+push" in spec else S * ((n + 1) / n + 2 * (n - 1) / n) if "zc" in spec
+            hbm = (S * (1 + 1) if "zc+push" in spec else S * (2 + 2 * (n - 1) / n) if "zc+put" in spec
+                   else S * ((n + 1) / n + 2 * (n - 1) / n) if "zc" in spec
                    else S * (2 * (n - 1) / n + (n + 2) / n + 2 * (n - 1) / n))
             print(json.dumps({"ranks": n, "MiB_fp32": mib, "spec": spec, "ms": round(ms, 4),
                               "busbw_GBps": round(S / (ms * 1e-3) * 2 * (n - 1) / n / 1e9, 1),

@@ -101,7 +101,9 @@ struct XgmiModel {
           f[3] += 2.0 * w * per_peer / 1e3;
         }
         if (s.zc) {  // registered buffers (flat only), no staging writes / reads: pull = a third hand-off
-          if (s.ag == AgMode::PUSH) {  // and 3/5 of the staging schedule's HBM bytes (profiles/r2_zc);
+          if (s.put) {  // put: the contributions land in the owners' staging and are read back once
+            f[3] *= 0.7;
+          } else if (s.ag == AgMode::PUSH) {  // and 3/5 of the staging schedule's HBM bytes (profiles/r2_zc);
             f[3] *= 0.4;               // push = each input byte read once, each result byte written once
           } else {
             f[1] += 1.0;

@@ -89,7 +89,8 @@ class Planner {
         if (err) *err = "zero-copy (+zc) runs the flat schedule over IPC-registered buffers (no wire type, no +rccl)";
         return false;
       }
-      build_flat_zc(spec.ag == AgMode::PUSH);
+      if (spec.put) build_flat_zc_put();
+      else build_flat_zc(spec.ag == AgMode::PUSH);
       P->zc = true;
       P->desc = spec.str();
     } else if (wire >= 2 && !(spec.kind == AlgoKind::TREE && spec.widths.size() == 1 && spec.widths[0] == (int)N)) {
@@ -733,6 +734,38 @@ class Planner {
       signal(peers, 2);
       wait(peers, 2);
     }
+    finish_channel();
+  }
+
+  // Zero-copy put form ("+zc+put"): only remote WRITES cross the links (no remote load waits on a round
+  // trip). Every rank writes its IN block p into slot r of owner p's staging (the reduce-scatter, like the
+  // staging flat push), then each owner sums its block in rank order - its own IN and the N - 1 landed slots
+  // - straight into its own OUT and every peer's registered OUT (the all-gather). Two hand-offs: slot 0 "my
+  // contributions are in your staging and I have entered the call" (so my OUT may be written), slot 1 "I
+  // have written your block" (no rank leaves the call before its OUT is complete). Only OUT is addressed on
+  // peers. In place is safe: a rank's IN block p is read by that rank (the push to p) before its slot-0
+  // signal, and p writes that block of its OUT only after waiting for that signal - per workgroup, over the
+  // same slice. Same rank-order sum as "+zc", so all forms give identical bits.
+  void build_flat_zc_put() {
+    const uint64_t split = round_up((count + N - 1) / N);
+    auto boff = [&](uint32_t k) { return (uint64_t)k * split; };
+    auto blen = [&](uint32_t k) -> uint64_t {
+      const uint64_t s = boff(k);
+      return s >= count ? 0 : std::min(split, count - s);
+    };
+    const uint64_t land = alloc((uint64_t)N * split);  // slot j: rank j's contribution to my block
+    auto slot = [&](uint32_t j) { return land + (uint64_t)j * split; };
+    auto peers = rotated_peers();
+    for (uint32_t p : peers) xfer(blen(p), {loc(BUF_IN, r, boff(p))}, {loc(BUF_STG, p, slot(r))}, 1.0f);
+    signal(peers, 0);
+    wait(peers, 0);
+    std::vector<Loc> srcs;
+    for (uint32_t j = 0; j < N; ++j) srcs.push_back(j == r ? loc(BUF_IN, r, boff(r)) : loc(BUF_STG, r, slot(j)));
+    std::vector<Loc> dsts{loc(BUF_OUT, r, boff(r))};
+    for (uint32_t p : peers) dsts.push_back(loc(BUF_OUT, p, boff(r)));
+    xfer(blen(r), srcs, dsts, scale);
+    signal(peers, 1);
+    wait(peers, 1);
     finish_channel();
   }
 

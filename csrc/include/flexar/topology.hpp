@@ -51,6 +51,10 @@ struct AlgoSpec {
   // peer's OUTPUT directly over IPC (buffers registered with flexar_reg_*), no staging copies; a closing
   // hand-off keeps each rank in the call until its peers have finished reading its buffers
   bool zc = false;
+  // zero-copy put form ("+zc+put"): remote WRITES only - each rank writes its contributions into the
+  // owners' staging, and each owner writes the reduced block into every rank's registered OUT; only the
+  // outputs need registering (meaningless without zc: the staging schedules already write-push)
+  bool put = false;
 
   std::string str() const {
     std::ostringstream ss;
@@ -66,7 +70,7 @@ struct AlgoSpec {
         break;
     }
     if (kind == AlgoKind::TREE && ag == AgMode::PULL) ss << "+pull";
-    if (kind == AlgoKind::TREE && ag == AgMode::PUSH) ss << "+push";
+    if (kind == AlgoKind::TREE && ag == AgMode::PUSH && !(put && zc)) ss << "+push";
     if (!fuse) ss << "+nofuse";
     if (nts) ss << "+nts";
     if (wt) ss << "+wt";
@@ -76,6 +80,7 @@ struct AlgoSpec {
     if (round_wire) ss << "+rw";
     if (msg) ss << "+rccl";
     if (zc) ss << "+zc";
+    if (zc && put) ss << "+put";
     return ss.str();
   }
 };
@@ -205,6 +210,7 @@ inline bool parse_algo(const std::string& raw, int nranks, AlgoSpec* spec, std::
     else if (mod == "rw") spec->round_wire = true;
     else if (mod == "rccl" || mod == "msg") spec->msg = true;
     else if (mod == "zc") spec->zc = true;
+    else if (mod == "put") spec->put = true, spec->ag = AgMode::PUSH;
     else { if (err) *err = "unknown algorithm modifier '+" + mod + "'"; return false; }
   }
   std::string head = s, arg;
@@ -250,12 +256,13 @@ inline bool parse_algo(const std::string& raw, int nranks, AlgoSpec* spec, std::
   if (head == "ft") {
     const char* env = getenv("FT_TOPO");
     AgMode ag = spec->ag; bool fuse = spec->fuse, nts = spec->nts, wt = spec->wt, rw = spec->round_wire;
-    bool msg = spec->msg, zc = spec->zc;
+    bool msg = spec->msg, zc = spec->zc, put = spec->put;
     int wire = spec->wire;
     if (!parse_ft_topo(!arg.empty() ? arg.c_str() : env, nranks, spec, err)) return false;
     spec->ag = ag; spec->fuse = fuse; spec->nts = nts; spec->wt = wt; spec->wire = wire; spec->round_wire = rw;
     spec->msg = msg;
     spec->zc = zc;
+    spec->put = put;
     return true;
   }
   if (err) *err = "unknown algorithm '" + raw + "'";

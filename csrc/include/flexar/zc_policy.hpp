@@ -50,6 +50,7 @@ inline int zc_decide(AlgoSpec* s, const ZcFacts& f, const XgmiModel& m) {
   }
   if (flat && s->zc && !f.registered && !f.named) {
     s->zc = false;
+    s->put = false;
     return -1;
   }
   return 0;

@@ -392,7 +392,7 @@ def _stress_worker(rank, world, port, calls, q, fault=""):
         comm = Communicator(workspace_bytes=32 << 20)
         specs = ["flat", "flat+push", "flat+wt", "flat+push+nts", "ring", "ring+wt", "oneshot", "ll", "dma",
                  "rhd", "tree:2,2+push"] if world == 4 else ["flat", "flat+push+wt", "ring", "oneshot", "ll", "dma"]
-        specs += ["flat+zc", "flat+zc+push"]
+        specs += ["flat+zc", "flat+zc+push", "flat+zc+put"]
         # zero-copy calls run on registered arenas (the same offsets on every rank: the same call sequence)
         arena_in = torch.empty(world * 2_000_003 + 64, device="cuda")
         arena_out = torch.empty(world * 2_000_003 + 64, device="cuda")
@@ -585,7 +585,8 @@ def _zc_worker(rank, world, port, q):
         x, y = arena[:n], arena[n + 64:2 * n + 64]
         rx, ry = comm.register(x), comm.register(y)
         errs = {}
-        for spec in ("flat+zc", "flat+zc+wt", "flat+zc+nts", "flat+zc+push", "flat+zc+push+wt"):
+        for spec in ("flat+zc", "flat+zc+wt", "flat+zc+nts", "flat+zc+push", "flat+zc+push+wt", "flat+zc+put",
+                     "flat+zc+put+wt", "flat+zc+put+nts"):
             for size in (7, 4096, 300001, n):
                 for call in range(3):  # consecutive calls: a peer still reading the last call would show
                     src = torch.randn(size, generator=torch.Generator().manual_seed(1000 * rank + size + call))
@@ -604,6 +605,10 @@ def _zc_worker(rank, world, port, q):
         comm.all_reduce(x[100:100 + 5003], algo="flat+zc+push")
         torch.cuda.synchronize()
         errs["in_place_push"] = (x[100:100 + 5003] - world * (world + 1) / 2).abs().max().item()
+        x[100:100 + 5003].fill_(float(rank + 1))
+        comm.all_reduce(x[100:100 + 5003], algo="flat+zc+put")
+        torch.cuda.synchronize()
+        errs["in_place_put"] = (x[100:100 + 5003] - world * (world + 1) / 2).abs().max().item()
         # an unregistered buffer is refused, not read through a stale mapping
         try:
             comm.all_reduce(torch.ones(64, device=dev), algo="flat+zc")

@@ -70,7 +70,8 @@ def _specs(n):
     from allreduce_over_mpi_amd import _native as nv
 
     base = ["flat", "flat+push", "ring", "oneshot", "ll", "flat+nts", "ring:2+nts"]
-    base += ["flat+wt", "flat+push+wt", "ring+wt", "ring:2+wt", "oneshot+wt", "dma", "flat+zc", "flat+zc+wt", "flat+zc+push"]
+    base += ["flat+wt", "flat+push+wt", "ring+wt", "ring:2+wt", "oneshot+wt", "dma", "flat+zc", "flat+zc+wt", "flat+zc+push",
+             "flat+zc+put"]
     base += [p for p in nv.enumerate_plans(n) if p.startswith("tree:") or p.startswith("ring:")]
     base += [p + "+push" for p in nv.enumerate_plans(n) if p.startswith("tree:") and "," in p]
     return sorted(set(base))

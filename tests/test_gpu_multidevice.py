@@ -65,7 +65,7 @@ def _worker(rank, world, port, specs, q, transport="rccl", no_ipc=False):
                 arena = torch.empty(1000003, device=dev, dtype=dtype)
                 out = torch.empty_like(arena)
                 comm.register_many([arena, out])
-                for spec in ("flat+zc", "flat+zc+push", "flat+zc+push+wt"):
+                for spec in ("flat+zc", "flat+zc+push", "flat+zc+push+wt", "flat+zc+put", "flat+zc+put+nts"):
                     for size in (5, 4096, 1000003):
                         xs = [torch.randn(size, generator=torch.Generator().manual_seed(7 * r + size)).to(dtype)
                               for r in range(world)]

@@ -13,7 +13,8 @@ from allreduce_over_mpi_amd import _native as nv
 
 @pytest.mark.parametrize("n", [2, 3, 4, 7, 8, 12, 16])
 @pytest.mark.parametrize("count", [1, 35, 4099, 10007])
-@pytest.mark.parametrize("spec", ["flat+zc", "flat+zc+wt", "flat+zc+nts", "flat+zc+push", "flat+zc+push+wt"])
+@pytest.mark.parametrize("spec", ["flat+zc", "flat+zc+wt", "flat+zc+nts", "flat+zc+push", "flat+zc+push+wt",
+                                  "flat+zc+put", "flat+zc+put+wt"])
 def test_zero_copy_exact_sum(n, count, spec):
     ins = [np.random.default_rng(7 * r + count).integers(-99, 99, count).astype(np.int32) for r in range(n)]
     want = np.sum(ins, axis=0)
@@ -22,7 +23,7 @@ def test_zero_copy_exact_sum(n, count, spec):
 
 
 @pytest.mark.parametrize("n", [2, 4, 8, 11])
-@pytest.mark.parametrize("spec", ["flat+zc", "flat+zc+push"])
+@pytest.mark.parametrize("spec", ["flat+zc", "flat+zc+push", "flat+zc+put"])
 def test_zero_copy_in_place(n, spec):
     # IN == OUT: block k of a rank's IN is read only by its owner k, which overwrites it (push) or lets it
     # be overwritten (pull) only afterwards
@@ -39,6 +40,10 @@ def test_zero_copy_float_is_rank_order_deterministic():
     for o in outs[1:]:
         assert np.array_equal(o, outs[0])  # the owner of each block sums in rank order; others copy it
     np.testing.assert_allclose(outs[0], np.mean(np.stack(ins).astype(np.float64), axis=0), rtol=1e-5, atol=1e-5)
+    # every zero-copy form sums in the same rank order: identical bits
+    for spec in ("flat+zc+push", "flat+zc+put"):
+        for o in nv.simulate(spec, ins, grid=2, op="avg"):
+            assert np.array_equal(o, outs[0]), spec
 
 
 def test_zero_copy_program_shape():
@@ -49,11 +54,16 @@ def test_zero_copy_program_shape():
     # push: one reduction straight into every rank's OUT, two hand-offs
     d = nv.plan_dump("flat+zc+push", 1, 4, 4096, "float32")
     assert "2 flag slots" in d and d.count("XFER") == 1 and "STG" not in d
+    # put: remote writes only - three pushes into the owners' staging, one reduction into every OUT; no
+    # peer IN is addressed (only the outputs need registering)
+    d = nv.plan_dump("flat+zc+put", 1, 4, 4096, "float32")
+    assert "2 flag slots" in d and d.count("XFER") == 4, d
+    assert "OUT@0" in d and "OUT@2" in d and "IN@0" not in d and "IN@2" not in d, d
 
 
 def test_zero_copy_refused_outside_flat():
     ins = [np.zeros(64, np.int32) for _ in range(4)]
-    for spec in ("ring+zc", "rhd+zc", "tree:2,2+zc"):
+    for spec in ("ring+zc", "rhd+zc", "tree:2,2+zc", "tree:2,2+zc+put"):
         with pytest.raises(nv.FlexarError):
             nv.simulate(spec, ins)
 
@@ -113,3 +123,5 @@ def test_zero_copy_policy():
     # one stays (and is refused at the call with an error)
     assert nv.zc_decide("flat+zc+push", 8, big, registered=False, auto=False) == (-1, "tree:8+push")
     assert nv.zc_decide("flat+zc+push", 8, big, registered=False, named=True, auto=False) == (0, "tree:8+push+zc")
+    assert nv.zc_decide("flat+zc+put", 8, big, registered=False, auto=False) == (-1, "tree:8+push")
+    assert nv.zc_decide("flat+zc+put", 8, big, auto=False) == (0, "tree:8+zc+put")
