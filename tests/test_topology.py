@@ -151,3 +151,38 @@ def test_selection_table_matches_selector():
     rows = selection_table(8, [4096, 1 << 20, 256 << 20])
     assert [r[1] for r in rows] == [nv.select_plan(8, b) for b in (4096, 1 << 20, 256 << 20)]
     assert rows[0][2] < rows[1][2] < rows[2][2]
+
+
+def _ordered_factorizations(n):
+    if n == 1:
+        return [[]]
+    return [[d] + rest for d in range(2, n + 1) if n % d == 0 for rest in _ordered_factorizations(n // d)]
+
+
+@pytest.mark.parametrize("lo,hi", [(2, 16), (17, 32), (33, 48), (49, 64)])
+def test_every_ordered_factorization_up_to_64(nv, lo, hi):
+    """the plan generator's invariants for EVERY ordered factorization of every N <= 64 (the
+    reference's whole FT_TOPO space: H(N) trees per N, plus the ring). Every rank ends with the exact sum
+    (uneven tail blocks: count is not a multiple of N), and every rank's program moves the
+    bandwidth-optimal 2 (N - 1) / N of the buffer over the links. The widths come from an independent
+    enumeration and are checked against the native one (count = H(N))."""
+    import math
+
+    import numpy as np
+
+    for n in range(lo, hi + 1):
+        facts = _ordered_factorizations(n)
+        assert len(facts) == nv.count_factorizations(n), n
+        specs = ["tree:" + ",".join(map(str, f)) for f in facts] + ["ring"]
+        count = 7 * n + 3  # uneven: the last block is short
+        ins = [np.arange(count, dtype=np.int64) * (r + 1) + r for r in range(n)]
+        want = np.sum(ins, axis=0)
+        big = 4096 * n
+        for spec in specs:
+            for o in nv.simulate(spec, ins, ncalls=2):
+                assert np.array_equal(o, want), (spec, n)
+            if n <= 32 or spec.count(",") <= 1:  # the byte count over every rank's dump, sampled above 32
+                for r in (0, n - 1):
+                    got = _remote_elems(nv.plan_dump(spec, r, n, big), r)
+                    assert abs(got - 2 * (n - 1) * big / n) <= 0.01 * big, (spec, n, r, got)
+        assert math.prod(facts[0]) == n
