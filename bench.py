@@ -628,7 +628,9 @@ def parse_bytes(v: str) -> int:
 
 
 def run_sweep(args, comm, world, rank, dev, dtype, op, dist, max_over_ranks):
-    """busbw vs bytes, flexar (cost-model 'auto' choice) vs RCCL — BASELINE config #4."""
+    """busbw vs bytes, flexar (cost-model 'auto' choice) vs RCCL — BASELINE config #4. Every size is also a
+    correctness check: rank r's input is (i mod 251) + r, whose sum N (i mod 251) + N (N - 1) / 2 is exact in
+    every dtype used here and computed locally (no reference collective on multi-GiB buffers)."""
     import torch
 
     from allreduce_over_mpi_amd.utils.perf import busbw_gbps
@@ -639,7 +641,10 @@ def run_sweep(args, comm, world, rank, dev, dtype, op, dist, max_over_ranks):
     b = lo
     while b <= hi:
         n = max(1, b // es)
-        x = torch.randn(n, device=dev).to(dtype)
+        pat = torch.remainder(torch.arange(n, device=dev, dtype=torch.int32), 251)
+        x = (pat + rank).to(dtype)
+        want = (pat * world + world * (world - 1) // 2).to(torch.float32)
+        del pat
         y = torch.empty_like(x)
         iters = max(3, min(50, int(2e8 // max(b, 1))))
 
@@ -656,8 +661,13 @@ def run_sweep(args, comm, world, rank, dev, dtype, op, dist, max_over_ranks):
             return max_over_ranks(time.perf_counter() - t0) / iters
 
         tf = t_of(lambda: comm.all_reduce(x, out=y, op=op))
+        # integers up to 2^24 (fp32) / 2048 (fp16) / 256 (bf16) are exact, and so is every partial sum below them
+        limit = {torch.float32: 1 << 24, torch.float16: 2048, torch.bfloat16: 256}.get(dtype, 0)
+        exact = op == "sum" and 250 * world + world * (world - 1) // 2 <= limit
+        ok = max_over_ranks(0.0 if torch.equal(y.float(), want) else 1.0) == 0.0 if exact else None  # every rank
         row = {"bytes": n * es, "algo": comm.describe(n, dtype).split(" ")[0], "flexar_us": round(tf * 1e6, 2),
-               "flexar_busbw": round(busbw_gbps(n * es, tf, world), 2)}
+               "flexar_busbw": round(busbw_gbps(n * es, tf, world), 2), "correct": ok}
+        del want
         if world > 1 and dtype != torch.float8_e4m3fn and not args.no_rccl:
             tr = t_of(lambda: dist.all_reduce(x))
             row.update(rccl_us=round(tr * 1e6, 2), rccl_busbw=round(busbw_gbps(n * es, tr, world), 2))
