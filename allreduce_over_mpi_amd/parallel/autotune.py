@@ -29,9 +29,12 @@ from .. import _native as nv
 def default_candidates(world: int, nbytes: int) -> list[str]:
     """The schedules worth measuring for ``nbytes`` on ``world`` ranks (bench.py, tools/flexar_tune.py and
     ``autotune`` share this list): latency protocols for small buffers, every flat-stage protocol, rings
-    on 1..4 arc-disjoint channels, RHD, the two-stage FlexTree factorizations and the copy engines."""
+    on 1..4 arc-disjoint channels, RHD, the two-stage FlexTree factorizations and the copy engines. The
+    direction-balanced flat ("+bidir") joins the flat protocols: on xGMI its reduce-scatter reads and its
+    all-gather writes share the links' two directions."""
     c = ["ll", "oneshot", "oneshot+wt"] if nbytes <= (1 << 20) else (["oneshot"] if nbytes <= (8 << 20) else [])
     c += ["flat+pull", "flat+push", "flat+pull+nts", "flat+push+nts", "flat+pull+wt", "flat+push+wt"]
+    c += ["flat+bidir", "flat+bidir+nts", "flat+bidir+wt"]  # both link directions in one XFER
     maxc = len([d for d in range(1, world) if math.gcd(d, world) == 1])
     c += ["ring", "ring+wt"] + [f"ring:{k}{m}" for k in (2, 4) if k <= maxc for m in ("", "+wt")]
     if world > 2 and (world & (world - 1)) == 0:

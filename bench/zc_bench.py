@@ -24,7 +24,7 @@ def main():
 
     mib = int(os.environ.get("ZCB_MIB", "64"))
     ranks = [int(v) for v in os.environ.get("ZCB_RANKS", "2,4,8").split(",")]
-    specs = os.environ.get("ZCB_SPECS", "flat+pull,flat+pull+nts,flat+zc,flat+zc+nts,flat+zc+wt,flat+zc+push,flat+zc+push+wt,"
+    specs = os.environ.get("ZCB_SPECS", "flat+pull,flat+pull+nts,flat+push,flat+bidir,flat+bidir+wt,flat+zc,flat+zc+nts,flat+zc+wt,flat+zc+push,flat+zc+push+wt,"
                            "flat+zc+put,flat+zc+put+nts").split(",")
     count = (mib << 20) // 4
     for n in ranks:
@@ -47,6 +47,7 @@ def main():
             ms = a.elapsed_time(b) / iters
             S = count * 4
             hbm = (S * (1 + 1) if "zc+push" in spec else S * (2 + 2 * (n - 1) / n) if "zc+put" in spec
+                   else S * (2 + 4 * (n - 1) / n) if "bidir" in spec
                    else S * ((n + 1) / n + 2 * (n - 1) / n) if "zc" in spec
                    else S * (2 * (n - 1) / n + (n + 2) / n + 2 * (n - 1) / n))
             print(json.dumps({"ranks": n, "MiB_fp32": mib, "spec": spec, "ms": round(ms, 4),

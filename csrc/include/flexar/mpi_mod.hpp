@@ -273,6 +273,8 @@ inline int resolve_algo(HostComm& h, double bytes, AlgoSpec* s) {
   if (s->kind == AlgoKind::TREE && (!h.shared || s->ag == AgMode::AUTO)) s->ag = AgMode::PUSH;
   s->wire = 0;  // typed staging is a device-executor feature: the host engines run the dtype throughout
   s->zc = false;  // so are registered (zero-copy) device buffers
+  s->put = false;
+  if (!h.shared) s->bidir = false;  // the p2p engine carries messages: no peer reads
   return 0;
 }
 

@@ -83,6 +83,7 @@ inline bool build_msg_plan(uint32_t N, uint32_t r, uint64_t count, uint32_t esiz
   spec.wire = 0;
   spec.msg = false;
   spec.zc = false;  // messages carry the bytes: no peer buffer is read
+  spec.put = spec.bidir = false;
   std::vector<Program> progs(N);
   for (uint32_t p = 0; p < N; ++p) {
     Planner pl(N, p, count, esize, scale);

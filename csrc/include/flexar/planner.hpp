@@ -93,6 +93,13 @@ class Planner {
       else build_flat_zc(spec.ag == AgMode::PUSH);
       P->zc = true;
       P->desc = spec.str();
+    } else if (spec.bidir) {
+      if (wire || spec.msg || !(spec.kind == AlgoKind::TREE && spec.widths.size() == 1 && spec.widths[0] == (int)N)) {
+        if (err) *err = "+bidir is the flat schedule over IPC staging (no wire type, no +rccl)";
+        return false;
+      }
+      build_flat_bidir();
+      P->desc = spec.str();
     } else if (wire >= 2 && !(spec.kind == AlgoKind::TREE && spec.widths.size() == 1 && spec.widths[0] == (int)N)) {
       if (err) *err = "fp8 wire compression needs the flat schedule (one quantisation per contribution)";
       return false;
@@ -734,6 +741,40 @@ class Planner {
       signal(peers, 2);
       wait(peers, 2);
     }
+    finish_channel();
+  }
+
+  // Direction-balanced flat over staging ("flat+bidir"): the staging twin of "+zc+push". The staging flat
+  // schedules move the reduce-scatter and the all-gather in SEPARATE phases, each in one link direction
+  // (RS push = outgoing, then AG pull = incoming, or both outgoing), so one direction idles at a time.
+  // Here one XFER does both: every rank first copies its IN blocks p != r into its own staging (local
+  // HBM, ~S of 8 TB/s), then owner r pulls block r from every peer's copy (incoming) and writes the reduced
+  // block into its OUT and every peer's landing slot r (outgoing) - both directions of all N - 1 links
+  // busy at once - and finally copies the landed blocks into OUT (local). Two hand-offs: slot 0 "my IN
+  // copy is published", slot 1 "your landing slot r holds my block" (and I have read your copy). In place
+  // is safe: peers read the copy, never IN, and this rank writes OUT block p != r only from the landing
+  // slots after slot 1. Rank-order sum: the same bits as "+zc".
+  void build_flat_bidir() {
+    const uint64_t split = round_up((count + N - 1) / N);
+    auto boff = [&](uint32_t k) { return (uint64_t)k * split; };
+    auto blen = [&](uint32_t k) -> uint64_t {
+      const uint64_t s = boff(k);
+      return s >= count ? 0 : std::min(split, count - s);
+    };
+    const uint64_t pub = alloc((uint64_t)N * split);   // my IN copy, block p at p * split
+    const uint64_t land = alloc((uint64_t)N * split);  // owner j's reduced block j at j * split
+    auto peers = rotated_peers();
+    for (uint32_t p : peers) xfer(blen(p), {loc(BUF_IN, r, boff(p))}, {loc(BUF_STG, r, pub + boff(p))}, 1.0f);
+    signal(peers, 0);
+    wait(peers, 0);
+    std::vector<Loc> srcs;
+    for (uint32_t j = 0; j < N; ++j) srcs.push_back(j == r ? loc(BUF_IN, r, boff(r)) : loc(BUF_STG, j, pub + boff(r)));
+    std::vector<Loc> dsts{loc(BUF_OUT, r, boff(r))};
+    for (uint32_t p : peers) dsts.push_back(loc(BUF_STG, p, land + boff(r)));
+    xfer(blen(r), srcs, dsts, scale);
+    signal(peers, 1);
+    wait(peers, 1);
+    for (uint32_t p : peers) xfer(blen(p), {loc(BUF_STG, r, land + boff(p))}, {loc(BUF_OUT, r, boff(p))}, 1.0f);
     finish_channel();
   }
 

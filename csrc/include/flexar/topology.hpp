@@ -55,6 +55,10 @@ struct AlgoSpec {
   // owners' staging, and each owner writes the reduced block into every rank's registered OUT; only the
   // outputs need registering (meaningless without zc: the staging schedules already write-push)
   bool put = false;
+  // direction-balanced flat ("flat+bidir", staging, no registration): the reduce-scatter PULLS every
+  // rank's published IN copy (incoming link direction) while the same XFER pushes the reduced block into
+  // every peer's landing slot (outgoing direction), as the zero-copy push form does over registered buffers
+  bool bidir = false;
 
   std::string str() const {
     std::ostringstream ss;
@@ -70,7 +74,8 @@ struct AlgoSpec {
         break;
     }
     if (kind == AlgoKind::TREE && ag == AgMode::PULL) ss << "+pull";
-    if (kind == AlgoKind::TREE && ag == AgMode::PUSH && !(put && zc)) ss << "+push";
+    if (kind == AlgoKind::TREE && ag == AgMode::PUSH && !(put && zc) && !bidir) ss << "+push";
+    if (bidir) ss << "+bidir";
     if (!fuse) ss << "+nofuse";
     if (nts) ss << "+nts";
     if (wt) ss << "+wt";
@@ -211,6 +216,7 @@ inline bool parse_algo(const std::string& raw, int nranks, AlgoSpec* spec, std::
     else if (mod == "rccl" || mod == "msg") spec->msg = true;
     else if (mod == "zc") spec->zc = true;
     else if (mod == "put") spec->put = true, spec->ag = AgMode::PUSH;
+    else if (mod == "bidir") spec->bidir = true, spec->ag = AgMode::PUSH;
     else { if (err) *err = "unknown algorithm modifier '+" + mod + "'"; return false; }
   }
   std::string head = s, arg;
@@ -256,13 +262,14 @@ inline bool parse_algo(const std::string& raw, int nranks, AlgoSpec* spec, std::
   if (head == "ft") {
     const char* env = getenv("FT_TOPO");
     AgMode ag = spec->ag; bool fuse = spec->fuse, nts = spec->nts, wt = spec->wt, rw = spec->round_wire;
-    bool msg = spec->msg, zc = spec->zc, put = spec->put;
+    bool msg = spec->msg, zc = spec->zc, put = spec->put, bidir = spec->bidir;
     int wire = spec->wire;
     if (!parse_ft_topo(!arg.empty() ? arg.c_str() : env, nranks, spec, err)) return false;
     spec->ag = ag; spec->fuse = fuse; spec->nts = nts; spec->wt = wt; spec->wire = wire; spec->round_wire = rw;
     spec->msg = msg;
     spec->zc = zc;
     spec->put = put;
+    spec->bidir = bidir;
     return true;
   }
   if (err) *err = "unknown algorithm '" + raw + "'";

@@ -58,7 +58,8 @@ def _worker(rank, world, port, specs, q):
 def test_ipc_allreduce_processes(cuda, world):
     import torch.multiprocessing as mp
 
-    specs = ["flat", "flat+push", "ring", "ring:2", "oneshot", "flat+wt", "flat+push+wt", "ring+wt", "dma"]
+    specs = ["flat", "flat+push", "ring", "ring:2", "oneshot", "flat+wt", "flat+push+wt", "ring+wt", "dma", "flat+bidir",
+             "flat+bidir+nts"]
     specs += ["rhd", "tree:2,2+push", "tree:2,2+wt"] if world == 4 else []
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -391,7 +392,8 @@ def _stress_worker(rank, world, port, calls, q, fault=""):
 
         comm = Communicator(workspace_bytes=32 << 20)
         specs = ["flat", "flat+push", "flat+wt", "flat+push+nts", "ring", "ring+wt", "oneshot", "ll", "dma",
-                 "rhd", "tree:2,2+push"] if world == 4 else ["flat", "flat+push+wt", "ring", "oneshot", "ll", "dma"]
+                 "rhd", "tree:2,2+push", "flat+bidir"] if world == 4 else ["flat", "flat+push+wt", "ring", "oneshot", "ll", "dma",
+                                                              "flat+bidir+wt"]
         specs += ["flat+zc", "flat+zc+push", "flat+zc+put"]
         # zero-copy calls run on registered arenas (the same offsets on every rank: the same call sequence)
         arena_in = torch.empty(world * 2_000_003 + 64, device="cuda")

@@ -71,7 +71,7 @@ def _specs(n):
 
     base = ["flat", "flat+push", "ring", "oneshot", "ll", "flat+nts", "ring:2+nts"]
     base += ["flat+wt", "flat+push+wt", "ring+wt", "ring:2+wt", "oneshot+wt", "dma", "flat+zc", "flat+zc+wt", "flat+zc+push",
-             "flat+zc+put"]
+             "flat+zc+put", "flat+bidir", "flat+bidir+wt"]
     base += [p for p in nv.enumerate_plans(n) if p.startswith("tree:") or p.startswith("ring:")]
     base += [p + "+push" for p in nv.enumerate_plans(n) if p.startswith("tree:") and "," in p]
     return sorted(set(base))

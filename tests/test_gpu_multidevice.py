@@ -93,7 +93,8 @@ def test_allreduce_one_process_per_gpu(cuda):
     import torch.multiprocessing as mp
 
     world = min(_ngpu(), 8)
-    specs = ["flat", "flat+push", "flat+wt", "ring", "ring+wt", "oneshot", "ll", "dma", "flat+rccl", "ring+rccl"]
+    specs = ["flat", "flat+push", "flat+wt", "ring", "ring+wt", "oneshot", "ll", "dma", "flat+rccl", "ring+rccl",
+             "flat+bidir", "flat+bidir+nts"]
     if world > 2:
         specs.append("ring:2")
     if world >= 4 and (world & (world - 1)) == 0:

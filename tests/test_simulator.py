@@ -192,3 +192,34 @@ def test_all_to_all(nv, n):
         for p in range(n):
             want = np.concatenate([ins[r][p * m:(p + 1) * m] for r in range(n)])
             np.testing.assert_array_equal(outs[p], want, err_msg=f"n={n} m={m} p={p}")
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 7, 8, 12, 16])
+@pytest.mark.parametrize("spec", ["flat+bidir", "flat+bidir+wt", "flat+bidir+nts"])
+def test_flat_bidir(nv, n, spec):
+    """Direction-balanced flat over staging (planner.hpp build_flat_bidir): the reduce-scatter pulls the
+    peers' published IN copies while the same XFER pushes the reduced block into every peer's landing slot.
+    Exact sums with uneven tails, out of place and in place, over consecutive calls (both staging parities)."""
+    for count in (1, 35, 4099, 10007):
+        ins = [np.random.default_rng(7 * r + count).integers(-99, 99, count).astype(np.int32) for r in range(n)]
+        want = np.sum(ins, axis=0)
+        for in_place in (False, True):
+            for o in nv.simulate(spec, ins, ncalls=3, grid=3, in_place=in_place):
+                np.testing.assert_array_equal(o, want)
+
+
+def test_flat_bidir_shape_and_bits(nv):
+    d = nv.plan_dump("flat+bidir", 1, 4, 4096, "float32")
+    assert "2 flag slots" in d and d.count("XFER") == 7, d  # 3 local copies, 1 pull-reduce-push, 3 copy-outs
+    # one XFER reads every peer's staging AND writes every peer's staging: both link directions at once
+    fused = [ln for ln in d.splitlines() if "OUT@1" in ln and "STG@0" in ln.split("->")[0]]
+    assert len(fused) == 1 and all(f"STG@{p}" in fused[0].split("->")[1] for p in (0, 2, 3)), d
+    # rank-order sum: the same bits as the zero-copy forms
+    ins = [np.random.default_rng(r).standard_normal(9001).astype(np.float32) * (r + 1) for r in range(8)]
+    ref = nv.simulate("flat+zc", ins, grid=2, op="avg")[0]
+    for o in nv.simulate("flat+bidir", ins, grid=2, op="avg"):
+        assert np.array_equal(o, ref)
+    # the message transport has no peer reads: "+bidir" falls back to the push flat's messages there
+    assert nv.msg_plan("flat+bidir", 0, 4, 1 << 20, "float32")["messages"] == 6
+    with pytest.raises(nv.FlexarError):
+        nv.simulate("ring+bidir", [np.zeros(64, np.int32)] * 4)

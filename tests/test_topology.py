@@ -136,7 +136,7 @@ def test_plans_move_bandwidth_optimal_bytes(nv, n):
     specs = [p for p in nv.enumerate_plans(n) if p.startswith(("tree:", "ring"))]
     specs = [s for s in specs if not s.startswith("tree:") or
              __import__("math").prod(int(w) for w in s[5:].split(",")) == n]  # lonely trees fold extra data
-    specs += [s + "+push" for s in specs if s.startswith("tree:")] + ["flat", "oneshot"]
+    specs += [s + "+push" for s in specs if s.startswith("tree:")] + ["flat", "oneshot", "flat+bidir"]
     for spec in specs:
         want = (n - 1) * count if spec == "oneshot" else 2 * (n - 1) * count / n
         for r in range(n):
