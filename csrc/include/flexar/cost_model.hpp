@@ -111,7 +111,6 @@ struct XgmiModel {
           }
           return true;
         }
-        if (s.bidir) f[3] += S / 1e3;  // the local IN copy it publishes
         if (s.ag == AgMode::PUSH || s.ag == AgMode::AUTO) f[3] += S / 1e3;  // local copy-out of pushed blocks
         return true;
       }
