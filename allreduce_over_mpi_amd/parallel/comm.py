@@ -184,18 +184,51 @@ class Communicator:
         self.selftest_failed: list[str] = []
         if os.environ.get("FLEXAR_SELFTEST", "1") == "0":
             return
-        fam = sum(nv.FAMILIES.values())
-        failed = ctypes.c_uint32(0)
-        rc = self._lib.flexar_comm_selftest(self._h, fam, ctypes.byref(failed))
-        msg = f"{rc}:{failed.value}:{nv.last_error() if rc else ''}".encode()
-        rows = [m.decode(errors="replace").split(":", 2) for m in exchange(msg)]  # also the barrier
-        errs = [f"rank {r}: {e}" for r, (c, _, e) in enumerate(rows) if c != "0"]
-        if errs:
-            self.close()
-            raise nv.FlexarError(3, "self-test: " + "; ".join(errs))
+        # FLEXAR_SELFTEST_SKEW="RANK:MS" (tests): that rank starts the first family MS late, past its peers'
+        # watchdog - the transient failure the retry below must absorb
+        skew = os.environ.get("FLEXAR_SELFTEST_SKEW", "")
+        late_ms = float(skew.split(":")[1]) if skew.count(":") == 1 and int(skew.split(":")[0]) == self.rank else 0.0
+
+        def run(fam):
+            """One family's exact allreduces, started together (a barrier first: a rank that arrives seconds
+            late - e.g. still finishing RCCL set-up - would otherwise trip its peers' short watchdog and shift
+            every later family out of step); returns the families that failed on ANY rank."""
+            nonlocal late_ms
+            exchange(b"")
+            if late_ms:
+                import time
+
+                time.sleep(late_ms / 1000.0)
+                late_ms = 0.0
+            failed = ctypes.c_uint32(0)
+            rc = self._lib.flexar_comm_selftest(self._h, fam, ctypes.byref(failed))
+            msg = f"{rc}:{failed.value}:{nv.last_error() if rc else ''}".encode()
+            rows = [m.decode(errors="replace").split(":", 2) for m in exchange(msg)]  # also the barrier
+            errs = [f"rank {r}: {e}" for r, (c, _, e) in enumerate(rows) if c != "0"]
+            if errs:
+                self.close()
+                raise nv.FlexarError(3, "self-test: " + "; ".join(errs))
+            m = 0
+            for _, f, _ in rows:
+                m |= int(f)
+            if m:  # every rank has finished every call of this family: forget its watchdog state
+                nv.check(self._lib.flexar_comm_clear_error(self._h), "clear_error")
+            return m
+
         mask = 0
-        for _, f, _ in rows:
-            mask |= int(f)
+        for fam in nv.FAMILIES.values():
+            mask |= run(fam)
+        # a failure must repeat to disable a family: a transient one (a rank descheduled past the watchdog)
+        # passes the second time, a broken protocol fails again (families a communicator cannot run at all,
+        # e.g. peer-memory ones without IPC mappings, fail at once without launching anything)
+        self.selftest_recovered = []
+        if mask:
+            again = 0
+            for fam in nv.FAMILIES.values():
+                if mask & fam:
+                    again |= run(fam)
+            self.selftest_recovered = nv.family_names(mask & ~again)
+            mask = again
         if mask:
             # every rank has finished every self-test call (the exchange above): forget the watchdog state
             nv.check(self._lib.flexar_comm_clear_error(self._h), "clear_error")

@@ -308,6 +308,7 @@ def main():
     algo = args.algo
     tune_log = {}
     calib = None
+    ranked = []  # (spec, grid) in the order the timed region tries them
     if fallback:
         algo = "rccl"
     elif world > 1 and algo == "auto" and not args.no_tune:
@@ -379,7 +380,8 @@ def main():
             grids = [g for g in (32, 64, 128, 256, 512, 1024) if g <= resident and
                      (not shared or g <= int(os.environ["FLEXAR_MAX_GRID"]))]
             best, best_grid, best_t = None, 0, float("inf")
-            for spec in sorted(timings, key=timings.get)[:2]:
+            ranked_specs = sorted(timings, key=timings.get)
+            for spec in ranked_specs[:2]:
                 if timings[spec] < best_t:
                     best, best_grid, best_t = spec, 0, timings[spec]
                 for g in grids:
@@ -390,39 +392,88 @@ def main():
                         best, best_grid, best_t = spec, g, t
             comm.set_grid(best_grid)
             algo = best
+            # the runners-up (auto grid) stand by in case the pick fails its final checks on this node
+            ranked = [(best, best_grid)] + [(sp, 0) for sp in ranked_specs if sp != best][:2]
             log(rank, f"tuner: selected {algo} grid={best_grid or 'auto'}")
             if rank == 0 and args.tune_out:
                 with open(args.tune_out, "a") as f:  # "nranks bytes spec" (cost_model.hpp TuneTable)
                     f.write(f"{world} {nbytes} {algo}\n")
 
-    ok, err = check(algo)
-    if max_over_ranks(0.0 if ok else 1.0) != 0.0:
-        raise SystemExit(f"{algo} result mismatch vs RCCL (max rel err {err:.3g})")
-    desc = comm.describe(count, dtype) if algo == "auto" else algo
-    log(rank, f"correctness vs {'RCCL' if world > 1 else 'input'}: max rel err {err:.3g} (ok); running {desc}")
-
     # ---------------------------------------------------------------- timed region
-    a = None if algo == "auto" else algo
-    for _ in range(args.warmup):
-        comm.all_reduce(x, out=y, op=op, algo=a)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        comm.all_reduce(x, out=y, op=op, algo=a)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = max_over_ranks(time.perf_counter() - t0)
-    comm.check()
-    t_step = elapsed / max(1, args.steps)
-    # the timed calls must have produced correct results too (checked again right after, same protocol state)
-    ok, err_after = check(algo)
-    if max_over_ranks(0.0 if ok else 1.0) != 0.0:
-        raise SystemExit(f"{algo} result mismatch vs RCCL after the timed run (max rel err {err_after:.3g})")
+    # The chosen algorithm is checked right before and right after the timed steps (same protocol state). A
+    # failure there - a protocol that passed the tuner's checks but not these, e.g. an intermittent visibility
+    # problem on a node never seen before - must not lose the run: the next-fastest correct candidate takes
+    # over (fresh communicator), then RCCL, and the JSON line names what was rejected and why.
+    if not ranked:
+        ranked = [(algo, None)]
+    if world > 1 and not host_ref and algo != "rccl":
+        ranked.append(("rccl", None))
+    rejected = {}
+    t_step = err = None
+    for attempt, (algo, grid) in enumerate(ranked):
+        if algo == "rccl" and not isinstance(comm, RcclOnly):
+            comm.close()
+            torch.cuda.synchronize()
+            comm, fallback = RcclOnly(dist), fallback or "every flexar candidate failed its final checks"
+        elif attempt > 0:  # the failed attempt may have left epochs / flags inconsistent
+            comm.close()
+            torch.cuda.synchronize()
+            comm = make_comm() or RcclOnly(dist)
+            zc = register_buffers(comm)
+            if "+zc" in algo and not zc:
+                rejected[algo] = "zero-copy registration failed on the rebuilt communicator"
+                continue
+        if grid is not None:
+            comm.set_grid(grid)
+        failed, err = 0.0, 0.0
+        try:
+            ok, err = check(algo)
+            comm.check()
+            failed = 0.0 if ok else 1.0
+        except nv.FlexarError as e:
+            failed, err = 1.0, str(e)
+        if attempt == 0 and os.environ.get("FLEXAR_BENCH_REJECT_FIRST") == "1":  # rehearses this fallback chain
+            failed, err = 1.0, "rejected by FLEXAR_BENCH_REJECT_FIRST=1"
+        if max_over_ranks(failed) != 0.0:
+            rejected[algo] = f"final check failed before timing ({err if isinstance(err, str) else f'max rel err {err:.3g}'})"
+            log(rank, f"{algo}: {rejected[algo]}; trying the next candidate")
+            continue
+        desc = comm.describe(count, dtype) if algo == "auto" else algo
+        log(rank, f"correctness vs {'RCCL' if world > 1 else 'input'}: max rel err {err:.3g} (ok); running {desc}")
+        a = None if algo == "auto" else algo
+        for _ in range(args.warmup):
+            comm.all_reduce(x, out=y, op=op, algo=a)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            comm.all_reduce(x, out=y, op=op, algo=a)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = max_over_ranks(time.perf_counter() - t0)
+        t_step = elapsed / max(1, args.steps)
+        # the timed calls must have produced correct results too (checked again right after, same protocol state)
+        failed, err_after = 0.0, 0.0
+        try:
+            comm.check()
+            ok, err_after = check(algo)
+            comm.check()
+            failed = 0.0 if ok else 1.0
+        except nv.FlexarError as e:
+            failed, err_after = 1.0, str(e)
+        if max_over_ranks(failed) == 0.0:
+            break
+        rejected[algo] = f"failed after the timed run ({err_after})"
+        log(rank, f"{algo}: {rejected[algo]}; trying the next candidate")
+        t_step = None
+    if t_step is None:
+        raise SystemExit(f"no algorithm passed the final checks: {rejected}")
+    if rejected and tune_log is not None:
+        tune_log["rejected_after_tuning"] = rejected
 
     rccl_busbw = None
     if world > 1 and not args.no_rccl and dtype != torch.float8_e4m3fn:

@@ -1240,6 +1240,7 @@ int flexar_comm_connect(flexar_comm_t c, const void* all) {
       if (e != hipSuccess) (void)hipIpcCloseMemHandle(c->peer_stg[r]);
     }
     if (e != hipSuccess) {
+      (void)hipGetLastError();  // the caller may fall back to the message transport: clear the sticky error
       set_error("mapping the workspace of rank " + std::to_string(r) + " (" + link_name(c->link_cls[r]) + " peer " +
                 c->peer_bus[r] + ") failed: hipIpcOpenMemHandle: " + hipGetErrorString(e) +
                 " (HSA_ENABLE_IPC_MODE_LEGACY=0 is needed on dmabuf-only drivers)");
@@ -1418,6 +1419,7 @@ static void reg_drop(flexar_comm* c, size_t i) {
     }
   }
   c->regs.erase(c->regs.begin() + (long)i);
+  (void)hipGetLastError();  // an ignored close failure must not surface in the caller's next launch
 }
 
 int flexar_reg_export(flexar_comm_t c, const void* ptr, size_t bytes, void* out) {
@@ -1499,6 +1501,7 @@ int flexar_reg_open(flexar_comm_t c, const void* ptr, size_t bytes, const void* 
         c->ipc_maps.erase(it);
       }
     }
+    (void)hipGetLastError();  // the failed open (and any close) must not stay the thread's sticky error
   };
   for (int p = 0; p < c->nranks; ++p) {
     RegBlob b;
@@ -1634,16 +1637,22 @@ int flexar_comm_destroy(flexar_comm_t c) {
   if (!c) return 0;
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
+  // teardown keeps going past failures; FLEXAR_LOG_LEVEL=info names them
+  auto ipc_close = [&](void* p, const char* what, int r) {
+    const hipError_t e = hipIpcCloseMemHandle(p);
+    if (e != hipSuccess)
+      logf(LOG_INFO, c->rank, "destroy: hipIpcCloseMemHandle(%s of rank %d, %p): %s", what, r, p, hipGetErrorString(e));
+  };
   for (auto& kv : c->cache) {
     (void)hipFree(kv.second->d_ops);
     (void)hipFree(kv.second->d_chan);
   }
   for (int r = 0; r < c->nranks; ++r)
     if (c->opened[r]) {
-      (void)hipIpcCloseMemHandle(c->peer_stg[r]);
-      (void)hipIpcCloseMemHandle(c->peer_flags[r]);
+      ipc_close(c->peer_stg[r], "workspace", r);
+      ipc_close(c->peer_flags[r], "flags", r);
     }
-  for (auto& kv : c->ipc_maps) (void)hipIpcCloseMemHandle(kv.second.first);
+  for (auto& kv : c->ipc_maps) ipc_close(kv.second.first, "registration", -1);
   c->ipc_maps.clear();
   c->regs.clear();
   for (int r = 0; r < kMaxRanks; ++r) {
@@ -1669,6 +1678,9 @@ int flexar_comm_destroy(flexar_comm_t c) {
   (void)hipFree(c->epochs);
   (void)hipHostFree(c->err_host);
   delete c;
+  // teardown ignores failures (e.g. closing a mapping a peer already released), but HIP keeps the last one
+  // as the thread's sticky error, and the caller's framework would report it at its next kernel launch
+  (void)hipGetLastError();
   return 0;
 }
 

@@ -505,7 +505,9 @@ def _readiness_worker(rank, world, port, q, fault):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
                           FLEXAR_TIMEOUT_MS="20000", FLEXAR_SELFTEST_TIMEOUT_MS="300")
-        if fault:
+        if fault.startswith("skew:"):
+            os.environ["FLEXAR_SELFTEST_SKEW"] = fault[5:]
+        elif fault:
             os.environ["FLEXAR_FAULT_INJECT"] = fault
         import torch.distributed as dist
 
@@ -528,19 +530,21 @@ def _readiness_worker(rank, world, port, q, fault):
         comm.close()
         dist.barrier()
         dist.destroy_process_group()
-        q.put((rank, (topo, stats, errs, list(comm.selftest_failed), desc), None))
+        q.put((rank, (topo, stats, errs, list(comm.selftest_failed), desc, list(comm.selftest_recovered)), None))
     except Exception:  # pragma: no cover
         import traceback
 
         q.put((rank, None, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("fault", ["", "drop:1:0:0"])
+@pytest.mark.parametrize("fault", ["", "drop:1:0:0", "skew:1:1500"])
 def test_ipc_connect_readiness_gate(cuda, fault):
     """Connect-time probe + exact self-test (readiness.hpp). Healthy: every family verified, peers on the
     same GPU. With rank 1 dropping its slot-0 SIGNAL (every executor schedule then breaks), the self-test
     disables the fence and write-through families on BOTH ranks and calls run on a verified family
-    (copy engines / LL) with exact results instead of timing out."""
+    (copy engines / LL) with exact results instead of timing out. With rank 1 starting the first family
+    1.5 s late (past the 0.3 s self-test watchdog: a transient failure), that family fails once, passes the
+    repeat, and nothing is disabled."""
     import torch.multiprocessing as mp
 
     world = 2
@@ -555,12 +559,14 @@ def test_ipc_connect_readiness_gate(cuda, fault):
         p.join(timeout=60)
     for rank, out, tb in res:
         assert tb is None, tb
-        topo, stats, errs, failed, desc = out
+        topo, stats, errs, failed, desc, recovered = out
         assert [p["link"] for p in topo["peers"]] == ["self" if r == rank else "same-device" for r in range(world)]
         assert topo["peers"][rank]["bus"] and topo["links"] == 1
         assert stats["selftested"] == "fence,wt,ll,dma"
         assert stats["resident_blocks"] >= 256, stats
-        if fault:
+        if fault.startswith("skew:"):
+            assert recovered == ["fence"] and failed == [] and stats["disabled"] == "", (recovered, failed, stats)
+        elif fault:
             assert failed == ["fence", "wt"], failed
             assert stats["disabled"] == "fence,wt"
             assert desc.startswith("dma"), desc
