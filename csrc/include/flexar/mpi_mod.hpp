@@ -463,12 +463,27 @@ inline flexar_comm_t device_comm(MPI_Comm comm) {
   if (!all_ok) abort();
   // connect-time self-test (readiness.hpp): a protocol family that failed on any rank is disabled on all
   if (size > 1 && !(getenv("FLEXAR_SELFTEST") && strcmp(getenv("FLEXAR_SELFTEST"), "0") == 0)) {
-    uint32_t failed = 0, any = 0;
-    if (flexar_comm_selftest(d->c, PF_ALL, &failed)) {
-      fprintf(stderr, "[flexar] rank %d self-test: %s\n", rank, flexar_last_error());
-      abort();
+    // one family at a time behind a barrier, and a failed family once more before it is disabled (a rank
+    // arriving past its peers' short watchdog must not shift every later family out of step)
+    auto run = [&](uint32_t fam) -> uint32_t {
+      uint32_t failed = 0, any = 0;
+      MPI_Barrier(comm);
+      if (flexar_comm_selftest(d->c, fam, &failed)) {
+        fprintf(stderr, "[flexar] rank %d self-test: %s\n", rank, flexar_last_error());
+        abort();
+      }
+      MPI_Allreduce(&failed, &any, 1, MPI_UINT32_T, MPI_BOR, comm);
+      if (any) flexar_comm_clear_error(d->c);  // every rank is past this family's calls
+      return any;
+    };
+    uint32_t any = 0;
+    for (uint32_t fam = 1; fam & PF_ALL; fam <<= 1) any |= run(fam);
+    if (any) {
+      uint32_t again = 0;
+      for (uint32_t fam = 1; fam & PF_ALL; fam <<= 1)
+        if (any & fam) again |= run(fam);
+      any = again;
     }
-    MPI_Allreduce(&failed, &any, 1, MPI_UINT32_T, MPI_BOR, comm);
     if (any) {
       flexar_comm_clear_error(d->c);  // every rank is past its self-test calls (the allreduce above)
       flexar_comm_set_disabled(d->c, any);
