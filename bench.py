@@ -414,15 +414,20 @@ def main():
         if algo == "rccl" and not isinstance(comm, RcclOnly):
             comm.close()
             torch.cuda.synchronize()
-            comm, fallback = RcclOnly(dist), fallback or "every flexar candidate failed its final checks"
+            comm = RcclOnly(dist)
         elif attempt > 0:  # the failed attempt may have left epochs / flags inconsistent
             comm.close()
             torch.cuda.synchronize()
             comm = make_comm() or RcclOnly(dist)
+            if isinstance(comm, RcclOnly):
+                rejected[algo] = "the flexar communicator could not be rebuilt"
+                continue
             zc = register_buffers(comm)
             if "+zc" in algo and not zc:
                 rejected[algo] = "zero-copy registration failed on the rebuilt communicator"
                 continue
+        if algo == "rccl":
+            fallback = fallback or "every flexar candidate failed its final checks"
         if grid is not None:
             comm.set_grid(grid)
         failed, err = 0.0, 0.0
