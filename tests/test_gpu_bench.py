@@ -1,0 +1,45 @@
+"""The driver's bench contract at N > 1, on a 1-GPU box: bench.py under torch.distributed.run with two ranks
+sharing device 0 and RCCL in the loop (FLEXAR_BENCH_SHARED_RCCL=1: one NCCL_HOSTID per rank). The tuner's pick
+is rejected on purpose (FLEXAR_BENCH_REJECT_FIRST=1), so the final-check fallback chain must hand over to the
+runner-up on a rebuilt communicator, which must still pass its connect-time self-test on every IPC family, and
+the one JSON line must carry the contract's keys and name the rejection."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_bench_json_and_fallback_chain_two_ranks(cuda):
+    env = dict(os.environ, FLEXAR_BENCH_SHARED_GPU="1", FLEXAR_BENCH_SHARED_RCCL="1", FLEXAR_BENCH_REJECT_FIRST="1",
+               FLEXAR_NO_BUILD="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--size-mb", "16", "--no-calibrate", "--no-small"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110, cwd=REPO)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in out, k
+    assert out["n_gpus"] == 2 and out["steps"] == 3 and out["value"] == out["busbw_GBps"] > 0
+    rejected = out["tuner"]["rejected_after_tuning"]
+    assert len(rejected) == 1 and "FLEXAR_BENCH_REJECT_FIRST" in next(iter(rejected.values())), rejected
+    assert out["fallback"] is None and out["config"]["algorithm"] not in rejected, out["config"]
+    assert out["readiness"]["disabled"] == "", out["readiness"]  # the rebuilt communicator kept every family
