@@ -80,6 +80,15 @@ class FlexarProcessGroup(dist.ProcessGroup):
         self._streams = {}
         self.hierarchical = False
         self._grid = int(os.environ.get("FLEXAR_PG_GRID", "0") or 0)  # executor workgroups (0 = auto)
+        # zero copy for persistent buffers (DDP gradient buckets): during the first FLEXAR_PG_ZC_PROBES
+        # allreduces every rank agrees (one host MIN over gloo) whether its tensor is new and >= 1 MiB, and
+        # such tensors are registered collectively; later calls on them then switch to "+zc+push" by
+        # themselves (comm.hip, FLEXAR_ZC_AUTO). The probe count is the same on every rank, so the
+        # agreement round never diverges. FLEXAR_PG_ZC=0 keeps every call on the staging schedules.
+        self._zc_on = os.environ.get("FLEXAR_PG_ZC", "1") == "1"
+        self._zc_probes_left = int(os.environ.get("FLEXAR_PG_ZC_PROBES", "64") or 0)
+        self._zc_seen = set()  # (data_ptr, nbytes) registered by this process group
+        self._zc_min = int(os.environ.get("FLEXAR_PG_ZC_MIN_BYTES", str(1 << 20)))
 
     # ------------------------------------------------------------------ plumbing
     def getBackendName(self):
@@ -168,6 +177,8 @@ class FlexarProcessGroup(dist.ProcessGroup):
             return self._fallback(tensor_list).allreduce(tensor_list, opts)
         dev = tensor_list[0].device
         comm = self.comm(dev.index)
+        if self._zc_on and self._zc_probes_left > 0 and not self.hierarchical and self._world > 1:
+            self._zc_probe(comm, tensor_list)
         cur = torch.cuda.current_stream(dev)
         side = self._side_stream(dev) if self.async_stream else cur
         if side is not cur:
@@ -187,6 +198,27 @@ class FlexarProcessGroup(dist.ProcessGroup):
             fut = torch.futures.Future(devices=[dev])
             fut.set_result(tensor_list)  # records an event on the side stream; wait() joins it
         return _create_work_from_future(fut)
+
+    def _zc_probe(self, comm, tensor_list):
+        """One agreement round of the zero-copy probe (see __init__): register this call's tensor when every
+        rank's is a new, 16-B aligned single tensor of at least FLEXAR_PG_ZC_MIN_BYTES (1 MiB)."""
+        self._zc_probes_left -= 1
+        t = tensor_list[0]
+        key = (t.data_ptr(), t.numel() * t.element_size())
+        want = (len(tensor_list) == 1 and key[1] >= self._zc_min and key[0] % 16 == 0 and key not in self._zc_seen
+                and len(self._zc_seen) < 64)
+        flag = torch.tensor([1 if want else 0], dtype=torch.int32)
+        o = AllreduceOptions()
+        o.reduceOp = dist.ReduceOp.MIN
+        self._gloo.allreduce([flag], o).wait()
+        if int(flag.item()) != 1:
+            return
+        try:
+            comm.register(t)  # collective; the allocation is mapped by the peers (DESIGN.md §17)
+            self._zc_seen.add(key)
+            self.stats["zc_registrations"] = self.stats.get("zc_registrations", 0) + 1
+        except nv.FlexarError:  # refused on every rank together (readiness check, allocation cap): staging
+            self._zc_on = False
 
     def _side_stream(self, dev):
         s = self._streams.get(dev.index)

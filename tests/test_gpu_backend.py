@@ -36,7 +36,7 @@ def _fallback_env(rank, fallback):
 def _train(rank, world, port, q, mode, model_kind="mlp", fallback="gloo"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
-                          FLEXAR_TIMEOUT_MS="20000")
+                          FLEXAR_TIMEOUT_MS="20000", FLEXAR_PG_ZC_MIN_BYTES="65536")  # GPT-tiny buckets register
         _fallback_env(rank, fallback)
         import torch.distributed as dist
         import torch.nn as nn
@@ -94,6 +94,8 @@ def _train(rank, world, port, q, mode, model_kind="mlp", fallback="gloo"):
         pg = dist.group.WORLD
         used = (getattr(pg, "stats", {}).get("flexar_allreduce", 0) if mode == "backend" else
                 1 if mode == "nccl" else state.calls)
+        if mode == "backend" and model_kind == "gpt" and not pg.stats.get("zc_registrations"):
+            used = 0  # the gradient buckets must have been registered (zero copy) by the backend's probe
         if mode == "zchook" and not state._bucket_regs:
             used = 0  # the zero-copy path must actually have registered the buckets
         dist.destroy_process_group()
