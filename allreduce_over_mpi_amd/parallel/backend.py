@@ -177,7 +177,8 @@ class FlexarProcessGroup(dist.ProcessGroup):
             return self._fallback(tensor_list).allreduce(tensor_list, opts)
         dev = tensor_list[0].device
         comm = self.comm(dev.index)
-        if self._zc_on and self._zc_probes_left > 0 and not self.hierarchical and self._world > 1:
+        if (self._zc_on and self._zc_probes_left > 0 and not self.hierarchical and self._world > 1
+                and not torch.cuda.is_current_stream_capturing()):  # no registration inside a graph capture
             self._zc_probe(comm, tensor_list)
         cur = torch.cuda.current_stream(dev)
         side = self._side_stream(dev) if self.async_stream else cur
