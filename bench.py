@@ -135,6 +135,11 @@ def main():
         args.no_rccl = args.no_rccl or not shared_rccl
         # every rank's workgroups must be co-resident on the one GPU (they spin on each other)
         os.environ.setdefault("FLEXAR_MAX_GRID", str(max(8, 256 // (2 * world))))
+    ndev = torch.cuda.device_count()
+    if not shared and ndev and local >= ndev:
+        # a launcher that restricts each rank to its own GPU (HIP_VISIBLE_DEVICES per rank): that GPU is device 0
+        log(rank, f"LOCAL_RANK {local} but {ndev} visible device(s): using device {local % ndev}")
+        local = local % ndev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
