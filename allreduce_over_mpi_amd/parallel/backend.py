@@ -84,8 +84,9 @@ class FlexarProcessGroup(dist.ProcessGroup):
         # allreduces every rank agrees (one host MIN over gloo) whether its tensor is new and >= 1 MiB, and
         # such tensors are registered collectively; later calls on them then switch to "+zc+push" by
         # themselves (comm.hip, FLEXAR_ZC_AUTO). The probe count is the same on every rank, so the
-        # agreement round never diverges. FLEXAR_PG_ZC=0 keeps every call on the staging schedules.
-        self._zc_on = os.environ.get("FLEXAR_PG_ZC", "1") == "1"
+        # agreement round never diverges. Opt-in (FLEXAR_PG_ZC=1): a registration keeps its buffer alive,
+        # so buffers DDP replaces (its bucket rebuild after the first iteration) stay allocated.
+        self._zc_on = os.environ.get("FLEXAR_PG_ZC", "0") == "1"
         self._zc_probes_left = int(os.environ.get("FLEXAR_PG_ZC_PROBES", "64") or 0)
         self._zc_seen = set()  # (data_ptr, nbytes) registered by this process group
         self._zc_min = int(os.environ.get("FLEXAR_PG_ZC_MIN_BYTES", str(1 << 20)))

@@ -36,7 +36,7 @@ def _fallback_env(rank, fallback):
 def _train(rank, world, port, q, mode, model_kind="mlp", fallback="gloo"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
-                          FLEXAR_TIMEOUT_MS="20000", FLEXAR_PG_ZC_MIN_BYTES="65536")  # GPT-tiny buckets register
+                          FLEXAR_TIMEOUT_MS="20000", FLEXAR_PG_ZC="1", FLEXAR_PG_ZC_MIN_BYTES="65536")  # GPT-tiny buckets register
         _fallback_env(rank, fallback)
         import torch.distributed as dist
         import torch.nn as nn
