@@ -423,7 +423,7 @@ class FlexarHookState:
         self.calls = 0
         self._streams = {}
         if zero_copy is None:
-            zero_copy = os.environ.get("FLEXAR_HOOK_ZC", "0") == "1"
+            zero_copy = os.environ.get("FLEXAR_HOOK_ZC", "1") == "1"
         self.zero_copy = bool(zero_copy) and self.comm.world_size > 1 and hasattr(self.comm, "register")
         self._bucket_regs = {}  # bucket index -> (data_ptr, nbytes, registration id)
         self.registrations = 0  # buckets registered so far (first sight + DDP's one bucket rebuild)
