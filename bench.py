@@ -296,6 +296,12 @@ def main():
             log(rank, f"cost model: {choice} predicted {model['predicted_us']} us, measured {model['measured_us']} us")
         except nv.FlexarError as e:
             model = {"error": str(e)}
+        if max_over_ranks(1.0 if "error" in model else 0.0) != 0.0:  # a failed call may leave epochs / flags
+            comm.close()                                             # inconsistent: start the tuner afresh
+            torch.cuda.synchronize()
+            comm = make_comm() or RcclOnly(dist)
+            if isinstance(comm, RcclOnly):
+                fallback = "flexar communicator could not be rebuilt"
     zc = register_buffers(comm)
     if model and "error" not in model and zc:
         # the same automatic choice once the buffers are registered: the flat schedule (or any choice the
