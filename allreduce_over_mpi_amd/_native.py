@@ -105,6 +105,10 @@ def _sig(lib):
         "flexar_reg_ids": (i, [vp, c.POINTER(i), i]),
         "flexar_zc_decide": (i, [cp, i, d, i, u32, c.POINTER(i), cp, sz]),
         "flexar_model_features": (i, [cp, i, d, i, c.POINTER(d)]),
+        "flexar_model_features_ex": (i, [cp, i, d, i, i, c.POINTER(d)]),
+        "flexar_program_cost": (i, [cp, i, i, sz, i, i, c.POINTER(d)]),
+        "flexar_select_plan_ex": (i, [i, d, i, i, i, cp, sz]),
+        "flexar_apply_partials": (i, [cp, i, d, i, i, cp, sz]),
         "flexar_kernel_info": (i, [i, i, i, i, c.POINTER(i), c.POINTER(i)]),
         "flexar_downgrade_spec": (i, [cp, i, u32, i, cp, sz]),
         "flexar_direct_links": (i, [c.POINTER(c.c_int32), c.POINTER(c.c_int32), i, i]),
@@ -225,15 +229,25 @@ def model_cost_us(spec: str, nranks: int, nbytes: float) -> float:
     return v
 
 
-def model_features(spec: str, nranks: int, nbytes: float, links: int = 0):
-    """Linear cost features of ``spec``: cost_us = f . (alpha_launch, alpha_sync, 1/link_gbps, 1/hbm_gbps);
-    None for schedules outside the linear model (copy engines, LL above its size cap)."""
+def model_features(spec: str, nranks: int, nbytes: float, links: int = 0, esize: int = 4):
+    """Linear cost features of ``spec``: cost_us = f . (alpha_launch, alpha_sync, 1/link_gbps, 1/hbm_gbps),
+    read off the compiled programs for elements of ``esize`` bytes; None for schedules outside the linear
+    model (copy engines, LL above its size cap)."""
     out = (ctypes.c_double * 4)()
-    rc = lib().flexar_model_features(spec.encode(), nranks, float(nbytes), int(links), out)
+    rc = lib().flexar_model_features_ex(spec.encode(), nranks, float(nbytes), int(links), int(esize), out)
     if rc == 2:
         return None
     check(rc, "model_features")
     return list(out)
+
+
+def program_cost(spec: str, rank: int, nranks: int, count: int, dtype="float32", links: int = 0) -> dict:
+    """What rank's compiled program costs (csrc/include/flexar/cost_model.hpp program_cost): hand-offs,
+    bytes over links (remote reads + writes), the busiest link's bytes phase by phase, HBM bytes."""
+    out = (ctypes.c_double * 5)()
+    check(lib().flexar_program_cost(spec.encode(), rank, nranks, int(count), dtype_code(dtype), int(links), out),
+          "program_cost")
+    return dict(zip(("handoffs", "link_bytes", "link_time_bytes", "hbm_read", "hbm_write"), list(out)))
 
 
 def zc_decide(spec: str, nranks: int, nbytes: float, registered=True, named=False, auto=True, zc_auto=True,
@@ -249,9 +263,23 @@ def zc_decide(spec: str, nranks: int, nbytes: float, registered=True, named=Fals
     return dec.value, b.value.decode()
 
 
-def select_plan(nranks: int, nbytes: float) -> str:
+def select_plan(nranks: int, nbytes: float, dtype=None, op="sum", links: int = 0) -> str:
+    """The cost model's choice for (nranks, nbytes); with ``dtype`` the typed form that call would run
+    (FLEXAR_PARTIALS and FLEXAR_MODEL apply)."""
     b = _strbuf(256)
-    check(lib().flexar_select_plan(nranks, float(nbytes), b, 256), "select_plan")
+    if dtype is None and not links:
+        check(lib().flexar_select_plan(nranks, float(nbytes), b, 256), "select_plan")
+    else:
+        check(lib().flexar_select_plan_ex(nranks, float(nbytes), dtype_code(dtype or "float32"), op_code(op),
+                                          int(links), b, 256), "select_plan")
+    return b.value.decode()
+
+
+def apply_partials(spec: str, nranks: int, nbytes: float, dtype="bfloat16", op="sum") -> str:
+    """The typed form ``spec`` runs for a call of ``dtype`` / ``op`` under FLEXAR_PARTIALS (cost_model.hpp)."""
+    b = _strbuf(256)
+    check(lib().flexar_apply_partials(spec.encode(), nranks, float(nbytes), dtype_code(dtype), op_code(op), b, 256),
+          "apply_partials")
     return b.value.decode()
 
 

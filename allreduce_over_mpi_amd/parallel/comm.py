@@ -364,12 +364,22 @@ class Communicator:
         if os.environ.get("FLEXAR_SELFTEST", "1") == "0":
             return True
         n = 65536 + 77
-        buf = torch.empty(2 * n + 64, dtype=torch.int32, device=f"cuda:{self.device}")
-        x, y = buf[:n], buf[n + 64:]
-        idx = torch.arange(n, dtype=torch.int32, device=buf.device) % 1009
+        # the scratch allocation is agreed on before anything collective: a rank that cannot allocate must
+        # not leave its peers inside the registration's exchanges while it waits in the final agreement
+        try:
+            buf = torch.empty(2 * n + 64, dtype=torch.int32, device=f"cuda:{self.device}")
+            x, y = buf[:n], buf[n + 64:]
+            idx = torch.arange(n, dtype=torch.int32, device=buf.device) % 1009
+            have = b"1"
+        except Exception:  # noqa: BLE001 - out of memory or a device error on this rank
+            have = b"0"
+        if any(r != b"1" for r in self._exchange(have)):
+            return False
         ok = True
         self._zc_testing = True
         rid = None
+        # every later failure on this rank (registration, calls, checks) is a "no" in the agreement below,
+        # which every rank reaches: the registration and the calls are collective with their own agreements
         try:
             rid = self._register(buf)
             w = self.world_size
@@ -380,7 +390,7 @@ class Communicator:
                     want = idx * (w * (w + 1) // 2) + call * w
                     ok = ok and bool(torch.equal(y, want))
             self.check()
-        except nv.FlexarError:
+        except Exception:  # noqa: BLE001 - any failure on this rank is a "no" in the agreement
             ok = False
         finally:
             self._zc_testing = False
@@ -415,13 +425,17 @@ class Communicator:
                 self._lib.flexar_reg_close(self._h, rid.value)
             raise nv.FlexarError(rc or 1, "register: " + "; ".join(bad))
         self._regs[rid.value] = tensor
-        # a registration this one replaced (contained in it) is gone on the native side: drop its reference
+        self._prune_regs()
+        return rid.value
+
+    def _prune_regs(self):
+        """Drop the references of registrations the native side replaced (a newer registration contained
+        them, or their allocation was freed and reused): they must not keep dead tensors alive."""
         ids = (ctypes.c_int * 4096)()
         k = self._lib.flexar_reg_ids(self._h, ids, 4096)
         live = set(ids[:min(k, 4096)])
         for old in [r for r in self._regs if r not in live]:
             del self._regs[old]
-        return rid.value
 
     def register_many(self, tensors) -> list:
         """:meth:`register` for several tensors with one handle exchange and one agreement round (every
@@ -463,6 +477,7 @@ class Communicator:
             raise nv.FlexarError(1, "register: " + "; ".join(bad))
         for rid, t in zip(ids, tensors):
             self._regs[rid] = t
+        self._prune_regs()
         return ids
 
     def deregister(self, rid: int):

@@ -23,11 +23,6 @@ from collections import defaultdict
 from .. import _native as nv
 
 
-def _family(spec: str) -> str:
-    """Schedule family of a spec for winner comparisons: the model does not price protocol modifiers."""
-    return spec.split("+")[0]
-
-
 def fit_model(rows, nranks: int, links: int = 0, min_bytes: float = 0.0):
     """Least-squares fit of theta to measured rows ({"spec", "bytes", "us"}). Returns a dict with the
     parameters, the FLEXAR_MODEL string, the rows' relative errors and the winner agreement."""
@@ -38,7 +33,7 @@ def fit_model(rows, nranks: int, links: int = 0, min_bytes: float = 0.0):
     for r in rows:
         if r["bytes"] < min_bytes or not r.get("us") or r["us"] <= 0:
             continue
-        f = nv.model_features(r["spec"], nranks, float(r["bytes"]), links)
+        f = nv.model_features(r["spec"], nranks, float(r["bytes"]), links, int(r.get("esize", 4)))
         if f is None:  # copy engines / LL above its cap: not in the linear model
             continue
         feats.append(f)
@@ -59,17 +54,25 @@ def fit_model(rows, nranks: int, links: int = 0, min_bytes: float = 0.0):
     hbm_gbps = 1.0 / inv_hbm if inv_hbm > 1e-12 else 1e6
     pred = A @ theta
     rel = np.abs(pred - y) / y
-    # winner agreement per size: the model's argmin family among the measured specs vs the measured winner
+    # winner agreement per size, full specs: the measured winner must be the model's argmin among the
+    # measured specs (flat+pull and flat+zc+push are different programs with different costs). Protocol
+    # variants of one program ("+wt", "+nts") have identical features: the model ranks them as a tie, and
+    # the winner counts as picked when it is tied for the model's minimum. `regret` = measured time of the
+    # model's pick over the measured best - 1 (what following the model costs at that size).
     by_size = defaultdict(list)
     for r, p in zip(used, pred):
         by_size[r["bytes"]].append((r["us"], p, r["spec"]))
-    agree, sizes = 0, []
+    agree, sizes, regrets = 0, [], []
     for b, cands in sorted(by_size.items()):
-        best_meas = min(cands)[2]
-        best_model = min(cands, key=lambda c: c[1])[2]
-        ok = _family(best_meas) == _family(best_model)
+        meas_best, _, best_meas = min(cands)
+        pmin = min(c[1] for c in cands)
+        pick = min(cands, key=lambda c: (c[1], c[0]))  # the model's argmin (ties: its fastest member)
+        ok = any(c[2] == best_meas and c[1] <= pmin * (1 + 1e-9) for c in cands)
+        regret = pick[0] / meas_best - 1.0
         agree += ok
-        sizes.append({"bytes": b, "measured_winner": best_meas, "model_winner": best_model, "agree": ok})
+        regrets.append(regret)
+        sizes.append({"bytes": b, "measured_winner": best_meas, "model_winner": pick[2], "agree": ok,
+                      "regret": round(regret, 4)})
     return {
         "alpha_launch_us": alpha_launch, "alpha_sync_us": alpha_sync, "link_gbps": link_gbps,
         "hbm_gbps": hbm_gbps, "links": links,
@@ -77,6 +80,7 @@ def fit_model(rows, nranks: int, links: int = 0, min_bytes: float = 0.0):
                         + (f",{links}" if links > 0 else ""),
         "median_rel_err": float(np.median(rel)), "max_rel_err": float(rel.max()), "rows": len(used),
         "winner_agreement": agree / max(1, len(by_size)), "sizes": sizes,
+        "max_regret": float(max(regrets)) if regrets else 0.0,
     }
 
 

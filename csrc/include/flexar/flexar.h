@@ -264,8 +264,17 @@ double flexar_model_cost_us(const char* spec, int nranks, double bytes);
 /* Linear cost features of spec (see XgmiModel::features): 4 doubles, cost = f . (alpha_launch_us,
  * alpha_sync_us, 1/link_gbps, 1/hbm_gbps). links <= 0: the model's default link count. */
 int flexar_model_features(const char* spec, int nranks, double bytes, int links, double* out);
+/* Same for elements of `esize` bytes (typed staging of a 16/8-bit dtype prices at its real sizes). */
+int flexar_model_features_ex(const char* spec, int nranks, double bytes, int links, int esize, double* out);
+/* Cost of rank's compiled program (cost_model.hpp program_cost): out[5] = {handoffs, link_bytes,
+ * link_time_bytes (busiest link, per phase), hbm_read, hbm_write}. links <= 0: the model's default. */
+int flexar_program_cost(const char* spec, int rank, int nranks, size_t count, int dtype, int links, double* out);
 /* Cost-model choice for (nranks, bytes) written to out. */
 int flexar_select_plan(int nranks, double bytes, char* out, size_t outlen);
+/* The typed form spec runs for a call of dtype / op (FLEXAR_PARTIALS: fp32 partials "+f32", per-hop "+rw"). */
+int flexar_apply_partials(const char* spec, int nranks, double bytes, int dtype, int op, char* out, size_t outlen);
+/* Cost-model choice for a call of dtype / op (the typed form it runs included; FLEXAR_PARTIALS applies). */
+int flexar_select_plan_ex(int nranks, double bytes, int dtype, int op, int links, char* out, size_t outlen);
 /* Reference cost model (cost_model/CostModel.h) score, fixed: returns the argmin spec and cost. */
 double flexar_legacy_cost(const char* widths_csv, int nranks, double chunk);
 /* Human-readable dump of rank's op program (like Operations::print_ops). */

@@ -150,7 +150,8 @@ inline uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull)
 inline const char* const* fingerprint_vars() {
   static const char* v[] = {"FLEXAR_ALGO",     "FT_TOPO",          "FLEXAR_CHUNK_BYTES", "FLEXAR_NCHANNELS",
                             "FLEXAR_MAX_GRID", "FLEXAR_MIN_BLOCK_BYTES", "FLEXAR_MODEL",
-                            "FLEXAR_SELFTEST", "FLEXAR_ZC_AUTO", nullptr};
+                            "FLEXAR_SELFTEST", "FLEXAR_ZC_AUTO", "FLEXAR_PARTIALS", "FLEXAR_CALIB",
+                            nullptr};
   return v;
 }
 inline uint64_t env_fingerprint(const std::string& extra) {

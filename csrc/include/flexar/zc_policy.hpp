@@ -27,6 +27,7 @@ struct ZcFacts {
   bool zc_auto = true;      // FLEXAR_ZC_AUTO
   bool have_tune = false;   // a measured tune table is installed
   uint32_t disabled = 0;    // protocol families that failed the connect-time self-test
+  uint32_t esize = 4;       // element size the cost model prices the two forms at
 };
 
 // Returns 1 when the spec switched to zero copy, -1 when it fell back to staging, 0 when unchanged.
@@ -42,7 +43,7 @@ inline int zc_decide(AlgoSpec* s, const ZcFacts& f, const XgmiModel& m) {
     z.wt = s->wt;
     z.nts = s->nts;
     if (f.disabled & proto_family(z)) return 0;
-    if (flat || (!f.have_tune && m.cost_us(z, f.nranks, f.bytes) < m.cost_us(*s, f.nranks, f.bytes))) {
+    if (flat || (!f.have_tune && m.cost_us(z, f.nranks, f.bytes, f.esize) < m.cost_us(*s, f.nranks, f.bytes, f.esize))) {
       *s = z;
       return 1;
     }

@@ -241,15 +241,74 @@ double flexar_model_cost_us(const char* spec, int nranks, double bytes) {
 
 // Cost-model feature vector of (spec, nranks, bytes) under `links` concurrent links (<= 0: FLEXAR_MODEL /
 // default): cost_us = out[0] alpha_launch + out[1] alpha_sync + out[2] / link_gbps + out[3] / hbm_gbps.
-int flexar_model_features(const char* spec, int nranks, double bytes, int links, double* out) {
-  if (!out || nranks < 1) { set_error("bad arguments"); return FLEXAR_ERR_INVALID; }
+// The spec is priced as written (its typing included: "+f32" fp32 partials, "+rw" per-hop rounding) for
+// elements of `esize` bytes.
+int flexar_model_features_ex(const char* spec, int nranks, double bytes, int links, int esize, double* out) {
+  if (!out || nranks < 1 || esize < 1 || esize > 8) { set_error("bad arguments"); return FLEXAR_ERR_INVALID; }
   AlgoSpec s;
   std::string err;
   if (!spec_for(spec, nranks, bytes, &s, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
   XgmiModel m = XgmiModel::from_env();
   if (links > 0) m.links = links;
-  if (!m.features(s, nranks, bytes, out)) { set_error("no linear cost features for " + s.str()); return FLEXAR_ERR_UNSUPPORTED; }
+  if (!m.features(s, nranks, bytes, out, (uint32_t)esize)) {
+    set_error("no linear cost features for " + s.str());
+    return FLEXAR_ERR_UNSUPPORTED;
+  }
   return 0;
+}
+
+int flexar_model_features(const char* spec, int nranks, double bytes, int links, double* out) {
+  return flexar_model_features_ex(spec, nranks, bytes, links, 4, out);
+}
+
+// What rank `rank`'s compiled program of (spec, nranks, count, dtype) costs (cost_model.hpp program_cost):
+// out = {handoffs, link_bytes, link_time_bytes, hbm_read, hbm_write}. The spec is built as written:
+// "+f32" types the partials of a 16/8-bit dtype, "+rw" or no suffix leaves them in the dtype.
+int flexar_program_cost(const char* spec, int rank, int nranks, size_t count, int dtype, int links, double* out) {
+  const size_t es = dtype_size(dtype);
+  if (!out || !es || nranks < 1 || rank < 0 || rank >= nranks) { set_error("bad arguments"); return FLEXAR_ERR_INVALID; }
+  AlgoSpec s;
+  std::string err;
+  if (!spec_for(spec, nranks, (double)count * es, &s, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  if (s.kind == AlgoKind::LL || s.kind == AlgoKind::DMA) { set_error("no op program for " + s.str()); return FLEXAR_ERR_UNSUPPORTED; }
+  Program P;
+  Planner pl(nranks, rank, count, (uint32_t)es, 1.0f);
+  if (!pl.build(s, &P, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  const ProgramCost c = program_cost(P, (uint32_t)rank, links > 0 ? links : XgmiModel::from_env().links);
+  out[0] = c.handoffs;
+  out[1] = c.link_bytes;
+  out[2] = c.link_time_bytes;
+  out[3] = c.hbm_read;
+  out[4] = c.hbm_write;
+  return 0;
+}
+
+// The typed form `spec` runs for a call of dtype / op (cost_model.hpp apply_partials; FLEXAR_PARTIALS and
+// FLEXAR_MODEL apply): "+f32" fp32 partials, "+rw" per-hop rounding, or unchanged.
+int flexar_apply_partials(const char* spec, int nranks, double bytes, int dtype, int op, char* out, size_t outlen) {
+  AlgoSpec s;
+  std::string err;
+  if (nranks < 1 || !dtype_size(dtype) || !parse_algo(spec ? spec : "", nranks, &s, &err) || s.kind == AlgoKind::AUTO) {
+    set_error(err.empty() ? "apply_partials needs a concrete spec" : err);
+    return FLEXAR_ERR_INVALID;
+  }
+  if (s.kind == AlgoKind::TREE && s.ag == AgMode::AUTO) s.ag = AgMode::PULL;
+  CallKind k;
+  k.esize = (uint32_t)dtype_size(dtype);
+  k.narrow_sum = (op == FLEXAR_SUM || op == FLEXAR_AVG) && dtype_is_float(dtype) && k.esize < 4;
+  apply_partials(&s, nranks, bytes, k, XgmiModel::from_env());
+  return copy_out(s.str(), out, outlen);
+}
+
+// The selector's choice for a call of `dtype` / `op` (the typed form it would run included).
+int flexar_select_plan_ex(int nranks, double bytes, int dtype, int op, int links, char* out, size_t outlen) {
+  if (nranks < 1 || !dtype_size(dtype)) return FLEXAR_ERR_INVALID;
+  XgmiModel m = XgmiModel::from_env();
+  if (links > 0) m.links = links;
+  CallKind k;
+  k.esize = (uint32_t)dtype_size(dtype);
+  k.narrow_sum = (op == FLEXAR_SUM || op == FLEXAR_AVG) && dtype_is_float(dtype) && k.esize < 4;
+  return copy_out(select_plan(m, nranks, bytes, nullptr, k).str(), out, outlen);
 }
 
 int flexar_select_plan(int nranks, double bytes, char* out, size_t outlen) {

@@ -1,0 +1,582 @@
+// flexar communicator lifecycle: create, export, connect (readiness gate), self-test, configuration
+// setters, topology report, destroy. Reference counterpart: FlexTree_Context and the lazily created
+// scratch buffer (allreduce_over_mpi/mpi_mod.hpp:216-243, 931-950).
+#include "comm_internal.hpp"
+
+namespace flexar {
+
+// Settings fingerprint exchanged in the handle (readiness.hpp): environment knobs + workspace size +
+// the loaded tune table.
+uint64_t comm_fingerprint(flexar_comm* c) {
+  std::string extra = "ws=" + std::to_string(c->ws_bytes) + ";";
+  for (auto& n : c->tune.rows)
+    for (auto& row : n.second) extra += std::to_string(n.first) + " " + std::to_string(row.first) + " " + row.second + ";";
+  return env_fingerprint(extra);
+}
+
+// Self-test pattern (flexar_comm_selftest): rank r contributes (r + 1) * p(i), p(i) in [1, 1000], so
+// the exact sum is N (N + 1) / 2 * p(i); OUT is poisoned so an element nobody wrote is caught too.
+__device__ FX_INLINE int selftest_pattern(uint64_t i, uint32_t salt) { return (int)((i * 7 + salt) % 1000) + 1; }
+static __global__ void selftest_fill(int* in, int* out, uint64_t n, int rank, uint32_t salt) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    in[i] = (rank + 1) * selftest_pattern(i, salt);
+    out[i] = -1;
+  }
+}
+static __global__ void selftest_check(const int* out, uint64_t n, int nranks, uint32_t salt, uint32_t* bad) {
+  uint32_t mine = 0;
+  const int tri = nranks * (nranks + 1) / 2;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    mine += out[i] != tri * selftest_pattern(i, salt);
+  if (mine) __hip_atomic_fetch_add(bad, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Executor workgroups resident at once on this device: occupancy of the fp32 fence executor (the
+// largest register footprint among the hot instantiations is within one workgroup of it) x CUs.
+int resident_blocks(int device) {
+  LaunchArgs la;
+  la.kind = LAUNCH_QUERY;
+  int occ = 0, regs = 0;
+  la.occ_out = &occ;
+  la.regs_out = &regs;
+  if (launch_dtype(FLEXAR_FLOAT32, FLEXAR_SUM, la) != 0 || occ < 1) return 0;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return occ * cus;
+}
+
+int check_err(flexar_comm* c) {
+  uint32_t e = __atomic_load_n(c->err_host, __ATOMIC_ACQUIRE);
+  if ((e & 0x40000000u) && ((e >> 8) & 0xffffu) == 0xfdu) {
+    set_error("rank " + std::to_string(c->rank) + ": internal: a typed transfer with an operand pattern the "
+              "executor does not run (planner/executor mismatch)");
+    return FLEXAR_ERR_STATE;
+  }
+  if (e & 0x40000000u) {
+    char buf[200];
+    snprintf(buf, sizeof(buf), "rank %d: protocol violation — peer %u is more than one call ahead (slot %u): "
+             "two calls of this communicator overlapped", c->rank, e & 0xffu, (e >> 8) & 0xffffu);
+    set_error(buf);
+    return FLEXAR_ERR_STATE;
+  }
+  if (e) {
+    char buf[160];
+    snprintf(buf, sizeof(buf), "rank %d: device wait timed out (slot %u, peer %u) — a peer stopped participating",
+             c->rank, (e >> 8) & 0xffffu, e & 0xffu);
+    set_error(buf);
+    return FLEXAR_ERR_TIMEOUT;
+  }
+  return 0;
+}
+
+int validate_call(flexar_comm* c, int dtype, int op, float scale) {
+  if (!c) { set_error("null communicator"); return FLEXAR_ERR_INVALID; }
+  if (!c->connected) { set_error("communicator not connected"); return FLEXAR_ERR_STATE; }
+  if (!op_supported(dtype, op)) {
+    set_error(std::string("unsupported dtype/op: ") + dtype_name(dtype) + "/" + op_name(op));
+    return FLEXAR_ERR_UNSUPPORTED;
+  }
+  if (scale != 1.0f && !(dtype_is_float(dtype) && (op == FLEXAR_SUM || op == FLEXAR_AVG))) {
+    set_error("a post-scale needs a float dtype with SUM/AVG");
+    return FLEXAR_ERR_INVALID;
+  }
+  return 0;
+}
+
+int alloc_workspace(flexar_comm* c, size_t ws) {
+  FX_HIP(hipSetDevice(c->device));
+  c->ws_bytes = (ws + 511) / 512 * 512;
+  c->half_bytes = c->ws_bytes / 2 / kStageAlignBytes * kStageAlignBytes;
+  FX_HIP(hipMalloc(&c->stg, c->ws_bytes));
+  FX_HIP(hipMemset(c->stg, 0, c->ws_bytes));  // LL granules: zero = epoch 0, never matches a live call
+  c->ll_bytes = (size_t)(2 * kLLMaxBytes) * c->nranks;
+  if (c->ll_bytes * 2 > c->half_bytes) c->ll_bytes = 0;
+  // each parity half: [op-program staging | amax granules (fp8 wire) | LL granules]
+  c->exec_half = c->half_bytes - c->ll_bytes - kAmaxRegion;
+  FX_HIP(hipExtMallocWithFlags((void**)&c->flags, kFlagWords * sizeof(uint64_t), hipDeviceMallocUncached));
+  FX_HIP(hipMemset(c->flags, 0, kFlagWords * sizeof(uint64_t)));
+  FX_HIP(hipMalloc(&c->epochs, kMaxGridBlocks * sizeof(uint64_t)));
+  FX_HIP(hipMemset(c->epochs, 0, kMaxGridBlocks * sizeof(uint64_t)));
+  FX_HIP(hipHostMalloc((void**)&c->err_host, 64, hipHostMallocMapped));
+  memset(c->err_host, 0, 64);
+  FX_HIP(hipHostGetDevicePointer((void**)&c->err_dev, c->err_host, 0));
+  FX_HIP(hipDeviceSynchronize());
+  return 0;
+}
+
+void init_defaults(flexar_comm* c) {
+  c->model = XgmiModel::from_env();
+  if (const char* m = getenv("FLEXAR_MODEL")) c->links_from_env = std::count(m, m + strlen(m), ',') >= 4;
+  c->have_tune = c->tune.load(getenv("FLEXAR_TUNE_FILE"));
+  c->timeout_ticks = env_u64("FLEXAR_TIMEOUT_MS", 20000) * 100000ull;  // 100 MHz s_memrealtime
+  c->zc_auto = env_u64("FLEXAR_ZC_AUTO", 1) != 0;
+  c->max_grid = (int)env_u64("FLEXAR_MAX_GRID", 256);
+  if (c->max_grid < 1) c->max_grid = 1;
+  if (c->max_grid > (int)kMaxGridBlocks) c->max_grid = kMaxGridBlocks;
+  c->min_block_bytes = env_u64("FLEXAR_MIN_BLOCK_BYTES", 32 * 1024);
+  c->chunk_bytes = env_u64("FLEXAR_CHUNK_BYTES", 0);
+  c->nchannels = (int)env_u64("FLEXAR_NCHANNELS", 0);
+  c->profile = env_u64("FLEXAR_PROFILE", 0) != 0;
+  c->unordered = env_u64("FLEXAR_UNORDERED_CALLS", 0) != 0;
+  if (!c->min_block_bytes) c->min_block_bytes = 1;
+  // FLEXAR_FAULT_INJECT=delay:RANK:SLOT:MICROSECONDS | drop:RANK:SLOT  (tests / race hunting)
+  if (const char* fi = getenv("FLEXAR_FAULT_INJECT")) {
+    char kind[16] = {0};
+    int rk = -1, slot = 0;
+    double us = 0;
+    if (sscanf(fi, "%15[a-z]:%d:%d:%lf", kind, &rk, &slot, &us) >= 3 && rk == c->rank) {
+      c->fi_kind = strcmp(kind, "drop") == 0 ? 2 : 1;
+      c->fi_slot = (uint32_t)slot;
+      c->fi_ticks = (uint64_t)(us * 100.0);  // 100 MHz s_memrealtime
+    }
+  }
+  const char* a = getenv("FLEXAR_ALGO");
+  std::string err;
+  if (a && *a && strcmp(a, "rccl") != 0) {  // "rccl" is routed by the Python layer / c10d backend
+    if (!parse_algo(a, c->nranks, &c->spec, &err)) logf(LOG_WARN, c->rank, "ignoring FLEXAR_ALGO: %s", err.c_str());
+    if (c->spec.kind == AlgoKind::RING && c->nchannels > 1 && !strchr(a, ':')) c->spec.channels = c->nchannels;
+  } else if (getenv("FT_TOPO")) {  // reference compatibility: FT_TOPO selects the algorithm
+    if (!parse_ft_topo(getenv("FT_TOPO"), c->nranks, &c->spec, &err))
+      logf(LOG_WARN, c->rank, "ignoring FT_TOPO: %s", err.c_str());
+  }
+}
+
+}  // namespace flexar
+
+extern "C" {
+
+int flexar_comm_create(int rank, int nranks, int device, size_t workspace_bytes, flexar_comm_t* out) {
+  if (!out || nranks < 1 || nranks > (int)kMaxRanks || rank < 0 || rank >= nranks) {
+    set_error("invalid rank/nranks (nranks must be 1..16)");
+    return FLEXAR_ERR_INVALID;
+  }
+  std::unique_ptr<flexar_comm> c(new flexar_comm);
+  c->rank = rank;
+  c->nranks = nranks;
+  c->device = device;
+  init_defaults(c.get());
+  size_t ws = workspace_bytes ? workspace_bytes : env_u64("FLEXAR_WORKSPACE_BYTES", 512ull << 20);
+  int rc = alloc_workspace(c.get(), ws);
+  if (rc) return rc;
+  c->resident = resident_blocks(device);
+  c->peer_stg[rank] = c->stg;
+  c->peer_flags[rank] = c->flags;
+  if (nranks == 1) c->connected = true;
+  *out = c.release();
+  return 0;
+}
+
+size_t flexar_handle_size(void) { return sizeof(CommHandle); }
+
+int flexar_comm_export(flexar_comm_t c, void* handle_out) {
+  if (!c || !handle_out) { set_error("null argument"); return FLEXAR_ERR_INVALID; }
+  FX_HIP(hipSetDevice(c->device));
+  CommHandle h;
+  memset(&h, 0, sizeof(h));
+  h.magic = kHandleMagic;
+  h.version = FLEXAR_VERSION_MAJOR * 100 + FLEXAR_VERSION_MINOR;
+  h.rank = c->rank;
+  h.nranks = c->nranks;
+  h.ws_bytes = c->ws_bytes;
+  FX_HIP(hipIpcGetMemHandle(&h.stg, c->stg));
+  FX_HIP(hipIpcGetMemHandle(&h.flags, c->flags));
+  h.pid = (int32_t)getpid();
+  h.device = c->device;
+  gethostname(h.host, sizeof(h.host) - 1);
+  if (hipDeviceGetPCIBusId(h.bus, sizeof(h.bus) - 1, c->device) != hipSuccess) {
+    (void)hipGetLastError();
+    snprintf(h.bus, sizeof(h.bus), "dev%d", c->device);
+  }
+  h.fingerprint = comm_fingerprint(c);
+  memcpy(handle_out, &h, sizeof(h));
+  return 0;
+}
+
+// Readiness gate (readiness.hpp), before any peer memory is mapped: every handle comes from this host,
+// the same library version and the same settings; every peer GPU that this process can see is
+// reachable peer-to-peer (hipDeviceCanAccessPeer) and its link class / hop count is recorded
+// (hipExtGetLinkTypeAndHopCount) and feeds the cost model's concurrent-link count. A failure names
+// the rank and the reason instead of surfacing as a raw hipIpcOpenMemHandle error or a device hang.
+int flexar_comm_connect(flexar_comm_t c, const void* all) {
+  if (!c || !all) { set_error("null argument"); return FLEXAR_ERR_INVALID; }
+  FX_HIP(hipSetDevice(c->device));
+  const CommHandle* hs = (const CommHandle*)all;
+  const CommHandle& me = hs[c->rank];
+  for (int r = 0; r < c->nranks; ++r) {
+    const CommHandle& h = hs[r];
+    const std::string who = "rank " + std::to_string(r);
+    if (h.magic != kHandleMagic || h.rank != r || h.nranks != c->nranks) {
+      set_error("bad handle from " + who + " (mismatched ranks or version)");
+      return FLEXAR_ERR_INVALID;
+    }
+    if (h.version != me.version) {
+      set_error(who + " runs another flexar version (" + std::to_string(h.version) + " vs " +
+                std::to_string(me.version) + ")");
+      return FLEXAR_ERR_INVALID;
+    }
+    if (h.ws_bytes != c->ws_bytes) {
+      set_error("workspace size differs across ranks (" + who + ": " + std::to_string(h.ws_bytes) + " B, rank " +
+                std::to_string(c->rank) + ": " + std::to_string(c->ws_bytes) + " B)");
+      return FLEXAR_ERR_INVALID;
+    }
+    if (strncmp(h.host, me.host, sizeof(h.host)) != 0) {
+      set_error(who + " is on host '" + std::string(h.host) + "', rank " + std::to_string(c->rank) + " on '" +
+                std::string(me.host) + "': the device transport is intra-node (IPC over xGMI); use the "
+                "hierarchical allreduce or RCCL across nodes");
+      return FLEXAR_ERR_UNSUPPORTED;
+    }
+    if (h.fingerprint != me.fingerprint) {
+      std::string vars;
+      for (const char* const* v = fingerprint_vars(); *v; ++v) vars += std::string(vars.empty() ? "" : ", ") + *v;
+      set_error(who + " resolves calls with different settings than rank " + std::to_string(c->rank) +
+                " (one of " + vars + " or the tune table differs): every rank must pick the same schedule");
+      return FLEXAR_ERR_INVALID;
+    }
+    memcpy(c->peer_bus[r], h.bus, sizeof(c->peer_bus[r]));
+    c->peer_bus[r][sizeof(c->peer_bus[r]) - 1] = 0;
+    c->peer_dev[r] = -1;
+    if (r == c->rank) {
+      c->peer_dev[r] = c->device;
+      c->link_cls[r] = LINK_SAME;
+      continue;
+    }
+    int pd = -1;
+    if (hipDeviceGetByPCIBusId(&pd, c->peer_bus[r]) != hipSuccess) {
+      (void)hipGetLastError();
+      pd = -1;
+    }
+    c->peer_dev[r] = pd;
+    if (pd < 0) {
+      c->link_cls[r] = LINK_UNKNOWN;  // not visible here (HIP_VISIBLE_DEVICES): IPC still maps it
+    } else if (pd == c->device) {
+      c->link_cls[r] = LINK_SAME;
+    } else {
+      int can = 0;
+      FX_HIP(hipDeviceCanAccessPeer(&can, c->device, pd));
+      if (!can) {
+        set_error("GPU " + std::to_string(c->device) + " (" + me.bus + ") cannot access GPU " + std::to_string(pd) +
+                  " (" + c->peer_bus[r] + ") of " + who + " peer-to-peer: no xGMI/PCIe P2P path");
+        return FLEXAR_ERR_UNSUPPORTED;
+      }
+      uint32_t lt = 0, hops = 0;
+      if (hipExtGetLinkTypeAndHopCount(c->device, pd, &lt, &hops) == hipSuccess) {
+        c->link_cls[r] = link_class_of_hsa(lt);
+        c->link_hops[r] = (int32_t)hops;
+      } else {
+        (void)hipGetLastError();
+        c->link_cls[r] = LINK_OTHER;
+      }
+    }
+  }
+  const bool no_ipc = env_u64("FLEXAR_FAULT_NO_IPC", 0) != 0;  // tests: behave as if mapping were impossible
+  for (int r = 0; r < c->nranks; ++r) {
+    if (r == c->rank) continue;
+    const CommHandle& h = hs[r];
+    void* p = nullptr;
+    hipError_t e = no_ipc ? hipErrorInvalidValue : hipIpcOpenMemHandle(&p, h.stg, hipIpcMemLazyEnablePeerAccess);
+    if (e == hipSuccess) {
+      c->peer_stg[r] = (char*)p;
+      e = hipIpcOpenMemHandle(&p, h.flags, hipIpcMemLazyEnablePeerAccess);
+      if (e != hipSuccess) (void)hipIpcCloseMemHandle(c->peer_stg[r]);
+    }
+    if (e != hipSuccess) {
+      (void)hipGetLastError();  // the caller may fall back to the message transport: clear the sticky error
+      set_error("mapping the workspace of rank " + std::to_string(r) + " (" + link_name(c->link_cls[r]) + " peer " +
+                c->peer_bus[r] + ") failed: hipIpcOpenMemHandle: " + hipGetErrorString(e) +
+                " (HSA_ENABLE_IPC_MODE_LEGACY=0 is needed on dmabuf-only drivers)");
+      return FLEXAR_ERR_HIP;
+    }
+    c->peer_flags[r] = (uint64_t*)p;
+    c->opened[r] = true;
+  }
+  if (!c->links_from_env) c->model.links = direct_links(c->link_cls, c->link_hops, c->nranks, c->rank);
+  c->memo_gen++;
+  c->connected = true;
+  return 0;
+}
+
+// Connect-time exact self-test (collective: every rank calls it after connect, in the same order).
+// Each protocol family runs three allreduces of an integer pattern whose sum every rank can compute
+// locally; the patterns change per call, so a read of a staging line left over from either of the two
+// previous calls (the parity halves) is a mismatch. Waits use a short watchdog, so a family whose
+// hand-off never becomes visible fails in seconds instead of hanging. Returns the mask of families
+// that failed ON THIS RANK; the caller ORs the masks of all ranks and installs the result with
+// flexar_comm_set_disabled (a family is usable only if it passed everywhere).
+int flexar_comm_selftest(flexar_comm_t c, uint32_t families, uint32_t* failed_out) {
+  if (!c || !failed_out) { set_error("null argument"); return FLEXAR_ERR_INVALID; }
+  if (!c->connected) { set_error("communicator not connected"); return FLEXAR_ERR_STATE; }
+  *failed_out = 0;
+  if (c->nranks == 1) return 0;
+  FX_HIP(hipSetDevice(c->device));
+  const uint64_t n = 65536 + 77;  // 256 KiB + an odd tail: several workgroups, a scalar tail, LL-sized
+  if (!c->st_buf) {
+    FX_HIP(hipMalloc(&c->st_buf, 2 * n * sizeof(int)));
+    FX_HIP(hipHostMalloc((void**)&c->st_bad, 64, hipHostMallocMapped));
+    FX_HIP(hipHostGetDevicePointer((void**)&c->st_bad_dev, c->st_bad, 0));
+  }
+  hipStream_t st = nullptr;
+  FX_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  const uint64_t saved_timeout = c->timeout_ticks, saved_gen = c->memo_gen;
+  const uint32_t saved_disabled = c->disabled;
+  const bool saved_profile = c->profile;
+  const uint64_t saved_calls = c->calls, saved_bytes = c->bytes;
+  c->disabled = 0;  // the self-test drives each family explicitly
+  c->profile = false;  // and stays out of the application's statistics
+  c->timeout_ticks = env_u64("FLEXAR_SELFTEST_TIMEOUT_MS", 2000) * 100000ull;
+  struct Case { uint32_t fam; const char* spec; };
+  const Case cases[] = {{PF_FENCE, "flat+pull"}, {PF_FENCE, "ring"}, {PF_WT, "flat+pull+wt"}, {PF_LL, "ll"},
+                        {PF_DMA, "dma"}, {PF_MSG, "flat+rccl"}, {PF_MSG, "ring+rccl"}};
+  if (!c->nccl) families &= ~(uint32_t)PF_MSG;
+  if (!c->ipc) {  // no peer memory on this communicator: only the message transport exists
+    families &= PF_MSG;
+    *failed_out |= PF_ALL;
+  }
+  int* in = c->st_buf;
+  int* out = c->st_buf + n;
+  const int N = c->nranks;
+  int rc = 0;
+  for (const Case& k : cases) {
+    if (!(families & k.fam)) continue;
+    if (k.fam == PF_LL && !ll_usable(c, n, 4)) continue;
+    c->selftested |= k.fam;
+    logf(LOG_INFO, c->rank, "self-test: %s", k.spec);
+    for (int call = 0; call < 3 && !rc; ++call) {
+      const uint32_t salt = (uint32_t)(call * 131 + k.fam * 17);
+      hipLaunchKernelGGL(selftest_fill, dim3(64), dim3(256), 0, st, in, out, n, c->rank, salt);
+      if ((rc = hipGetLastError() != hipSuccess ? FLEXAR_ERR_HIP : 0)) break;
+      int e = flexar_allreduce_ex(c, in, out, n, FLEXAR_INT32, FLEXAR_SUM, st, k.spec, 1.0f);
+      if (e == FLEXAR_ERR_TIMEOUT || e == FLEXAR_ERR_STATE) {
+        *failed_out |= k.fam;  // a previous call of this family timed out
+      } else if (e) {
+        rc = e;
+        break;
+      }
+      *c->st_bad = 0;
+      hipLaunchKernelGGL(selftest_check, dim3(64), dim3(256), 0, st, out, n, N, salt, c->st_bad_dev);
+      if (hipStreamSynchronize(st) != hipSuccess) { rc = FLEXAR_ERR_HIP; break; }
+      if (__atomic_load_n(c->st_bad, __ATOMIC_ACQUIRE) != 0) *failed_out |= k.fam;
+      if (__atomic_load_n(c->err_host, __ATOMIC_ACQUIRE) != 0) {
+        *failed_out |= k.fam;
+        __atomic_store_n(c->err_host, 0u, __ATOMIC_RELEASE);  // every rank still makes every call
+      }
+    }
+    if (rc) break;
+  }
+  (void)hipStreamSynchronize(st);
+  (void)hipStreamDestroy(st);
+  c->have_last = false;  // `st` is gone (and synchronised): the next call must not order behind it
+  c->timeout_ticks = saved_timeout;
+  c->disabled = saved_disabled;
+  c->profile = saved_profile;
+  c->calls = saved_calls;
+  c->bytes = saved_bytes;
+  c->memo_gen = saved_gen + 1;
+  if (rc == FLEXAR_ERR_HIP && std::string(flexar_last_error()).empty()) set_error("self-test: HIP error");
+  logf(*failed_out ? LOG_WARN : LOG_INFO, c->rank, "self-test: ran %s, failed on this rank: %s",
+       family_names(c->selftested).c_str(), family_names(*failed_out).c_str());
+  return rc;
+}
+
+// Cost-model time (us) of `spec` on this communicator's model (links from the connect-time probe).
+double flexar_comm_predict_us(flexar_comm_t c, const char* spec, double bytes) {
+  if (!c) return -1.0;
+  AlgoSpec s;
+  std::string err;
+  if (!parse_algo(spec ? spec : "auto", c->nranks, &s, &err)) { set_error(err); return -1.0; }
+  if (s.kind == AlgoKind::AUTO) s = select_plan(c->model, c->nranks, bytes);
+  return c->model.cost_us(s, c->nranks, bytes);
+}
+
+int flexar_rccl_available(void) { return rccl().ok ? 1 : 0; }
+
+int flexar_rccl_unique_id(void* out, size_t len) {
+  if (!out || len < sizeof(ncclUniqueId)) { set_error("unique id buffer too small (128 bytes)"); return FLEXAR_ERR_INVALID; }
+  if (!rccl().ok) { set_error("RCCL not found (librccl.so)"); return FLEXAR_ERR_UNSUPPORTED; }
+  ncclUniqueId id;
+  int rc = rccl_check(rccl().GetUniqueId(&id), "ncclGetUniqueId");
+  if (rc) return rc;
+  memcpy(out, &id, sizeof(id));
+  return 0;
+}
+
+// Collective: every rank passes rank 0's unique id; creates the RCCL communicator of the message
+// transport ("+rccl" specs, and every call when the communicator has no IPC mapping).
+int flexar_comm_init_msg(flexar_comm_t c, const void* unique_id) {
+  if (!c || !unique_id) { set_error("null argument"); return FLEXAR_ERR_INVALID; }
+  if (!rccl().ok) { set_error("RCCL not found (librccl.so)"); return FLEXAR_ERR_UNSUPPORTED; }
+  if (c->nccl) return 0;
+  FX_HIP(hipSetDevice(c->device));
+  ncclUniqueId id;
+  memcpy(&id, unique_id, sizeof(id));
+  int rc = rccl_check(rccl().CommInitRank(&c->nccl, c->nranks, id, c->rank), "ncclCommInitRank");
+  if (rc) c->nccl = nullptr;
+  c->memo_gen++;
+  return rc;
+}
+
+// After a failed flexar_comm_connect on some rank (no usable IPC mapping): run every call over the
+// message transport instead (flexar_comm_init_msg first). Collective in effect.
+int flexar_comm_connect_msg_only(flexar_comm_t c) {
+  if (!c) return FLEXAR_ERR_INVALID;
+  if (!c->nccl) { set_error("message transport not initialised"); return FLEXAR_ERR_STATE; }
+  c->ipc = false;
+  c->connected = true;
+  c->memo_gen++;
+  return 0;
+}
+
+int flexar_comm_set_model(flexar_comm_t c, double alpha_launch_us, double alpha_sync_us, double link_gbps,
+                          double hbm_gbps, int links) {
+  if (!c || !(link_gbps > 0) || !(hbm_gbps > 0) || alpha_launch_us < 0 || alpha_sync_us < 0) {
+    set_error("cost model: positive bandwidths and non-negative latencies required");
+    return FLEXAR_ERR_INVALID;
+  }
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->model.alpha_launch_us = alpha_launch_us;
+  c->model.alpha_sync_us = alpha_sync_us;
+  c->model.link_gbps = link_gbps;
+  c->model.hbm_gbps = hbm_gbps;
+  if (links > 0) c->model.links = links;
+  c->memo_gen++;
+  return 0;
+}
+
+int flexar_comm_set_disabled(flexar_comm_t c, uint32_t families) {
+  if (!c) return FLEXAR_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->disabled = families & PF_ALL;
+  c->memo_gen++;
+  return 0;
+}
+
+uint32_t flexar_comm_disabled(flexar_comm_t c) { return c ? c->disabled : 0; }
+
+// JSON: the topology probe's view of every peer and the readiness state.
+int flexar_comm_topology(flexar_comm_t c, char* buf, size_t buflen) {
+  if (!c || !buf) return FLEXAR_ERR_INVALID;
+  std::string j = "{\"rank\": " + std::to_string(c->rank) + ", \"device\": " + std::to_string(c->device) +
+                  ", \"links\": " + std::to_string(c->model.links) + ", \"resident_blocks\": " +
+                  std::to_string(c->resident) + ", \"selftested\": \"" + family_names(c->selftested) +
+                  "\", \"disabled\": \"" + (c->disabled ? family_names(c->disabled) : std::string()) +
+                  "\", \"ipc\": " + (c->ipc ? "true" : "false") + ", \"rccl\": " + (c->nccl ? "true" : "false") +
+                  ", \"peers\": [";
+  for (int r = 0; r < c->nranks; ++r) {
+    char t[256];
+    snprintf(t, sizeof(t), "%s{\"rank\": %d, \"bus\": \"%s\", \"device\": %d, \"link\": \"%s\", \"hops\": %d}",
+             r ? ", " : "", r, c->peer_bus[r], c->peer_dev[r], r == c->rank ? "self" : link_name(c->link_cls[r]),
+             c->link_hops[r]);
+    j += t;
+  }
+  j += "]}";
+  snprintf(buf, buflen, "%s", j.c_str());
+  return j.size() < buflen ? 0 : FLEXAR_ERR_NOMEM;
+}
+
+int flexar_comm_destroy(flexar_comm_t c) {
+  if (!c) return 0;
+  (void)hipSetDevice(c->device);
+  (void)hipDeviceSynchronize();
+  // teardown keeps going past failures; FLEXAR_LOG_LEVEL=info names them
+  auto ipc_close = [&](void* p, const char* what, int r) {
+    const hipError_t e = hipIpcCloseMemHandle(p);
+    if (e != hipSuccess)
+      logf(LOG_INFO, c->rank, "destroy: hipIpcCloseMemHandle(%s of rank %d, %p): %s", what, r, p, hipGetErrorString(e));
+  };
+  for (auto& kv : c->cache) {
+    (void)hipFree(kv.second->d_ops);
+    (void)hipFree(kv.second->d_chan);
+  }
+  for (int r = 0; r < c->nranks; ++r)
+    if (c->opened[r]) {
+      ipc_close(c->peer_stg[r], "workspace", r);
+      ipc_close(c->peer_flags[r], "flags", r);
+    }
+  for (auto& kv : c->ipc_maps) ipc_close(kv.second.first, "registration", -1);
+  c->ipc_maps.clear();
+  c->regs.clear();
+  for (int r = 0; r < kMaxRanks; ++r) {
+    if (c->dma_st[r]) (void)hipStreamDestroy(c->dma_st[r]);
+    if (c->dma_ag[r]) (void)hipStreamDestroy(c->dma_ag[r]);
+    if (c->dma_join[r]) (void)hipEventDestroy(c->dma_join[r]);
+    if (c->dma_rs_end[r]) (void)hipEventDestroy(c->dma_rs_end[r]);
+    for (int k = 0; k < 2; ++k)
+      if (c->dma_ag_done[r][k]) (void)hipEventDestroy(c->dma_ag_done[r][k]);
+  }
+  if (c->dma_fork) (void)hipEventDestroy(c->dma_fork);
+  if (c->order_ev) (void)hipEventDestroy(c->order_ev);
+  for (auto& kv : c->msg_cache) {
+    for (Op* p : kv.second->d_ops) (void)hipFree(p);
+    for (uint32_t* p : kv.second->d_chan) (void)hipFree(p);
+  }
+  if (c->msg_ws) (void)hipFree(c->msg_ws);
+  if (c->nccl && rccl().ok) (void)rccl().CommDestroy(c->nccl);
+  if (c->st_buf) (void)hipFree(c->st_buf);
+  if (c->st_bad) (void)hipHostFree(c->st_bad);
+  (void)hipFree(c->stg);
+  (void)hipFree(c->flags);
+  (void)hipFree(c->epochs);
+  (void)hipHostFree(c->err_host);
+  delete c;
+  // teardown ignores failures (e.g. closing a mapping a peer already released), but HIP keeps the last one
+  // as the thread's sticky error, and the caller's framework would report it at its next kernel launch
+  (void)hipGetLastError();
+  return 0;
+}
+
+int flexar_comm_rank(flexar_comm_t c) { return c ? c->rank : -1; }
+int flexar_comm_size(flexar_comm_t c) { return c ? c->nranks : -1; }
+
+int flexar_comm_set_tune_table(flexar_comm_t c, const char* text) {
+  if (!c) return FLEXAR_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  TuneTable t;
+  if (text && *text) {
+    if (!t.load_text(text)) { set_error("tune table: no 'nranks bytes spec' lines"); return FLEXAR_ERR_INVALID; }
+    for (auto& n : t.rows)
+      for (auto& row : n.second) {
+        AlgoSpec s;
+        std::string err;
+        if (!parse_algo(row.second, c->nranks, &s, &err)) { set_error("tune table: " + err); return FLEXAR_ERR_INVALID; }
+      }
+  }
+  c->tune = t;
+  c->have_tune = !t.rows.empty();
+  c->memo_gen++;
+  return 0;
+}
+
+int flexar_comm_set_algo(flexar_comm_t c, const char* spec) {
+  if (!c) return FLEXAR_ERR_INVALID;
+  std::string err;
+  AlgoSpec s;
+  if (!parse_algo(spec ? spec : "auto", c->nranks, &s, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->spec = s;
+  c->memo_gen++;
+  return 0;
+}
+
+int flexar_comm_set_grid(flexar_comm_t c, int grid_blocks, int block_threads) {
+  if (!c) return FLEXAR_ERR_INVALID;
+  (void)block_threads;
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->grid_override = grid_blocks < 0 ? 0 : grid_blocks;
+  c->memo_gen++;
+  return 0;
+}
+
+// After every rank has synchronised (no kernel of this communicator in flight anywhere), forget a
+// recorded watchdog timeout: epochs advance once per call on every rank even when a call aborts, and
+// flags only ever grow, so the next call starts from a consistent state (the autotuner's recovery).
+int flexar_comm_clear_error(flexar_comm_t c) {
+  if (!c) return FLEXAR_ERR_INVALID;
+  FX_HIP(hipSetDevice(c->device));
+  FX_HIP(hipDeviceSynchronize());
+  __atomic_store_n(c->err_host, 0u, __ATOMIC_RELEASE);
+  return 0;
+}
+
+}  // extern "C"
