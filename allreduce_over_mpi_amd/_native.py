@@ -112,6 +112,20 @@ def _sig(lib):
         "flexar_kernel_info": (i, [i, i, i, i, c.POINTER(i), c.POINTER(i)]),
         "flexar_downgrade_spec": (i, [cp, i, u32, i, cp, sz]),
         "flexar_direct_links": (i, [c.POINTER(c.c_int32), c.POINTER(c.c_int32), i, i]),
+        "flexar_probe_blob_size": (sz, []),
+        "flexar_probe_agree": (i, [vp, i, c.POINTER(i)]),
+        "flexar_comm_probe_export": (i, [vp, vp]),
+        "flexar_comm_probe_agree": (i, [vp, vp]),
+        "flexar_comm_calibrate": (i, [vp, i, cp, sz]),
+        "flexar_comm_calibration": (i, [vp, cp, sz]),
+        "flexar_comm_reset_model": (i, [vp]),
+        "flexar_comm_model_hash": (u64, [vp]),
+        "flexar_calib_fit": (i, [i, cp, c.POINTER(d), c.POINTER(d), i, i, i, c.POINTER(d)]),
+        "flexar_calib_key": (i, [cp, i, i, cp, u32, cp, sz]),
+        "flexar_calib_path": (i, [cp, cp, sz]),
+        "flexar_calib_load": (i, [cp, cp, c.POINTER(d)]),
+        "flexar_calib_store": (i, [cp, cp, c.POINTER(d), i, cp, c.POINTER(d), c.POINTER(d)]),
+        "flexar_calib_points": (i, [i, cp, sz]),
     }
     for name, (res, args) in table.items():
         fn = getattr(lib, name)
@@ -281,6 +295,54 @@ def apply_partials(spec: str, nranks: int, nbytes: float, dtype="bfloat16", op="
     check(lib().flexar_apply_partials(spec.encode(), nranks, float(nbytes), dtype_code(dtype), op_code(op), b, 256),
           "apply_partials")
     return b.value.decode()
+
+
+def _rows_args(rows):
+    n = len(rows)
+    specs = "\n".join(r["spec"] for r in rows).encode()
+    b = (ctypes.c_double * max(1, n))(*[float(r["bytes"]) for r in rows])
+    u = (ctypes.c_double * max(1, n))(*[float(r["us"]) for r in rows])
+    return n, specs, b, u
+
+
+def calib_fit(rows, nranks: int, links: int = 0, esize: int = 4) -> dict:
+    """The native least-squares fit of the connect-time calibration (calibration.hpp fit_theta) on rows
+    ({"spec", "bytes", "us"})."""
+    out = (ctypes.c_double * 7)()
+    n, specs, b, u = _rows_args(rows)
+    check(lib().flexar_calib_fit(n, specs, b, u, nranks, int(links), int(esize), out), "calib_fit")
+    keys = ("alpha_launch_us", "alpha_sync_us", "link_gbps", "hbm_gbps", "median_rel_err", "max_rel_err", "rows")
+    return dict(zip(keys, list(out)))
+
+
+def calib_key(arch: str, nranks: int, links: int, classes: str = "", disabled: int = 0) -> str:
+    b = _strbuf(1024)
+    check(lib().flexar_calib_key(arch.encode(), nranks, links, classes.encode(), disabled, b, 1024), "calib_key")
+    return b.value.decode()
+
+
+def calib_path(key: str) -> str:
+    b = _strbuf(4096)
+    check(lib().flexar_calib_path(key.encode(), b, 4096), "calib_path")
+    return b.value.decode()
+
+
+def calib_load(path: str, key: str):
+    """theta (alpha_launch_us, alpha_sync_us, 1/link_gbps, 1/hbm_gbps) from the cache file, or None."""
+    t = (ctypes.c_double * 4)()
+    return list(t) if lib().flexar_calib_load(path.encode(), key.encode(), t) == 1 else None
+
+
+def calib_store(path: str, key: str, theta, rows=()):
+    t = (ctypes.c_double * 4)(*[float(x) for x in theta])
+    n, specs, b, u = _rows_args(list(rows))
+    check(lib().flexar_calib_store(path.encode(), key.encode(), t, n, specs, b, u), "calib_store")
+
+
+def calib_points(nranks: int) -> list:
+    b = _strbuf(4096)
+    check(lib().flexar_calib_points(nranks, b, 4096), "calib_points")
+    return [(ln.split()[0], int(ln.split()[1])) for ln in b.value.decode().splitlines() if ln.strip()]
 
 
 def legacy_cost(widths, nranks: int, chunk: float) -> float:

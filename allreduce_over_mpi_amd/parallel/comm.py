@@ -118,6 +118,7 @@ class Communicator:
         self._h = h
         self._hi = int(h.value or 0)  # the handle as an int, for the fast-call path
         self.selftest_failed = []
+        self.calibration = None
         self.transport_note = None
         self._exchange = None
         self._regs = {}
@@ -156,7 +157,9 @@ class Communicator:
                     nv.check(self._lib.flexar_comm_connect_msg_only(self._h), "connect_msg_only")
                     self.transport_note = "IPC unavailable (" + "; ".join(b.split(":", 1)[1] for b in bad) + \
                                           "): every call runs over the RCCL message transport"
+            self._agree_probe(exchange)
             self._readiness(exchange)
+            self._calibrate(exchange)
         self._rccl_default = False
         self._rccl_group = None
         env_algo = os.environ.get("FLEXAR_ALGO", "")
@@ -176,6 +179,46 @@ class Communicator:
         if bad:
             self.close()
             raise nv.FlexarError(7, "message transport: " + "; ".join(bad))
+
+    def _agree_probe(self, exchange):
+        """Probe agreement (flexar_comm_probe_agree): every rank's link classes / link count / settings
+        fingerprint are exchanged; the minimum link count is installed everywhere and a real disagreement
+        (asymmetric link classes, different settings) fails on every rank with a message naming the ranks,
+        instead of as a device watchdog timeout in the first collective."""
+        blob = ctypes.create_string_buffer(int(self._lib.flexar_probe_blob_size()))
+        nv.check(self._lib.flexar_comm_probe_export(self._h, blob), "probe_export")
+        rc = self._lib.flexar_comm_probe_agree(self._h, b"".join(exchange(bytes(blob.raw))))
+        if rc:  # deterministic on identical inputs: every rank fails the same way
+            err = nv.last_error()
+            self.close()
+            raise nv.FlexarError(rc, "comm_connect: " + err)
+
+    def _calibrate(self, exchange):
+        """Connect-time calibration of the cost model (flexar_comm_calibrate; FLEXAR_CALIB = 0 | 1 (default:
+        the cached constants of this node shape, else measure) | force): a few executor schedules timed on
+        the real links, max over ranks, fitted and installed identically on every rank. If the ranks end up
+        with different models (a rank failed mid-way), every rank falls back to the default model."""
+        import json
+
+        self.calibration = None
+        mode = {"0": 0, "off": 0, "1": 1, "force": 2, "2": 2}.get(os.environ.get("FLEXAR_CALIB", "1"), 1)
+        exchange(b"")  # start together: a rank still finishing the self-test must not trip the short watchdog
+        buf = ctypes.create_string_buffer(1 << 14)
+        rc = self._lib.flexar_comm_calibrate(self._h, mode, buf, 1 << 14)
+        err = nv.last_error() if rc else ""
+        h = int(self._lib.flexar_comm_model_hash(self._h)) if rc == 0 else 0
+        rows = exchange(f"{rc}:{h}".encode())
+        if len(set(rows)) != 1 or rc:
+            nv.check(self._lib.flexar_comm_clear_error(self._h), "clear_error")
+            nv.check(self._lib.flexar_comm_reset_model(self._h), "reset_model")
+            self.calibration = {"source": "disagreed", "error": err or None,
+                                "ranks": [r.decode(errors="replace") for r in rows]}
+            exchange(b"")
+            return
+        try:
+            self.calibration = json.loads(buf.value.decode() or "{}")
+        except ValueError:
+            self.calibration = {"source": "unparsed", "raw": buf.value.decode(errors="replace")}
 
     def _readiness(self, exchange):
         """Connect-time self-test (flexar_comm_selftest): every protocol family runs exact integer

@@ -191,6 +191,20 @@ double flexar_comm_predict_us(flexar_comm_t comm, const char* spec, double bytes
  * the connect-time probe unless links > 0). Collective in effect: every rank must install the same. */
 int flexar_comm_set_model(flexar_comm_t comm, double alpha_launch_us, double alpha_sync_us, double link_gbps,
                           double hbm_gbps, int links);
+/* Probe agreement (collective in effect, after connect): every rank exports its topology-probe summary
+ * (flexar_probe_blob_size() bytes), the application all-gathers them, every rank agrees: the minimum link
+ * count is installed everywhere, asymmetric link classes or settings fail with a message naming the ranks. */
+size_t flexar_probe_blob_size(void);
+int flexar_comm_probe_export(flexar_comm_t comm, void* out);
+int flexar_comm_probe_agree(flexar_comm_t comm, const void* all_blobs);
+int flexar_probe_agree(const void* all_blobs, int nranks, int* links_out); /* host-only check of the blobs */
+/* Connect-time calibration (collective, after the self-test): mode 0 off, 1 cached-or-measure, 2 measure.
+ * Times fixed executor schedules, max over ranks, fits and installs the cost model; caches it on disk per
+ * (arch, N, links, link classes, disabled families, version). Writes a JSON report. */
+int flexar_comm_calibrate(flexar_comm_t comm, int mode, char* json, size_t jlen);
+int flexar_comm_calibration(flexar_comm_t comm, char* json, size_t jlen); /* the last report */
+int flexar_comm_reset_model(flexar_comm_t comm);   /* FLEXAR_MODEL / defaults, agreed links kept */
+uint64_t flexar_comm_model_hash(flexar_comm_t comm);
 /* JSON statistics (calls, bytes; per-algorithm device time when FLEXAR_PROFILE=1). */
 int flexar_comm_stats(flexar_comm_t comm, char* buf, size_t buflen);
 /* Describe the algorithm the communicator would run for (count, dtype). */
@@ -275,6 +289,18 @@ int flexar_select_plan(int nranks, double bytes, char* out, size_t outlen);
 int flexar_apply_partials(const char* spec, int nranks, double bytes, int dtype, int op, char* out, size_t outlen);
 /* Cost-model choice for a call of dtype / op (the typed form it runs included; FLEXAR_PARTIALS applies). */
 int flexar_select_plan_ex(int nranks, double bytes, int dtype, int op, int links, char* out, size_t outlen);
+/* Calibration helpers (calibration.hpp): fit theta to rows (specs newline-separated; out[7] = alpha_launch_us,
+ * alpha_sync_us, link_gbps, hbm_gbps, median / max relative error, rows used), the cache key / path / file,
+ * and the measurement set ("spec bytes" lines) of flexar_comm_calibrate. */
+int flexar_calib_fit(int nrows, const char* specs_nl, const double* bytes, const double* us, int nranks, int links,
+                     int esize, double* out);
+int flexar_calib_key(const char* arch, int nranks, int links, const char* classes, uint32_t disabled, char* out,
+                     size_t outlen);
+int flexar_calib_path(const char* key, char* out, size_t outlen);
+int flexar_calib_load(const char* path, const char* key, double* theta); /* 1 loaded, 0 miss */
+int flexar_calib_store(const char* path, const char* key, const double* theta, int nrows, const char* specs_nl,
+                       const double* bytes, const double* us);
+int flexar_calib_points(int nranks, char* out, size_t outlen);
 /* Reference cost model (cost_model/CostModel.h) score, fixed: returns the argmin spec and cost. */
 double flexar_legacy_cost(const char* widths_csv, int nranks, double chunk);
 /* Human-readable dump of rank's op program (like Operations::print_ops). */

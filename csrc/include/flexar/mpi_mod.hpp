@@ -461,6 +461,16 @@ inline flexar_comm_t device_comm(MPI_Comm comm) {
   if (!ok) fprintf(stderr, "[flexar] rank %d connect: %s\n", rank, flexar_last_error());
   MPI_Allreduce(&ok, &all_ok, 1, MPI_INT, MPI_MIN, comm);
   if (!all_ok) abort();
+  // probe agreement (readiness.hpp probe_agree): the minimum link count on every rank, or a named error
+  if (size > 1) {
+    std::vector<char> pb(flexar_probe_blob_size()), pall(pb.size() * size);
+    flexar_comm_probe_export(d->c, pb.data());
+    MPI_Allgather(pb.data(), (int)pb.size(), MPI_BYTE, pall.data(), (int)pb.size(), MPI_BYTE, comm);
+    if (flexar_comm_probe_agree(d->c, pall.data())) {
+      fprintf(stderr, "[flexar] rank %d: %s\n", rank, flexar_last_error());
+      abort();
+    }
+  }
   // connect-time self-test (readiness.hpp): a protocol family that failed on any rank is disabled on all
   if (size > 1 && !(getenv("FLEXAR_SELFTEST") && strcmp(getenv("FLEXAR_SELFTEST"), "0") == 0)) {
     // one family at a time behind a barrier, and a failed family once more before it is disabled (a rank
@@ -490,6 +500,23 @@ inline flexar_comm_t device_comm(MPI_Comm comm) {
       fprintf(stderr, "[flexar] rank %d: protocol families failing the self-test disabled: %s\n", rank,
               family_names(any).c_str());
       if (any == PF_ALL) abort();
+    }
+  }
+  // connect-time calibration of the cost model (FLEXAR_CALIB=0 | 1 | force; calibration.hpp): the cached
+  // constants of this node shape or a short measurement, identical on every rank; ranks whose models end
+  // up different all fall back to the default model
+  if (size > 1) {
+    const char* cm = getenv("FLEXAR_CALIB");
+    const int mode = !cm ? 1 : (!strcmp(cm, "0") || !strcmp(cm, "off")) ? 0 : !strcmp(cm, "force") ? 2 : 1;
+    MPI_Barrier(comm);
+    const int crc = flexar_comm_calibrate(d->c, mode, nullptr, 0);
+    unsigned long long h[2] = {crc ? 0ull : (unsigned long long)flexar_comm_model_hash(d->c), 0}, lo = 0, hi = 0;
+    h[1] = h[0];
+    MPI_Allreduce(&h[0], &lo, 1, MPI_UNSIGNED_LONG_LONG, MPI_MIN, comm);
+    MPI_Allreduce(&h[1], &hi, 1, MPI_UNSIGNED_LONG_LONG, MPI_MAX, comm);
+    if (lo != hi || lo == 0) {
+      flexar_comm_clear_error(d->c);
+      flexar_comm_reset_model(d->c);
     }
   }
   MPI_Barrier(comm);

@@ -14,6 +14,7 @@
 
 #include <stdint.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <string>
 
@@ -136,6 +137,60 @@ inline int direct_links(const int32_t* cls, const int32_t* hops, int n, int self
     if ((cls[p] == LINK_XGMI && hops[p] <= 1) || cls[p] == LINK_UNKNOWN) ++x;
   }
   return x < 1 ? 1 : x;
+}
+
+// ---- probe agreement ----------------------------------------------------------
+// The link count that prices schedules comes from each rank's OWN probe. The reference derives its
+// geometry from the communicator alone, identically on every rank (mpi_mod.hpp:216-243); here the probe
+// results are exchanged after connect and agreed on, so ranks cannot select different schedules (which
+// would surface as a device watchdog timeout in the first collective):
+//  * every rank installs the MINIMUM of the ranks' direct-link counts (a conservative, identical value);
+//  * the link classes must be symmetric - rank r's view of rank p equals p's view of r wherever both
+//    see each other (UNKNOWN = not visible in that process: no claim) - and a rank that sees a peer as
+//    the same device must be seen the same way; anything else is a real disagreement about the machine
+//    and connect fails with a message naming both ranks and both views;
+//  * the post-probe settings fingerprint must match (FLEXAR_MODEL fixing the link count included).
+struct ProbeBlob {
+  uint32_t magic;
+  int32_t rank;
+  int32_t links;          // this rank's direct_links()
+  int32_t links_fixed;    // FLEXAR_MODEL fixed the link count (the probe does not override it)
+  uint64_t fingerprint;   // settings fingerprint, recomputed after the probe
+  int8_t cls[16];         // link class of every peer as this rank sees it
+  int8_t hops[16];
+};
+constexpr uint32_t kProbeMagic = 0xF1E8B10Bu;
+
+// Returns true and the agreed link count, or false with a message naming the disagreement.
+inline bool probe_agree(const ProbeBlob* all, int nranks, int* links_out, std::string* why) {
+  int links = 1 << 30;
+  for (int r = 0; r < nranks; ++r) {
+    const ProbeBlob& a = all[r];
+    if (a.magic != kProbeMagic || a.rank != r) {
+      if (why) *why = "probe summary of rank " + std::to_string(r) + " is malformed";
+      return false;
+    }
+    if (a.fingerprint != all[0].fingerprint || a.links_fixed != all[0].links_fixed) {
+      if (why) *why = "rank " + std::to_string(r) + " resolves calls with different settings than rank 0 after the "
+                      "topology probe (FLEXAR_MODEL, FLEXAR_PARTIALS or another selector setting differs)";
+      return false;
+    }
+    links = std::min(links, (int)a.links);
+    for (int p = 0; p < nranks; ++p) {
+      if (p == r) continue;
+      const int8_t rp = a.cls[p], pr = all[p].cls[r];
+      if (rp == LINK_UNKNOWN || pr == LINK_UNKNOWN) continue;
+      if (rp != pr) {
+        if (why)
+          *why = "ranks disagree on the machine shape: rank " + std::to_string(r) + " sees rank " + std::to_string(p) +
+                 " over " + link_name(rp) + " but rank " + std::to_string(p) + " sees rank " + std::to_string(r) +
+                 " over " + link_name(pr);
+        return false;
+      }
+    }
+  }
+  if (links_out) *links_out = links < 1 ? 1 : links;
+  return true;
 }
 
 // ---- settings fingerprint ----------------------------------------------------------------------

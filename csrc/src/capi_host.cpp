@@ -12,6 +12,7 @@
 #include <thread>
 #include <vector>
 
+#include "flexar/calibration.hpp"
 #include "flexar/cost_model.hpp"
 #include "flexar/flexar.h"
 #include "flexar/host_exec.hpp"
@@ -525,6 +526,81 @@ int flexar_zc_decide(const char* spec, int nranks, double bytes, int flags, uint
   f.disabled = disabled;
   *decision = zc_decide(&s, f, XgmiModel::from_env());
   return copy_out(s.str(), out, outlen);
+}
+
+// Probe agreement on rank-major ProbeBlobs (readiness.hpp probe_agree), host-only: the agreed link count
+// in *links_out, or FLEXAR_ERR_INVALID with the disagreement in flexar_last_error().
+int flexar_probe_agree(const void* blobs, int nranks, int* links_out) {
+  if (!blobs || nranks < 1 || nranks > 16) { set_error("bad arguments"); return FLEXAR_ERR_INVALID; }
+  std::vector<ProbeBlob> v(nranks);
+  memcpy(v.data(), blobs, sizeof(ProbeBlob) * nranks);
+  std::string why;
+  if (!probe_agree(v.data(), nranks, links_out, &why)) { set_error(why); return FLEXAR_ERR_INVALID; }
+  return 0;
+}
+
+// ---- calibration helpers (calibration.hpp), host-only: the device measurement is flexar_comm_calibrate ----
+static std::vector<CalibRow> calib_rows(int nrows, const char* specs_nl, const double* bytes, const double* us) {
+  std::vector<CalibRow> rows;
+  std::istringstream ss(specs_nl ? specs_nl : "");
+  std::string spec;
+  for (int i = 0; i < nrows && std::getline(ss, spec); ++i) rows.push_back({spec, bytes[i], us[i]});
+  return rows;
+}
+
+// Fit theta to rows (specs newline-separated): out = {alpha_launch_us, alpha_sync_us, link_gbps, hbm_gbps,
+// median_rel_err, max_rel_err, rows used}. links <= 0: the default model's.
+int flexar_calib_fit(int nrows, const char* specs_nl, const double* bytes, const double* us, int nranks, int links,
+                     int esize, double* out) {
+  if (nrows < 0 || !out || nranks < 1 || (nrows && (!bytes || !us))) { set_error("bad arguments"); return FLEXAR_ERR_INVALID; }
+  XgmiModel m = XgmiModel::from_env();
+  if (links > 0) m.links = links;
+  const CalibFit f = fit_theta(calib_rows(nrows, specs_nl, bytes, us), m, nranks, (uint32_t)(esize > 0 ? esize : 4));
+  if (!f.ok) { set_error("calibration: fewer than 4 usable rows or no non-negative fit"); return FLEXAR_ERR_INVALID; }
+  const XgmiModel fm = model_with_theta(m, f.theta);
+  out[0] = fm.alpha_launch_us;
+  out[1] = fm.alpha_sync_us;
+  out[2] = fm.link_gbps;
+  out[3] = fm.hbm_gbps;
+  out[4] = f.median_rel_err;
+  out[5] = f.max_rel_err;
+  out[6] = f.rows;
+  return 0;
+}
+
+int flexar_calib_key(const char* arch, int nranks, int links, const char* classes, uint32_t disabled, char* out,
+                     size_t outlen) {
+  return copy_out(calib_key(arch ? arch : "", nranks, links, classes ? classes : "", disabled, flexar_version()), out,
+                  outlen);
+}
+
+int flexar_calib_path(const char* key, char* out, size_t outlen) {
+  const std::string d = calib_dir();
+  if (d.empty()) { set_error("no calibration cache directory (FLEXAR_CALIB_DIR / HOME)"); return FLEXAR_ERR_UNSUPPORTED; }
+  return copy_out(calib_path(d, key ? key : ""), out, outlen);
+}
+
+// theta = {alpha_launch_us, alpha_sync_us, 1/link_gbps, 1/hbm_gbps}; 1 = loaded, 0 = miss
+int flexar_calib_load(const char* path, const char* key, double* theta) {
+  if (!path || !key || !theta) return FLEXAR_ERR_INVALID;
+  return calib_load(path, key, theta) ? 1 : 0;
+}
+
+int flexar_calib_store(const char* path, const char* key, const double* theta, int nrows, const char* specs_nl,
+                       const double* bytes, const double* us) {
+  if (!path || !key || !theta) return FLEXAR_ERR_INVALID;
+  if (!calib_store(path, key, theta, calib_rows(nrows, specs_nl, bytes, us))) {
+    set_error(std::string("calibration cache: cannot write ") + path);
+    return FLEXAR_ERR_INVALID;
+  }
+  return 0;
+}
+
+// The measurement set of flexar_comm_calibrate for nranks: "spec bytes" lines.
+int flexar_calib_points(int nranks, char* out, size_t outlen) {
+  std::string s;
+  for (const CalibPoint& p : calib_points(nranks)) s += p.spec + " " + std::to_string((long long)p.bytes) + "\n";
+  return copy_out(s, out, outlen);
 }
 
 int flexar_direct_links(const int32_t* cls, const int32_t* hops, int nranks, int self) {

@@ -1,6 +1,8 @@
 // flexar communicator lifecycle: create, export, connect (readiness gate), self-test, configuration
 // setters, topology report, destroy. Reference counterpart: FlexTree_Context and the lazily created
 // scratch buffer (allreduce_over_mpi/mpi_mod.hpp:216-243, 931-950).
+#include <chrono>
+
 #include "comm_internal.hpp"
 
 namespace flexar {
@@ -292,7 +294,24 @@ int flexar_comm_connect(flexar_comm_t c, const void* all) {
     c->peer_flags[r] = (uint64_t*)p;
     c->opened[r] = true;
   }
-  if (!c->links_from_env) c->model.links = direct_links(c->link_cls, c->link_hops, c->nranks, c->rank);
+  // FLEXAR_TEST_PROBE="RANK:class=pcie|xgmi|same|other" or "RANK:links=K" (tests only): that rank reports
+  // a different link class for every peer, or a different link count - what probe agreement must catch
+  if (const char* tp = getenv("FLEXAR_TEST_PROBE")) {
+    int rk = -1;
+    char what[16] = {0}, val[16] = {0};
+    if (sscanf(tp, "%d:%15[a-z]=%15s", &rk, what, val) == 3 && rk == c->rank) {
+      if (!strcmp(what, "links")) {
+        c->links_local = atoi(val);
+      } else if (!strcmp(what, "class")) {
+        const int32_t k = !strcmp(val, "pcie") ? LINK_PCIE : !strcmp(val, "xgmi") ? LINK_XGMI
+                          : !strcmp(val, "same") ? LINK_SAME : LINK_OTHER;
+        for (int r = 0; r < c->nranks; ++r)
+          if (r != c->rank) c->link_cls[r] = k, c->link_hops[r] = 1;
+      }
+    }
+  }
+  if (!c->links_local) c->links_local = direct_links(c->link_cls, c->link_hops, c->nranks, c->rank);
+  if (!c->links_from_env) c->model.links = c->links_local;
   c->memo_gen++;
   c->connected = true;
   return 0;
@@ -458,7 +477,9 @@ uint32_t flexar_comm_disabled(flexar_comm_t c) { return c ? c->disabled : 0; }
 int flexar_comm_topology(flexar_comm_t c, char* buf, size_t buflen) {
   if (!c || !buf) return FLEXAR_ERR_INVALID;
   std::string j = "{\"rank\": " + std::to_string(c->rank) + ", \"device\": " + std::to_string(c->device) +
-                  ", \"links\": " + std::to_string(c->model.links) + ", \"resident_blocks\": " +
+                  ", \"links\": " + std::to_string(c->model.links) + ", \"links_local\": " +
+                  std::to_string(c->links_local) + ", \"links_agreed\": " + (c->links_agreed ? "true" : "false") +
+                  ", \"resident_blocks\": " +
                   std::to_string(c->resident) + ", \"selftested\": \"" + family_names(c->selftested) +
                   "\", \"disabled\": \"" + (c->disabled ? family_names(c->disabled) : std::string()) +
                   "\", \"ipc\": " + (c->ipc ? "true" : "false") + ", \"rccl\": " + (c->nccl ? "true" : "false") +
@@ -514,6 +535,7 @@ int flexar_comm_destroy(flexar_comm_t c) {
   if (c->msg_ws) (void)hipFree(c->msg_ws);
   if (c->nccl && rccl().ok) (void)rccl().CommDestroy(c->nccl);
   if (c->st_buf) (void)hipFree(c->st_buf);
+  if (c->cal_dev) (void)hipFree(c->cal_dev);
   if (c->st_bad) (void)hipHostFree(c->st_bad);
   (void)hipFree(c->stg);
   (void)hipFree(c->flags);
@@ -577,6 +599,259 @@ int flexar_comm_clear_error(flexar_comm_t c) {
   FX_HIP(hipDeviceSynchronize());
   __atomic_store_n(c->err_host, 0u, __ATOMIC_RELEASE);
   return 0;
+}
+
+// ---- probe agreement (readiness.hpp probe_agree) -----------------------------------------------------
+size_t flexar_probe_blob_size(void) { return sizeof(ProbeBlob); }
+
+int flexar_comm_probe_export(flexar_comm_t c, void* out) {
+  if (!c || !out) { set_error("null argument"); return FLEXAR_ERR_INVALID; }
+  ProbeBlob b;
+  memset(&b, 0, sizeof(b));
+  b.magic = kProbeMagic;
+  b.rank = c->rank;
+  b.links = c->links_local > 0 ? c->links_local : 1;
+  b.links_fixed = c->links_from_env ? c->model.links : 0;
+  b.fingerprint = comm_fingerprint(c);
+  for (int r = 0; r < c->nranks && r < 16; ++r) {
+    b.cls[r] = (int8_t)(r == c->rank ? LINK_SAME : c->link_cls[r]);
+    b.hops[r] = (int8_t)c->link_hops[r];
+  }
+  memcpy(out, &b, sizeof(b));
+  return 0;
+}
+
+// Collective in effect: every rank passes every rank's blob (rank-major). Installs the agreed link count;
+// a real disagreement fails with a message naming both ranks (and every rank fails the same way).
+int flexar_comm_probe_agree(flexar_comm_t c, const void* all) {
+  if (!c || !all) { set_error("null argument"); return FLEXAR_ERR_INVALID; }
+  std::vector<ProbeBlob> v(c->nranks);
+  memcpy(v.data(), all, sizeof(ProbeBlob) * c->nranks);
+  int links = 1;
+  std::string why;
+  if (!probe_agree(v.data(), c->nranks, &links, &why)) {
+    set_error(why);
+    return FLEXAR_ERR_INVALID;
+  }
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (!c->links_from_env) c->model.links = links;
+  c->links_agreed = true;
+  c->memo_gen++;
+  return 0;
+}
+
+// ---- connect-time calibration (calibration.hpp) ---------------------------------------------------------
+// Element-wise MIN over the ranks of n doubles, through this communicator (a verified family: the call
+// runs after the self-test). Every rank makes the same calls.
+static int agree_min(flexar_comm* c, double* v, int n, hipStream_t st) {
+  if (n > 256) { set_error("calibration: agreement vector too long"); return FLEXAR_ERR_INVALID; }
+  if (!c->cal_dev) FX_HIP(hipMalloc(&c->cal_dev, 256 * sizeof(double)));
+  FX_HIP(hipMemcpyAsync(c->cal_dev, v, n * sizeof(double), hipMemcpyHostToDevice, st));
+  int rc = flexar_allreduce_ex(c, c->cal_dev, c->cal_dev, (size_t)n, FLEXAR_FLOAT64, FLEXAR_MIN, st, nullptr, 1.0f);
+  if (rc) return rc;
+  FX_HIP(hipMemcpyAsync(v, c->cal_dev, n * sizeof(double), hipMemcpyDeviceToHost, st));
+  FX_HIP(hipStreamSynchronize(st));
+  return check_err(c);
+}
+
+static std::string json_num(double x) {
+  char b[64];
+  snprintf(b, sizeof(b), "%.6g", x);
+  return b;
+}
+
+// Link classes this rank sees, as counts (part of the cache key): x = xGMI one hop, m = xGMI multi-hop,
+// s = same device, p = PCIe, u = not visible, o = other.
+static std::string link_classes(flexar_comm* c) {
+  int x = 0, m = 0, s = 0, p = 0, u = 0, o = 0;
+  for (int r = 0; r < c->nranks; ++r) {
+    if (r == c->rank) continue;
+    switch (c->link_cls[r]) {
+      case LINK_XGMI: (c->link_hops[r] <= 1 ? x : m)++; break;
+      case LINK_SAME: ++s; break;
+      case LINK_PCIE: ++p; break;
+      case LINK_UNKNOWN: ++u; break;
+      default: ++o;
+    }
+  }
+  char b[96];
+  snprintf(b, sizeof(b), "x%dm%ds%dp%du%do%d", x, m, s, p, u, o);
+  return b;
+}
+
+// Collective (every rank, after connect, probe agreement and the self-test). mode 0 = off, 1 = the cached
+// calibration of this node shape if every rank has it, else measure; 2 = measure even if cached. Times the
+// calib_points() executor schedules (fp32, skipping families the self-test disabled), takes the max over
+// ranks (every rank then fits identical rows to identical theta), fits and installs the model; rank 0
+// writes the cache. FLEXAR_MODEL in the environment fixes the model: nothing is measured. Writes a JSON
+// report. A failed measurement leaves the model unchanged on every rank (the failure flag is agreed on).
+int flexar_comm_calibrate(flexar_comm_t c, int mode, char* json, size_t jlen) {
+  if (!c) { set_error("null communicator"); return FLEXAR_ERR_INVALID; }
+  if (!c->connected) { set_error("communicator not connected"); return FLEXAR_ERR_STATE; }
+  const auto t_start = std::chrono::steady_clock::now();
+  auto report = [&](const std::string& j) {
+    c->calib_json = j;
+    if (json && jlen) snprintf(json, jlen, "%s", j.c_str());
+    return j.size() < jlen || !json ? 0 : FLEXAR_ERR_NOMEM;
+  };
+  const char* env_model = getenv("FLEXAR_MODEL");
+  if (c->nranks == 1 || mode == 0) return report("{\"source\": \"off\"}");
+  if (env_model && *env_model) return report("{\"source\": \"FLEXAR_MODEL\"}");
+  if (!c->ipc) return report("{\"source\": \"off\", \"note\": \"message transport only\"}");
+  FX_HIP(hipSetDevice(c->device));
+  hipDeviceProp_t prop;
+  FX_HIP(hipGetDeviceProperties(&prop, c->device));
+  std::string arch = prop.gcnArchName;
+  arch = arch.substr(0, arch.find(':'));
+  // the settings fingerprint too (grid cap, block size, chunking, tune table change what a schedule costs)
+  char fp[24];
+  snprintf(fp, sizeof(fp), ";settings=%016llx", (unsigned long long)comm_fingerprint(c));
+  const std::string key = calib_key(arch, c->nranks, c->model.links, link_classes(c), c->disabled, flexar_version()) + fp;
+  const std::string dir = calib_dir();
+  const std::string path = dir.empty() ? std::string() : calib_path(dir, key);
+  hipStream_t st = nullptr;
+  FX_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  const uint64_t saved_timeout = c->timeout_ticks, saved_calls = c->calls, saved_bytes = c->bytes;
+  const bool saved_profile = c->profile;
+  c->timeout_ticks = env_u64("FLEXAR_SELFTEST_TIMEOUT_MS", 2000) * 100000ull;
+  c->profile = false;
+  auto finish = [&](int rc) {
+    (void)hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
+    c->have_last = false;
+    c->timeout_ticks = saved_timeout;
+    c->profile = saved_profile;
+    c->calls = saved_calls;
+    c->bytes = saved_bytes;
+    return rc;
+  };
+  // 1. the cache: used only if EVERY rank loaded the same constants
+  double theta[4] = {0, 0, 0, 0};
+  const bool have = mode == 1 && !path.empty() && calib_load(path, key, theta);
+  double v[9] = {have ? 1.0 : 0.0, theta[0], theta[1], theta[2], theta[3], -theta[0], -theta[1], -theta[2], -theta[3]};
+  int rc = agree_min(c, v, 9, st);
+  if (rc) return finish(rc);
+  const bool same = v[0] == 1.0 && v[1] == -v[5] && v[2] == -v[6] && v[3] == -v[7] && v[4] == -v[8];
+  std::string rows_json = "[]";
+  CalibFit fit;
+  std::string source;
+  if (same) {
+    source = "cache";
+  } else {
+    // 2. measure: every rank runs every point (epochs stay aligned); failures are agreed on below
+    const std::vector<CalibPoint> pts = calib_points(c->nranks);
+    double maxb = 0;
+    for (const auto& p : pts) maxb = std::max(maxb, p.bytes);
+    char* buf = nullptr;
+    FX_HIP(hipMalloc(&buf, 2 * (size_t)maxb));
+    FX_HIP(hipMemsetAsync(buf, 0, 2 * (size_t)maxb, st));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    FX_HIP(hipEventCreate(&e0));
+    FX_HIP(hipEventCreate(&e1));
+    std::vector<double> t(pts.size() + 1, 0.0);
+    double failed = 0;
+    for (size_t i = 0; i < pts.size(); ++i) {
+      AlgoSpec s;
+      std::string err;
+      if (!parse_algo(pts[i].spec, c->nranks, &s, &err) || (c->disabled & proto_family(s))) continue;
+      const size_t n = (size_t)(pts[i].bytes / 4);
+      const int iters = (int)std::max(5.0, std::min(50.0, 2e8 / pts[i].bytes));
+      int e = 0;
+      for (int k = 0; k < 2 && !e; ++k)
+        e = flexar_allreduce_ex(c, buf, buf + (size_t)maxb, n, FLEXAR_FLOAT32, FLEXAR_SUM, st, pts[i].spec.c_str(), 1.0f);
+      if (!e) e = hipEventRecord(e0, st) == hipSuccess ? 0 : FLEXAR_ERR_HIP;
+      for (int k = 0; k < iters && !e; ++k)
+        e = flexar_allreduce_ex(c, buf, buf + (size_t)maxb, n, FLEXAR_FLOAT32, FLEXAR_SUM, st, pts[i].spec.c_str(), 1.0f);
+      if (!e) e = hipEventRecord(e1, st) == hipSuccess ? 0 : FLEXAR_ERR_HIP;
+      if (!e) e = hipStreamSynchronize(st) == hipSuccess ? 0 : FLEXAR_ERR_HIP;
+      float ms = 0;
+      if (!e) e = hipEventElapsedTime(&ms, e0, e1) == hipSuccess ? 0 : FLEXAR_ERR_HIP;
+      if (!e) e = check_err(c);
+      if (e) {
+        failed = 1;
+        (void)hipStreamSynchronize(st);
+        (void)hipGetLastError();
+        __atomic_store_n(c->err_host, 0u, __ATOMIC_RELEASE);  // every rank still makes every call
+        continue;
+      }
+      t[i] = -(double)ms * 1e3 / iters;  // negated: the MIN agreement below is a max over ranks
+    }
+    t[pts.size()] = -failed;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFree(buf);
+    rc = agree_min(c, t.data(), (int)t.size(), st);
+    if (rc) return finish(rc);
+    std::vector<CalibRow> rows;
+    rows_json = "[";
+    for (size_t i = 0; i < pts.size(); ++i) {
+      if (t[i] == 0.0) continue;
+      rows.push_back({pts[i].spec, pts[i].bytes, -t[i]});
+      rows_json += std::string(rows.size() > 1 ? ", " : "") + "[\"" + pts[i].spec + "\", " +
+                   json_num(pts[i].bytes) + ", " + json_num(-t[i]) + "]";
+    }
+    rows_json += "]";
+    if (-t[pts.size()] != 0.0) {
+      logf(LOG_WARN, c->rank, "calibration: a measurement failed on some rank; the model stays unchanged");
+      finish(0);
+      return report("{\"source\": \"failed\", \"key\": \"" + key + "\", \"rows\": " + rows_json + "}");
+    }
+    fit = fit_theta(rows, c->model, c->nranks);
+    if (!fit.ok) {
+      finish(0);
+      return report("{\"source\": \"no-fit\", \"key\": \"" + key + "\", \"rows\": " + rows_json + "}");
+    }
+    for (int j = 0; j < 4; ++j) theta[j] = fit.theta[j];
+    source = "measured";
+    if (c->rank == 0 && !path.empty() && !calib_store(path, key, theta, rows))
+      logf(LOG_INFO, c->rank, "calibration: cannot write the cache %s", path.c_str());
+  }
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->model = model_with_theta(c->model, theta);
+    c->memo_gen++;
+  }
+  finish(0);
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+  logf(LOG_INFO, c->rank, "calibration (%s): alpha_launch %.3g us, alpha_sync %.3g us, link %.4g GB/s, hbm %.4g GB/s",
+       source.c_str(), c->model.alpha_launch_us, c->model.alpha_sync_us, c->model.link_gbps, c->model.hbm_gbps);
+  std::string j = "{\"source\": \"" + source + "\", \"key\": \"" + key + "\", \"path\": \"" + path +
+                  "\", \"alpha_launch_us\": " + json_num(c->model.alpha_launch_us) + ", \"alpha_sync_us\": " +
+                  json_num(c->model.alpha_sync_us) + ", \"link_gbps\": " + json_num(c->model.link_gbps) +
+                  ", \"hbm_gbps\": " + json_num(c->model.hbm_gbps) + ", \"links\": " + std::to_string(c->model.links) +
+                  ", \"rows\": " + rows_json;
+  if (source == "measured")
+    j += ", \"median_rel_err\": " + json_num(fit.median_rel_err) + ", \"max_rel_err\": " + json_num(fit.max_rel_err);
+  j += ", \"ms\": " + json_num(ms) + "}";
+  return report(j);
+}
+
+// The calibration report of the last flexar_comm_calibrate ("" if none ran).
+int flexar_comm_calibration(flexar_comm_t c, char* json, size_t jlen) {
+  if (!c || !json) return FLEXAR_ERR_INVALID;
+  snprintf(json, jlen, "%s", c->calib_json.c_str());
+  return c->calib_json.size() < jlen ? 0 : FLEXAR_ERR_NOMEM;
+}
+
+// Back to the environment's / default model (links stay the agreed count): what every rank installs when
+// the ranks' calibrations disagree.
+int flexar_comm_reset_model(flexar_comm_t c) {
+  if (!c) return FLEXAR_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  const int links = c->model.links;
+  c->model = XgmiModel::from_env();
+  if (!c->links_from_env) c->model.links = links;
+  c->memo_gen++;
+  return 0;
+}
+
+// Bit pattern hash of the installed model (ranks compare it after calibration).
+uint64_t flexar_comm_model_hash(flexar_comm_t c) {
+  if (!c) return 0;
+  char b[256];
+  snprintf(b, sizeof(b), "%a %a %a %a %d %d", c->model.alpha_launch_us, c->model.alpha_sync_us, c->model.link_gbps,
+           c->model.hbm_gbps, c->model.links, (int)c->model.partials);
+  return fnv1a(b);
 }
 
 }  // extern "C"

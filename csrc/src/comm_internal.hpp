@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "launch.hpp"
+#include "flexar/calibration.hpp"
 #include "flexar/cost_model.hpp"
 #include "flexar/flexar.h"
 #include "flexar/log.hpp"
@@ -232,6 +233,10 @@ struct flexar_comm {
   int32_t peer_dev[kMaxRanks] = {};  // peer's device ordinal in THIS process (-1 = not visible)
   char peer_bus[kMaxRanks][32] = {};
   bool links_from_env = false;  // FLEXAR_MODEL fixed the link count: the probe does not override it
+  int links_local = 0;          // this rank's own probe result (model.links = the ranks' agreed minimum)
+  bool links_agreed = false;    // flexar_comm_probe_agree ran
+  std::string calib_json;       // the connect-time calibration's report (flexar_comm_calibrate)
+  double* cal_dev = nullptr;    // agreement scratch of the calibration (device, 256 doubles)
   int resident = 0;             // executor workgroups resident at once on this GPU (occupancy x CUs)
   // message transport (msg_plan.hpp over RCCL): its own staging arena (never the IPC workspace, whose
   // parity halves peers may still read), the RCCL communicator, plans per call shape
