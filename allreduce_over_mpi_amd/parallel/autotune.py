@@ -26,12 +26,14 @@ from typing import Optional, Sequence
 from .. import _native as nv
 
 
-def default_candidates(world: int, nbytes: int) -> list[str]:
+def default_candidates(world: int, nbytes: int, esize: int = 4) -> list[str]:
     """The schedules worth measuring for ``nbytes`` on ``world`` ranks (bench.py, tools/flexar_tune.py and
     ``autotune`` share this list): latency protocols for small buffers, every flat-stage protocol, rings
     on 1..4 arc-disjoint channels, RHD, the two-stage FlexTree factorizations and the copy engines. The
     direction-balanced flat ("+bidir") joins the flat protocols: on xGMI its reduce-scatter reads and its
-    all-gather writes share the links' two directions."""
+    all-gather writes share the links' two directions. For 16/8-bit elements (``esize`` < 4) every multi-hop
+    schedule is measured twice: with fp32 partials (the default typed staging, one rounding) and rounded
+    per hop ("+rw", 16-bit partials on the links, up to +43 % fewer link bytes for a ring at N = 8)."""
     c = ["ll", "oneshot", "oneshot+wt"] if nbytes <= (1 << 20) else (["oneshot"] if nbytes <= (8 << 20) else [])
     c += ["flat+pull", "flat+push", "flat+pull+nts", "flat+push+nts", "flat+pull+wt", "flat+push+wt"]
     c += ["flat+bidir", "flat+bidir+nts", "flat+bidir+wt"]  # both link directions in one XFER
@@ -43,6 +45,9 @@ def default_candidates(world: int, nbytes: int) -> list[str]:
         c += [f"tree:4,{world // 4}+pull", f"tree:{world // 4},4+pull"]
     if nbytes >= (1 << 20):
         c.append("dma")
+    if esize < 4:  # the single-rounding trade-off, measured: per-hop rounded forms of the multi-hop schedules
+        c += [s.replace("+wt", "") + "+rw" + ("+wt" if "+wt" in s else "") for s in c
+              if (s.startswith("ring") or s.startswith("rhd") or (s.startswith("tree:") and "," in s))]
     return c
 
 

@@ -8,7 +8,7 @@ only; here every rank is timed over K steps bracketed by barrier + device synchr
 the MAX over ranks is reported.
 
     python bench.py --gpus 1 --steps 20 --warmup 5
-    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \\
         --master-addr 127.0.0.1 --master-port 29500 bench.py --gpus 8
 
 Numbers (rccl-tests convention): algbw = bytes / t and busbw = algbw * 2 (N - 1) / N. `value` IS the
@@ -19,17 +19,29 @@ inter-GPU traffic), so `value` is 0 there by definition; the device-copy algbw o
 separately as `algbw_GBps` and is not comparable with busbw. `aggregate_busbw_GBps` (busbw x N) is kept
 as an extra key for whole-job accounting.
 
-At N >= 2 the line also carries the cost model's own choice for this size (no tune table: what
-`auto` runs in production), the model's predicted time for it and its measured time, next to the
-start-up tuner's choice (BASELINE config #4 "cost-model-selected"), the connect-time readiness
-result (probed links, self-tested protocol families), and `cost_model_fit`: every correct candidate at
-64 KiB / 1 MiB / 8 MiB / 64 MiB (checked against RCCL) next to RCCL's own allreduce, and the cost model
-fitted to those timings with its pick at the headline size.
+At N >= 2 the same JSON line also measures every other BASELINE config, OUTSIDE the headline's timed
+region, each next to RCCL and timed max-over-ranks:
+  config3  bf16 1 GiB: RHD with fp32 partials ("+f32"), RHD rounded per hop ("+rw") and the selector's own
+           choice, each checked against an fp32 reference, next to RCCL bf16;
+  config4  the 4 KiB -> 1 GiB (x4) sweep of the selector's choice, every size an exact-integer correctness
+           check, next to RCCL;
+  config5  the fused-scale fp8 gradient allreduce (fp32 256 MiB in, OCP e4m3 on the links, AVG; amax pass +
+           one executor launch) with its max relative error, next to RCCL fp32 AVG;
+plus the cost model's own choice at the headline size (the connect-time calibrated selector, what `auto`
+runs in production), the connect-time readiness result and calibration, and the start-up tuner's table.
+
+Wall-clock budget: FLEXAR_BENCH_BUDGET_S (default 400 s, the driver allows 600). Optional items are
+dropped in a fixed order when the budget runs short - first the calibration mini-sweep
+(`cost_model_fit`), then config #4's tail sizes (>= 64 MiB), then the tuner's grid sweep - and every
+dropped item is listed under `dropped`; `bench_wall_s` is the max over ranks of the time since start.
+Skipping decisions use the max-over-ranks elapsed time, so every rank takes the same path.
 
 Correctness: every tuner candidate and the final choice are checked against RCCL's result
 (torch.distributed "nccl") on three consecutive calls whose inputs are scaled by 1, 1/2 and 1/4 (exact
 in every dtype). Calls alternate staging halves, so a read of a staging line left over from one of the
 two previous calls changes the result and is caught. The check runs again after the timed region.
+Every failure is agreed on by all ranks (one max-over-ranks per candidate, whether or not this rank
+raised), so ranks never diverge in their collective calls.
 Data: synthetic torch.randn buffers seeded per rank. If no flexar algorithm is correct on this node the
 run falls back to RCCL and says so in `config.algorithm` and `fallback`.
 """
@@ -42,6 +54,7 @@ import os
 import sys
 import time
 
+_T_START = time.monotonic()
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
@@ -49,6 +62,11 @@ sys.path.insert(0, REPO)
 # (measured locally on CPU/MPICH — the reference publishes no numbers).
 BASELINE_BUSBW_256MIB = 3.15
 CHECK_SCALES = (1.0, 0.5, 0.25)  # powers of two: exact scaling of inputs and of the reference sum
+CALIB_SIZES = (64 << 10, 1 << 20, 8 << 20, 64 << 20)
+# budget fractions: an optional item runs only if the agreed elapsed time is below this share of the budget
+# (the lowest-priority item needs the most headroom, so it is the first to go)
+DROP_AT = {"cost_model_fit": 0.45, "config4_tail": 0.6, "grid_sweep": 0.3}
+COMPANION_AT = 0.85  # config3 / config4 head / config5 / small messages
 
 
 def log(rank, *a):
@@ -61,6 +79,7 @@ class RcclOnly:
 
     def __init__(self, dist):
         self.dist = dist
+        self.calibration = None
 
     def all_reduce(self, tensor, op="sum", out=None, algo=None, scale=1.0):
         dst = tensor if out is None else out.copy_(tensor)
@@ -78,6 +97,26 @@ class RcclOnly:
 
     def close(self):
         pass
+
+
+class Budget:
+    """Wall-clock budget of the whole run; decisions on the max-over-ranks elapsed time (collective)."""
+
+    def __init__(self, seconds, agree):
+        self.seconds = seconds
+        self.agree = agree
+        self.dropped = []
+
+    def elapsed(self):
+        return self.agree(time.monotonic() - _T_START)
+
+    def allow(self, item, fraction):
+        """Collective: True if the agreed elapsed time leaves room for `item` (else it is listed as dropped)."""
+        e = self.elapsed()
+        if e <= fraction * self.seconds:
+            return True
+        self.dropped.append({"item": item, "elapsed_s": round(e, 1), "limit_s": round(fraction * self.seconds, 1)})
+        return False
 
 
 def main():
@@ -98,6 +137,10 @@ def main():
     ap.add_argument("--no-tune", action="store_true", help="use the cost model instead of the start-up tuner")
     ap.add_argument("--no-calibrate", action="store_true",
                     help="skip the 64 KiB..64 MiB mini-sweep of the tuner's candidates vs RCCL and the cost-model fit")
+    ap.add_argument("--no-configs", action="store_true", help="skip the BASELINE config #3/#4/#5 companion sections")
+    ap.add_argument("--config3-mb", type=float, default=1024.0, help="config #3 buffer MiB (bf16)")
+    ap.add_argument("--config4-max", default="1G", help="config #4 sweep top size")
+    ap.add_argument("--config5-mb", type=float, default=256.0, help="config #5 buffer MiB (fp32 in, e4m3 wire)")
     ap.add_argument("--transport", default="rccl", choices=["rccl", "auto", "ipc"],
                     help="Communicator transport at N > 1 (rccl: IPC + the '+rccl' message transport candidates)")
     args = ap.parse_args()
@@ -105,9 +148,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # every rank's Python stacks on stderr if the run is still going after this long (the bench takes about a
-    # minute; a stuck collective then names itself in the log); FLEXAR_BENCH_TRACEBACK_S=0 disables it
-    tb_s = int(os.environ.get("FLEXAR_BENCH_TRACEBACK_S", "600" if world > 1 else "0"))
+    # every rank's Python stacks on stderr if the run is still going after this long (a stuck collective
+    # then names itself in the log); FLEXAR_BENCH_TRACEBACK_S=0 disables it
+    tb_s = int(os.environ.get("FLEXAR_BENCH_TRACEBACK_S", "540" if world > 1 else "0"))
     if tb_s > 0:
         import faulthandler
 
@@ -166,6 +209,22 @@ def main():
     ws_bytes = max(512 << 20, 4 * nbytes + (64 << 20))
     fallback = None
 
+    def max_over_ranks(v: float) -> float:
+        if world == 1:
+            return v
+        t = torch.tensor([v], device="cpu" if host_ref else dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def max_vec(vals):
+        if world == 1:
+            return list(vals)
+        t = torch.tensor(list(vals), device="cpu" if host_ref else dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return [float(v) for v in t.tolist()]
+
+    budget = Budget(float(os.environ.get("FLEXAR_BENCH_BUDGET_S", "400")), max_over_ranks)
+
     # one rank per GPU: IPC plus the RCCL message transport, so the tuner also measures the FlexTree / ring /
     # RHD schedules over ncclSend/ncclRecv ("+rccl"); if RCCL cannot be set up, IPC alone
     transports = ["ipc"] if (world == 1 or host_ref) else [args.transport, "ipc"] if args.transport != "ipc" else ["ipc"]
@@ -218,14 +277,16 @@ def main():
             log(rank, f"zero-copy candidates skipped: {e}")
             return False
 
-    zc = False  # registered after the cost-model measurement (which runs the unregistered, staging path)
+    def rebuild(why):
+        """Collective: a failed call may leave epochs / flags inconsistent - start from a fresh communicator."""
+        nonlocal comm, fallback
+        comm.close()
+        torch.cuda.synchronize()
+        comm = make_comm() or RcclOnly(dist)
+        if isinstance(comm, RcclOnly):
+            fallback = f"flexar communicator could not be rebuilt ({why})"
 
-    def max_over_ranks(v: float) -> float:
-        if world == 1:
-            return v
-        t = torch.tensor([v], device="cpu" if host_ref else dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+    zc = False  # registered after the cost-model measurement (which runs the unregistered, staging path)
 
     # ---------------------------------------------------------------- correctness vs RCCL
     op = args.op
@@ -249,76 +310,93 @@ def main():
     tol = tol * math.sqrt(world) * 4 if dtype != torch.float8_e4m3fn else tol
 
     def check(spec):
-        """Three consecutive calls with inputs x, x/2, x/4: every result must match the reference scaled
-        the same way (a stale staging line from either of the two previous calls would be off by 2x/4x)."""
+        """Local (no collectives): three consecutive calls with inputs x, x/2, x/4 - every result must match
+        the reference scaled the same way (a stale staging line from either of the two previous calls would
+        be off by 2x/4x). Returns (failed, err): failed 0 ok, 0.5 wrong result, 1 error (the communicator
+        may be inconsistent); the caller agrees on it with every rank."""
         worst = 0.0
-        for s in CHECK_SCALES:
-            src = x
-            if s != 1.0:
-                xs.copy_((x.float() * s).to(dtype))
-                src = xs
-            comm.all_reduce(src, out=y, op=op, algo=None if spec == "auto" else spec)
-            torch.cuda.synchronize()
-            err = float((y.float() - ref_f * s).abs().max().item()) / (ref_max * s)
-            worst = max(worst, err)
-        return worst <= tol, worst
+        try:
+            for s in CHECK_SCALES:
+                src = x
+                if s != 1.0:
+                    xs.copy_((x.float() * s).to(dtype))
+                    src = xs
+                comm.all_reduce(src, out=y, op=op, algo=None if spec == "auto" else spec)
+                torch.cuda.synchronize()
+                err = float((y.float() - ref_f * s).abs().max().item()) / (ref_max * s)
+                worst = max(worst, err)
+            comm.check()
+        except nv.FlexarError as e:
+            return 1.0, str(e)
+        return (0.0 if worst <= tol else 0.5), worst
 
     def verify(out, n):
         """A prefix of n elements of the last result against the same prefix of the reference."""
         err = float((out.float() - ref_f[:n]).abs().max().item()) / ref_max
         return err <= tol, err
 
-    def timed(spec, iters, warm=1):
-        a = None if spec == "auto" else spec
-        for _ in range(warm):
-            comm.all_reduce(x, out=y, op=op, algo=a)
-        torch.cuda.synchronize()
+    def timed_fn(fn, iters, warm=1):
+        """Collective: per-call seconds (max over ranks) of fn, or None if it failed on any rank. Exactly one
+        barrier and one agreement on every rank whether or not this rank raised."""
+        failed = 0.0
+        try:
+            for _ in range(warm):
+                fn()
+            torch.cuda.synchronize()
+        except nv.FlexarError:
+            failed = 1.0
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
-        for _ in range(iters):
-            comm.all_reduce(x, out=y, op=op, algo=a)
-        torch.cuda.synchronize()
-        return max_over_ranks(time.perf_counter() - t0) / iters
+        try:
+            if not failed:
+                for _ in range(iters):
+                    fn()
+                torch.cuda.synchronize()
+                comm.check()
+        except nv.FlexarError:
+            failed = 1.0
+        dt, bad = max_vec([time.perf_counter() - t0, failed])
+        return None if bad else dt / iters
+
+    def timed(spec, iters, warm=1):
+        a = None if spec == "auto" else spec
+        return timed_fn(lambda: comm.all_reduce(x, out=y, op=op, algo=a), iters, warm)
 
     # ---------------------------------------------------------------- cost model (no tune table)
     model = None
     if world > 1 and not fallback:
-        try:
-            choice = comm.describe(count, dtype)
-            spec0 = choice.split(" ")[0]
-            ok0, err0 = check("auto")
-            t0_model = timed("auto", 5) if max_over_ranks(0.0 if ok0 else 1.0) == 0.0 else None
-            model = {"choice": choice, "predicted_us": round(comm.predict_us(spec0, nbytes), 1),
-                     "measured_us": round(t0_model * 1e6, 1) if t0_model else None,
-                     "busbw_GBps": round(busbw_gbps(nbytes, t0_model, world), 2) if t0_model else None,
-                     "correct": ok0}
-            log(rank, f"cost model: {choice} predicted {model['predicted_us']} us, measured {model['measured_us']} us")
-        except nv.FlexarError as e:
-            model = {"error": str(e)}
-        if max_over_ranks(1.0 if "error" in model else 0.0) != 0.0:  # a failed call may leave epochs / flags
-            comm.close()                                             # inconsistent: start the tuner afresh
-            torch.cuda.synchronize()
-            comm = make_comm() or RcclOnly(dist)
-            if isinstance(comm, RcclOnly):
-                fallback = "flexar communicator could not be rebuilt"
+        choice = comm.describe(count, dtype)
+        spec0 = choice.split(" ")[0]
+        failed0, err0 = check("auto")
+        failed0 = max_over_ranks(failed0)
+        t0_model = timed("auto", 5) if failed0 == 0.0 else None
+        model = {"choice": choice, "predicted_us": round(comm.predict_us(spec0, nbytes), 1),
+                 "measured_us": round(t0_model * 1e6, 1) if t0_model else None,
+                 "busbw_GBps": round(busbw_gbps(nbytes, t0_model, world), 2) if t0_model else None,
+                 "correct": failed0 == 0.0, "error": err0 if isinstance(err0, str) else None}
+        log(rank, f"cost model: {choice} predicted {model['predicted_us']} us, measured {model['measured_us']} us")
+        if failed0 >= 1.0 or (failed0 == 0.0 and t0_model is None):
+            rebuild("cost-model measurement failed")
     zc = register_buffers(comm)
-    if model and "error" not in model and zc:
+    if model and model["correct"] and zc and not isinstance(comm, RcclOnly):
         # the same automatic choice once the buffers are registered: the flat schedule (or any choice the
         # model prices higher than the zero-copy push form) runs "+zc+push" (comm.hip, FLEXAR_ZC_AUTO)
-        try:
-            ok1, _ = check("auto")
-            t1 = timed("auto", 5) if max_over_ranks(0.0 if ok1 else 1.0) == 0.0 else None
-            model["registered_measured_us"] = round(t1 * 1e6, 1) if t1 else None
-            model["registered_busbw_GBps"] = round(busbw_gbps(nbytes, t1, world), 2) if t1 else None
-            model["registered_correct"] = ok1
-        except nv.FlexarError as e:
-            model["registered_error"] = str(e)
+        f1, _ = check("auto")
+        f1 = max_over_ranks(f1)
+        t1 = timed("auto", 5) if f1 == 0.0 else None
+        model["registered_measured_us"] = round(t1 * 1e6, 1) if t1 else None
+        model["registered_busbw_GBps"] = round(busbw_gbps(nbytes, t1, world), 2) if t1 else None
+        model["registered_correct"] = f1 == 0.0
+        if f1 >= 1.0 or (f1 == 0.0 and t1 is None):
+            rebuild("registered cost-model measurement failed")
+            zc = register_buffers(comm)
 
     # ---------------------------------------------------------------- start-up tuner
     algo = args.algo
     tune_log = {}
     calib = None
+    timings = {}
     ranked = []  # (spec, grid) in the order the timed region tries them
     if fallback:
         algo = "rccl"
@@ -327,53 +405,31 @@ def main():
 
         # flat-stage protocols, rings on 1..4 arc-disjoint channels, RHD, two-stage FlexTree factorizations,
         # the copy engines (and the latency protocols for small buffers)
-        cands = default_candidates(world, nbytes)
+        cands = default_candidates(world, nbytes, esize=esize)
         if comm.topology().get("rccl"):  # the schedules over RCCL send/recv as well
             cands += ["flat+rccl", "ring+rccl"] + (["rhd+rccl"] if world > 2 and not world & (world - 1) else [])
         if zc:  # registered buffers: the flat schedule straight from / to the peers' x and y (put: remote writes only)
             cands += ["flat+zc", "flat+zc+nts", "flat+zc+wt", "flat+zc+push", "flat+zc+push+nts", "flat+zc+push+wt",
                       "flat+zc+put", "flat+zc+put+nts", "flat+zc+put+wt"]
-        timings = {}
         for spec in cands:
-            failed = 0.0
-            try:
-                ok, err = check(spec)
-                comm.check()  # a watchdog timeout belongs to THIS candidate (its wrong result is a symptom)
-                if max_over_ranks(0.0 if ok else 1.0) != 0.0:
-                    failed = 1.0
-                    tune_log[spec] = f"WRONG (max rel err {err:.3g})"
-                    log(rank, f"tuner: {spec} produced wrong results (rel err {err:.3g}); excluded")
-                else:
-                    t = timed(spec, 5, warm=2)
-                    comm.check()
-            except nv.FlexarError as e:
+            failed, err = check(spec)
+            failed = max_over_ranks(failed)  # one agreement per candidate, on every rank
+            t = timed(spec, 5, warm=2) if failed == 0.0 else None
+            if failed == 0.0 and t is None:
                 failed = 1.0
-                tune_log[spec] = f"error: {e}"
-                log(rank, f"tuner: {spec} failed on this rank: {e}")
-            if max_over_ranks(failed) != 0.0:
-                # a failed candidate may leave the communicator's epochs/flags inconsistent: rebuild it
-                tune_log.setdefault(spec, "failed on a peer")
-                comm.close()
-                torch.cuda.synchronize()
-                comm = make_comm() or RcclOnly(dist)
-                if isinstance(comm, RcclOnly):
-                    fallback = "flexar communicator could not be rebuilt"
-                    break
-                zc = register_buffers(comm)
+            if failed:
+                tune_log[spec] = f"WRONG (max rel err {err:.3g})" if failed < 1.0 and not isinstance(err, str) \
+                    else f"error: {err}" if isinstance(err, str) else "failed on a peer"
+                log(rank, f"tuner: {spec} excluded ({tune_log[spec]})")
+                if failed >= 1.0:  # the communicator's epochs / flags may be inconsistent now
+                    rebuild(f"tuner candidate {spec} failed")
+                    if isinstance(comm, RcclOnly):
+                        break
+                    zc = register_buffers(comm)
                 continue
             timings[spec] = t
             tune_log[spec] = round(busbw_gbps(nbytes, t, world), 2)
             log(rank, f"tuner: {spec:14s} {t*1e3:8.3f} ms  busbw {busbw_gbps(nbytes, t, world):8.1f} GB/s")
-        if timings and not fallback and not args.no_calibrate:
-            calib = calibrate_model(comm, timings, nbytes, esize, world, x, y, op, dist, max_over_ranks, rank, shared,
-                                    verify, world > 1 and not args.no_rccl and dtype != torch.float8_e4m3fn)
-            if calib.get("broken"):  # a candidate failed at a small size: start from a fresh communicator
-                comm.close()
-                torch.cuda.synchronize()
-                comm = make_comm() or RcclOnly(dist)
-                if isinstance(comm, RcclOnly):
-                    fallback = "flexar communicator could not be rebuilt"
-                zc = register_buffers(comm)
         if not timings or fallback:
             fallback = fallback or "no flexar algorithm produced correct results on this node"
             log(rank, f"tuner: {fallback}; measuring RCCL instead")
@@ -387,21 +443,28 @@ def main():
             # rank's workgroup b only ever waits for workgroup b of its peers, so one rank per GPU needs no
             # co-residency, but more resident workgroups keep more xGMI loads in flight. Ranks sharing one GPU
             # must stay co-resident with each other (FLEXAR_MAX_GRID caps them).
-            resident = int(comm.stats().get("resident_blocks") or 256)
-            grids = [g for g in (32, 64, 128, 256, 512, 1024) if g <= resident and
-                     (not shared or g <= int(os.environ["FLEXAR_MAX_GRID"]))]
-            best, best_grid, best_t = None, 0, float("inf")
             ranked_specs = sorted(timings, key=timings.get)
-            for spec in ranked_specs[:2]:
-                if timings[spec] < best_t:
-                    best, best_grid, best_t = spec, 0, timings[spec]
-                for g in grids:
-                    comm.set_grid(g)
-                    t = timed(spec, 5)
-                    tune_log[f"{spec}@grid{g}"] = round(busbw_gbps(nbytes, t, world), 2)
-                    if t < best_t:
-                        best, best_grid, best_t = spec, g, t
-            comm.set_grid(best_grid)
+            best, best_grid, best_t = ranked_specs[0], 0, timings[ranked_specs[0]]
+            if budget.allow("grid_sweep", DROP_AT["grid_sweep"]):
+                resident = int(comm.stats().get("resident_blocks") or 256)
+                grids = [g for g in (32, 64, 128, 256, 512, 1024) if g <= resident and
+                         (not shared or g <= int(os.environ["FLEXAR_MAX_GRID"]))]
+                for spec in ranked_specs[:2]:
+                    for g in grids:
+                        comm.set_grid(g)
+                        t = timed(spec, 5)
+                        if t is None:  # failed on some rank: stop the sweep on a fresh communicator
+                            tune_log[f"{spec}@grid{g}"] = "failed"
+                            rebuild(f"grid sweep {spec}@{g} failed")
+                            zc = register_buffers(comm)
+                            break
+                        tune_log[f"{spec}@grid{g}"] = round(busbw_gbps(nbytes, t, world), 2)
+                        if t < best_t:
+                            best, best_grid, best_t = spec, g, t
+                    if isinstance(comm, RcclOnly):
+                        break
+            if not isinstance(comm, RcclOnly):
+                comm.set_grid(best_grid)
             algo = best
             # the runners-up (auto grid) stand by in case the pick fails its final checks on this node
             ranked = [(best, best_grid)] + [(sp, 0) for sp in ranked_specs if sp != best][:2]
@@ -421,6 +484,7 @@ def main():
         ranked.append(("rccl", None))
     rejected = {}
     t_step = err = None
+    desc = algo
     for attempt, (algo, grid) in enumerate(ranked):
         if algo == "rccl" and not isinstance(comm, RcclOnly):
             comm.close()
@@ -441,13 +505,7 @@ def main():
             fallback = fallback or "every flexar candidate failed its final checks"
         if grid is not None:
             comm.set_grid(grid)
-        failed, err = 0.0, 0.0
-        try:
-            ok, err = check(algo)
-            comm.check()
-            failed = 0.0 if ok else 1.0
-        except nv.FlexarError as e:
-            failed, err = 1.0, str(e)
+        failed, err = check(algo)
         if attempt == 0 and os.environ.get("FLEXAR_BENCH_REJECT_FIRST") == "1":  # rehearses this fallback chain
             failed, err = 1.0, "rejected by FLEXAR_BENCH_REJECT_FIRST=1"
         if max_over_ranks(failed) != 0.0:
@@ -457,30 +515,31 @@ def main():
         desc = comm.describe(count, dtype) if algo == "auto" else algo
         log(rank, f"correctness vs {'RCCL' if world > 1 else 'input'}: max rel err {err:.3g} (ok); running {desc}")
         a = None if algo == "auto" else algo
-        for _ in range(args.warmup):
-            comm.all_reduce(x, out=y, op=op, algo=a)
-        torch.cuda.synchronize()
+        run_failed = 0.0
+        try:
+            for _ in range(args.warmup):
+                comm.all_reduce(x, out=y, op=op, algo=a)
+            torch.cuda.synchronize()
+        except nv.FlexarError:
+            run_failed = 1.0
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            comm.all_reduce(x, out=y, op=op, algo=a)
+        try:
+            if not run_failed:
+                for _ in range(args.steps):
+                    comm.all_reduce(x, out=y, op=op, algo=a)
+        except nv.FlexarError:
+            run_failed = 1.0
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
-        elapsed = max_over_ranks(time.perf_counter() - t0)
+        elapsed, run_failed = max_vec([time.perf_counter() - t0, run_failed])
         t_step = elapsed / max(1, args.steps)
         # the timed calls must have produced correct results too (checked again right after, same protocol state)
-        failed, err_after = 0.0, 0.0
-        try:
-            comm.check()
-            ok, err_after = check(algo)
-            comm.check()
-            failed = 0.0 if ok else 1.0
-        except nv.FlexarError as e:
-            failed, err_after = 1.0, str(e)
+        failed, err_after = check(algo) if not run_failed else (1.0, "a timed call failed")
         if max_over_ranks(failed) == 0.0:
             break
         rejected[algo] = f"failed after the timed run ({err_after})"
@@ -494,48 +553,55 @@ def main():
     rccl_busbw = None
     if world > 1 and not args.no_rccl and dtype != torch.float8_e4m3fn:
         z = x.clone()
-        for _ in range(max(1, args.warmup)):
-            dist.all_reduce(z)
-        torch.cuda.synchronize()
-        dist.barrier()
-        t1 = time.perf_counter()
-        for _ in range(args.steps):
-            dist.all_reduce(z)
-        torch.cuda.synchronize()
-        dist.barrier()
-        rt = max_over_ranks(time.perf_counter() - t1) / max(1, args.steps)
-        rccl_busbw = round(busbw_gbps(nbytes, rt, world), 2)
+        rt = timed_fn(lambda: dist.all_reduce(z), max(1, args.steps), max(1, args.warmup))
+        rccl_busbw = round(busbw_gbps(nbytes, rt, world), 2) if rt else None
+        del z
+
+    # ---------------------------------------------------------------- BASELINE configs #3 / #4 / #5
+    sections = {}
+    flex = not isinstance(comm, RcclOnly)
+    if world > 1 and flex and not args.no_configs:
+        if budget.allow("config5", COMPANION_AT):
+            sections["config5"] = run_config5(comm, world, dev, dist, timed_fn, max_vec, host_ref, args, rank)
+        if budget.allow("config3", COMPANION_AT):
+            sections["config3"] = run_config3(comm, world, rank, dev, dist, timed_fn, max_vec, host_ref, args)
+        if budget.allow("config4", COMPANION_AT):
+            tail_ok = budget.allow("config4_tail", DROP_AT["config4_tail"])
+            hi = parse_bytes(args.config4_max)
+            sections["config4"] = run_sweep(comm, world, rank, dev, torch.float32, "sum", dist, max_over_ranks,
+                                            4096, hi if tail_ok else min(hi, 16 << 20), not args.no_rccl and not host_ref,
+                                            timed_fn, args.sweep_out)
+            if not tail_ok:
+                sections["config4"]["dropped_sizes"] = [b for b in _x4(4096, hi) if b > (16 << 20)]
 
     # latency-bound companion figure (outside the timed region): an 8 KiB fp32 allreduce, eager, the
     # selector's choice (LL), against RCCL's on the same buffer
     small = None
-    if world > 1 and not args.no_small:
-        xs = torch.randn(2048, device=dev)
-        ys = torch.empty_like(xs)
-
-        def per_call(fn, iters=200):
-            for _ in range(20):
-                fn()
-            torch.cuda.synchronize()
-            dist.barrier()
-            t2 = time.perf_counter()
-            for _ in range(iters):
-                fn()
-            torch.cuda.synchronize()
-            return round(max_over_ranks(time.perf_counter() - t2) / iters * 1e6, 2)
-
-        small = {"flexar": per_call(lambda: comm.all_reduce(xs, out=ys))}
+    if world > 1 and not args.no_small and budget.allow("small_msg", COMPANION_AT):
+        xsm = torch.randn(2048, device=dev)
+        ysm = torch.empty_like(xsm)
+        tf = timed_fn(lambda: comm.all_reduce(xsm, out=ysm), 200, 20)
+        small = {"flexar": round(tf * 1e6, 2) if tf else None}
         if not args.no_rccl and not host_ref:
-            small["rccl"] = per_call(lambda: dist.all_reduce(xs))
+            tr = timed_fn(lambda: dist.all_reduce(xsm), 200, 20)
+            small["rccl"] = round(tr * 1e6, 2) if tr else None
+
+    # calibration mini-sweep of the tuner's candidates vs RCCL + the cost-model fit (the first item dropped)
+    if timings and flex and not args.no_calibrate and world > 1 and \
+            budget.allow("cost_model_fit", DROP_AT["cost_model_fit"]):
+        calib = calibrate_model(comm, timings, nbytes, esize, world, x, y, op, dist, max_over_ranks, rank, shared,
+                                verify, world > 1 and not args.no_rccl and dtype != torch.float8_e4m3fn)
 
     algbw = algbw_gbps(nbytes, t_step)
     busbw = busbw_gbps(nbytes, t_step, world)
     value = busbw  # rccl-tests busbw; 0 at N = 1 by definition (see the module docstring)
     readiness = None
-    if world > 1 and not isinstance(comm, RcclOnly):
+    if world > 1 and isinstance(comm, Communicator):
         topo = comm.topology()
-        readiness = {"links": topo["links"], "selftested": topo["selftested"], "disabled": topo["disabled"],
-                     "peer_links": sorted({p["link"] for p in topo["peers"] if p["link"] != "self"})}
+        readiness = {"links": topo["links"], "links_local": topo.get("links_local"), "selftested": topo["selftested"],
+                     "disabled": topo["disabled"],
+                     "peer_links": sorted({p["link"] for p in topo["peers"] if p["link"] != "self"}),
+                     "calibration": comm.calibration}
     out = {
         "metric": "allreduce bus bandwidth (GB/s)",
         "value": round(value, 2),
@@ -574,11 +640,18 @@ def main():
         "zero_copy": {"registered": zc, "note": zc_note} if world > 1 else None,
         "small_msg_8KiB_us_per_call": small,
     }
+    out.update(sections)
     if args.sweep:
-        out["sweep"] = run_sweep(args, comm, world, rank, dev, dtype, op, dist, max_over_ranks)
+        lo, hi = (parse_bytes(t) for t in args.sweep.split(":"))
+        out["sweep"] = run_sweep(comm, world, rank, dev, dtype, op, dist, max_over_ranks, lo, hi,
+                                 world > 1 and dtype != torch.float8_e4m3fn and not args.no_rccl and not host_ref,
+                                 timed_fn, args.sweep_out)
     if world == 1:
         out["note"] = ("N=1: no inter-GPU traffic, busbw = 0 by definition (value); algbw_GBps is the device copy "
                        "through the flexar executor kernel and is not comparable with busbw")
+    out["dropped"] = budget.dropped or None
+    out["budget_s"] = budget.seconds
+    out["bench_wall_s"] = round(budget.elapsed(), 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
     comm.close()
@@ -586,7 +659,118 @@ def main():
         dist.destroy_process_group()
 
 
-CALIB_SIZES = (64 << 10, 1 << 20, 8 << 20, 64 << 20)
+def _x4(lo, hi):
+    out, b = [], lo
+    while b <= hi:
+        out.append(b)
+        b *= 4
+    return out
+
+
+def run_config5(comm, world, dev, dist, timed_fn, max_vec, host_ref, args, rank):
+    """BASELINE config #5: the fused-scale fp8 gradient allreduce. fp32 256 MiB per rank in and out, OCP
+    e4m3 on the links, AVG: one amax pass + ONE executor launch whose first transfer quantises with the
+    global pre-scale and whose last dequantises with the post-scale (Communicator.all_reduce_fp8). Max
+    relative error against the exact fp32 AVG (RCCL's), and RCCL's own fp32 AVG time next to it."""
+    import torch
+
+    from allreduce_over_mpi_amd import _native as nv
+    from allreduce_over_mpi_amd.utils.perf import busbw_gbps
+
+    n = int(args.config5_mb * (1 << 20)) // 4
+    g = torch.Generator(device=dev)
+    g.manual_seed(777 + rank)
+    x = torch.randn(n, device=dev, generator=g)
+    y = torch.empty_like(x)
+    ref = x.cpu() if host_ref else x.clone()
+    dist.all_reduce(ref)
+    ref = (ref / world).to(dev)
+    out = {"what": f"all_reduce_fp8: fp32 {args.config5_mb:g} MiB per rank, e4m3 wire, AVG (amax + one fused launch)"}
+    failed, err = 0.0, None
+    try:
+        comm.all_reduce_fp8(x, op="avg", out=y)
+        torch.cuda.synchronize()
+        err = float((y - ref).abs().max().item()) / (float(ref.abs().max().item()) + 1e-12)
+    except nv.FlexarError as e:
+        failed, err = 1.0, str(e)
+    failed, = max_vec([failed])
+    if failed:
+        out["error"] = err if isinstance(err, str) else "failed on a peer"
+        return out
+    t = timed_fn(lambda: comm.all_reduce_fp8(x, op="avg", out=y), 10, 2)
+    errs = max_vec([err])
+    out.update(flexar_us=round(t * 1e6, 1) if t else None,
+               flexar_busbw_GBps=round(busbw_gbps(4 * n, t, world), 2) if t else None,
+               max_rel_err=round(errs[0], 5),
+               correct=errs[0] <= 0.13)  # e4m3: 3 mantissa bits, one rounding per contribution and result
+    if not host_ref and not args.no_rccl:
+        z = x.clone()
+        tr = timed_fn(lambda: dist.all_reduce(z, op=dist.ReduceOp.AVG), 10, 2)
+        out.update(rccl_fp32_avg_us=round(tr * 1e6, 1) if tr else None,
+                   rccl_fp32_avg_busbw_GBps=round(busbw_gbps(4 * n, tr, world), 2) if tr else None)
+    del x, y, ref
+    return out
+
+
+def run_config3(comm, world, rank, dev, dist, timed_fn, max_vec, host_ref, args):
+    """BASELINE config #3: bf16, 1 GiB per rank. RHD (tree 2,..,2) with fp32 partials ("+f32": one rounding)
+    and rounded per hop ("+rw": the reference's ring semantics, bf16 partials on the links), and the
+    selector's own choice, each checked against the fp32 sum of the same bf16 inputs, next to RCCL bf16."""
+    import torch
+
+    from allreduce_over_mpi_amd import _native as nv
+    from allreduce_over_mpi_amd.utils.perf import busbw_gbps
+
+    nbytes = int(args.config3_mb * (1 << 20))
+    n = nbytes // 2
+    g = torch.Generator(device=dev)
+    g.manual_seed(4242 + rank)
+    x = torch.randn(n, device=dev, generator=g).to(torch.bfloat16)
+    y = torch.empty_like(x)
+    ref = x.float().cpu() if host_ref else x.float()
+    dist.all_reduce(ref)
+    ref = ref.to(dev)
+    ref_max = float(ref.abs().max().item()) + 1e-6
+    out = {"what": f"bf16 {args.config3_mb:g} MiB per rank", "bytes": n * 2, "variants": {}}
+    pow2 = world > 1 and not world & (world - 1)
+    variants = (["rhd+pull+f32", "rhd+pull+rw"] if pow2 else []) + ["auto"]
+    for spec in variants:
+        a = None if spec == "auto" else spec
+        failed, err = 0.0, None
+        try:
+            comm.all_reduce(x, out=y, algo=a)
+            torch.cuda.synchronize()
+            err = float((y.float() - ref).abs().max().item()) / ref_max
+            comm.check()
+        except nv.FlexarError as e:
+            failed, err = 1.0, str(e)
+        failed, = max_vec([failed])
+        row = {"spec": comm.describe(n, torch.bfloat16).split(" ")[0] if spec == "auto" else spec}
+        if failed:
+            row["error"] = err if isinstance(err, str) else "failed on a peer"
+            out["variants"][spec] = row
+            continue
+        t = timed_fn(lambda: comm.all_reduce(x, out=y, algo=a), 5, 1)
+        e = max_vec([err])[0]
+        row.update(us=round(t * 1e6, 1) if t else None, busbw_GBps=round(busbw_gbps(n * 2, t, world), 2) if t else None,
+                   max_rel_err=round(e, 6), correct=e <= 2e-2 * math.sqrt(world) * 4)
+        out["variants"][spec] = row
+        log(rank, f"config3 {spec}: {row}")
+    if not host_ref and not args.no_rccl:
+        z = x.clone()
+        tr = timed_fn(lambda: dist.all_reduce(z), 5, 1)
+        z.copy_(x)
+        dist.all_reduce(z)
+        e = float((z.float() - ref).abs().max().item()) / ref_max
+        out["rccl"] = {"us": round(tr * 1e6, 1) if tr else None,
+                       "busbw_GBps": round(busbw_gbps(n * 2, tr, world), 2) if tr else None,
+                       "max_rel_err": round(max_vec([e])[0], 6)}
+        del z
+    del x, y, ref
+    return out
+
+
+CALIB_NOTE = "calibration mini-sweep of the tuner's candidates vs RCCL and the cost-model fit"
 
 
 def calibrate_model(comm, timings, nbytes, esize, world, x, y, op, dist, max_over_ranks, rank, shared, verify,
@@ -598,7 +782,7 @@ def calibrate_model(comm, timings, nbytes, esize, world, x, y, op, dist, max_ove
     tuner's at the headline size) and report the fitted constants, the fit error and the schedule the
     FITTED model would pick at the headline size next to the tuner's winner ("cost-model-selected" priced
     with measured constants). Not installed: the timed region runs the tuner's pick. Times are max over
-    ranks, so every rank fits the same rows."""
+    ranks, so every rank fits the same rows. Every failure is agreed on before anything else collective."""
     import torch
 
     from allreduce_over_mpi_amd import _native as nv
@@ -608,20 +792,29 @@ def calibrate_model(comm, timings, nbytes, esize, world, x, y, op, dist, max_ove
     links = int(comm.topology().get("links", 0)) if not shared else 0
     # the model prices executor schedules over IPC only (not the copy engines or the message transport)
     model_specs = [s for s in timings if "+rccl" not in s and "+msg" not in s
-                   and nv.model_features(s, world, float(nbytes), links) is not None]
-    rows = [{"spec": s, "bytes": nbytes, "us": timings[s] * 1e6} for s in model_specs]
+                   and nv.model_features(s, world, float(nbytes), links, esize) is not None]
+    rows = [{"spec": s, "bytes": nbytes, "us": timings[s] * 1e6, "esize": esize} for s in model_specs]
     table, wrong = [], []
 
     def t_of(fn, iters):
-        fn()
-        torch.cuda.synchronize()
+        failed = 0.0
+        try:
+            fn()
+            torch.cuda.synchronize()
+        except nv.FlexarError:
+            failed = 1.0
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
-        for _ in range(iters):
-            fn()
-        torch.cuda.synchronize()
-        return max_over_ranks(time.perf_counter() - t0) / iters
+        try:
+            if not failed:
+                for _ in range(iters):
+                    fn()
+                torch.cuda.synchronize()
+        except nv.FlexarError:
+            failed = 1.0
+        dt = max_over_ranks(time.perf_counter() - t0 + (1e9 if failed else 0.0))
+        return None if dt >= 1e9 else dt / iters
 
     broken = None
     for b in CALIB_SIZES:
@@ -649,13 +842,17 @@ def calibrate_model(comm, timings, nbytes, esize, world, x, y, op, dist, max_ove
             failed = max_over_ranks(failed)
             if failed:
                 wrong.append(f"{s}@{b}" + (" (error)" if failed >= 1.0 else f" (rel err {err:.3g})"))
-                if failed >= 1.0:  # the communicator may be inconsistent now: the caller rebuilds it
+                if failed >= 1.0:  # the communicator may be inconsistent now: stop the sweep here
                     broken = f"{s} at {b} B"
                     break
                 continue
             t = t_of(lambda: comm.all_reduce(xv, out=yv, op=op, algo=s), iters)
-            if "+rccl" not in s and nv.model_features(s, world, float(b), links) is not None:
-                rows.append({"spec": s, "bytes": b, "us": t * 1e6})
+            if t is None:
+                wrong.append(f"{s}@{b} (timed call failed)")
+                broken = f"{s} at {b} B"
+                break
+            if "+rccl" not in s and nv.model_features(s, world, float(b), links, esize) is not None:
+                rows.append({"spec": s, "bytes": b, "us": t * 1e6, "esize": esize})
             if t < best_t:
                 best, best_t = s, t
         if broken:
@@ -665,7 +862,8 @@ def calibrate_model(comm, timings, nbytes, esize, world, x, y, op, dist, max_ove
         if with_rccl:
             z = xv.clone()
             tr = t_of(lambda: dist.all_reduce(z), iters)
-            row.update(rccl_us=round(tr * 1e6, 1), rccl_busbw=round(busbw_gbps(b, tr, world), 2))
+            row.update(rccl_us=round(tr * 1e6, 1) if tr else None,
+                       rccl_busbw=round(busbw_gbps(b, tr, world), 2) if tr else None)
         table.append(row)
         log(rank, "calibration sweep", json.dumps(row))
     out = {"sweep_vs_rccl": table, "wrong": wrong or None, "broken": broken}
@@ -674,13 +872,13 @@ def calibrate_model(comm, timings, nbytes, esize, world, x, y, op, dist, max_ove
     except ValueError as e:
         out["error"] = str(e)
         return out
-    feats = {s: nv.model_features(s, world, float(nbytes), links) for s in model_specs}
+    feats = {s: nv.model_features(s, world, float(nbytes), links, esize) for s in model_specs}
     theta = (fit["alpha_launch_us"], fit["alpha_sync_us"], 1.0 / fit["link_gbps"], 1.0 / fit["hbm_gbps"])
     pick = min(model_specs, key=lambda s: sum(f * t for f, t in zip(feats[s], theta)))
     best = min(timings, key=timings.get)
     out.update({"FLEXAR_MODEL": fit["FLEXAR_MODEL"], "rows": fit["rows"],
                 "median_rel_err": round(fit["median_rel_err"], 3), "max_rel_err": round(fit["max_rel_err"], 3),
-                "winner_agreement": round(fit["winner_agreement"], 2),
+                "winner_agreement": round(fit["winner_agreement"], 2), "max_regret": round(fit["max_regret"], 3),
                 "fitted_choice": pick, "fitted_choice_us": round(timings[pick] * 1e6, 1),
                 "tuner_best": best, "tuner_best_us": round(timings[best] * 1e6, 1), "sizes": fit["sizes"]})
     log(rank, f"calibration: FLEXAR_MODEL={fit['FLEXAR_MODEL']} median rel err {out['median_rel_err']}, "
@@ -694,19 +892,17 @@ def parse_bytes(v: str) -> int:
     return int(float(v[:-1]) * mult[v[-1]]) if v and v[-1] in mult else int(float(v))
 
 
-def run_sweep(args, comm, world, rank, dev, dtype, op, dist, max_over_ranks):
-    """busbw vs bytes, flexar (cost-model 'auto' choice) vs RCCL — BASELINE config #4. Every size is also a
-    correctness check: rank r's input is (i mod 251) + r, whose sum N (i mod 251) + N (N - 1) / 2 is exact in
+def run_sweep(comm, world, rank, dev, dtype, op, dist, max_over_ranks, lo, hi, with_rccl, timed_fn, sweep_out=""):
+    """busbw vs bytes, flexar (the selector's 'auto' choice) vs RCCL - BASELINE config #4. Every size is also
+    a correctness check: rank r's input is (i mod 251) + r, whose sum N (i mod 251) + N (N - 1) / 2 is exact in
     every dtype used here and computed locally (no reference collective on multi-GiB buffers)."""
     import torch
 
     from allreduce_over_mpi_amd.utils.perf import busbw_gbps
 
-    lo, hi = (parse_bytes(t) for t in args.sweep.split(":"))
     es = torch.tensor([], dtype=dtype).element_size()
     rows = []
-    b = lo
-    while b <= hi:
+    for b in _x4(lo, hi):
         n = max(1, b // es)
         pat = torch.remainder(torch.arange(n, device=dev, dtype=torch.int32), 251)
         x = (pat + rank).to(dtype)
@@ -714,38 +910,28 @@ def run_sweep(args, comm, world, rank, dev, dtype, op, dist, max_over_ranks):
         del pat
         y = torch.empty_like(x)
         iters = max(3, min(50, int(2e8 // max(b, 1))))
-
-        def t_of(fn):
-            for _ in range(2):
-                fn()
-            torch.cuda.synchronize()
-            if world > 1:
-                dist.barrier()
-            t0 = time.perf_counter()
-            for _ in range(iters):
-                fn()
-            torch.cuda.synchronize()
-            return max_over_ranks(time.perf_counter() - t0) / iters
-
-        tf = t_of(lambda: comm.all_reduce(x, out=y, op=op))
+        tf = timed_fn(lambda: comm.all_reduce(x, out=y, op=op), iters, 2)
         # integers up to 2^24 (fp32) / 2048 (fp16) / 256 (bf16) are exact, and so is every partial sum below them
         limit = {torch.float32: 1 << 24, torch.float16: 2048, torch.bfloat16: 256}.get(dtype, 0)
         exact = op == "sum" and 250 * world + world * (world - 1) // 2 <= limit
-        ok = max_over_ranks(0.0 if torch.equal(y.float(), want) else 1.0) == 0.0 if exact else None  # every rank
-        row = {"bytes": n * es, "algo": comm.describe(n, dtype).split(" ")[0], "flexar_us": round(tf * 1e6, 2),
-               "flexar_busbw": round(busbw_gbps(n * es, tf, world), 2), "correct": ok}
+        ok = None
+        if exact:  # every rank's result, agreed on by every rank
+            ok = max_over_ranks(0.0 if tf is not None and torch.equal(y.float(), want) else 1.0) == 0.0
+        row = {"bytes": n * es, "algo": comm.describe(n, dtype).split(" ")[0],
+               "flexar_us": round(tf * 1e6, 2) if tf else None,
+               "flexar_busbw": round(busbw_gbps(n * es, tf, world), 2) if tf else None, "correct": ok}
         del want
-        if world > 1 and dtype != torch.float8_e4m3fn and not args.no_rccl:
-            tr = t_of(lambda: dist.all_reduce(x))
-            row.update(rccl_us=round(tr * 1e6, 2), rccl_busbw=round(busbw_gbps(n * es, tr, world), 2))
+        if with_rccl and world > 1:
+            tr = timed_fn(lambda: dist.all_reduce(x), iters, 2)
+            row.update(rccl_us=round(tr * 1e6, 2) if tr else None,
+                       rccl_busbw=round(busbw_gbps(n * es, tr, world), 2) if tr else None)
         rows.append(row)
         log(rank, "sweep", json.dumps(row))
-        if rank == 0 and args.sweep_out:
-            with open(args.sweep_out, "a") as f:
-                f.write(json.dumps(dict(row, n_gpus=world, dtype=args.dtype)) + "\n")
+        if rank == 0 and sweep_out:
+            with open(sweep_out, "a") as f:
+                f.write(json.dumps(dict(row, n_gpus=world, dtype=str(dtype).replace("torch.", ""))) + "\n")
         del x, y
-        b *= 4
-    return rows
+    return {"rows": rows} if rows else {"rows": []}
 
 
 if __name__ == "__main__":

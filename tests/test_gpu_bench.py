@@ -43,3 +43,45 @@ def test_bench_json_and_fallback_chain_two_ranks(cuda):
     assert len(rejected) == 1 and "FLEXAR_BENCH_REJECT_FIRST" in next(iter(rejected.values())), rejected
     assert out["fallback"] is None and out["config"]["algorithm"] not in rejected, out["config"]
     assert out["readiness"]["disabled"] == "", out["readiness"]  # the rebuilt communicator kept every family
+
+
+def _bench(extra_env, args, timeout=300):
+    env = dict(os.environ, FLEXAR_BENCH_SHARED_GPU="1", FLEXAR_BENCH_SHARED_RCCL="1", FLEXAR_NO_BUILD="1", **extra_env)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", *args]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=REPO)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_baseline_config_sections(cuda):
+    """Configs #3 / #4 / #5 ride along in the same JSON line (small buffers here; the driver's run uses the
+    BASELINE sizes): each next to RCCL, with correctness."""
+    out = _bench({}, ["--size-mb", "16", "--config3-mb", "16", "--config4-max", "1M", "--config5-mb", "16",
+                      "--no-calibrate"])
+    c3, c4, c5 = out["config3"], out["config4"], out["config5"]
+    assert set(c3["variants"]) == {"rhd+pull+f32", "rhd+pull+rw", "auto"}, c3
+    for v in c3["variants"].values():
+        assert v.get("correct") is True and v["busbw_GBps"] > 0, c3
+    assert c3["rccl"]["busbw_GBps"] > 0
+    sizes = [r["bytes"] for r in c4["rows"]]
+    assert sizes == [4096, 16384, 65536, 262144, 1048576], c4
+    assert all(r["correct"] is True and r["rccl_busbw"] for r in c4["rows"]), c4
+    assert c5["correct"] is True and c5["max_rel_err"] < 0.13 and c5["rccl_fp32_avg_busbw_GBps"] > 0, c5
+    assert out["dropped"] is None and out["bench_wall_s"] > 0 and out["budget_s"] == 400
+    assert out["readiness"]["calibration"]["source"] in ("measured", "cache"), out["readiness"]
+
+
+def test_bench_budget_drops_in_order(cuda):
+    """A budget that is already spent: every optional item and companion section is dropped and listed,
+    the headline still runs and the JSON line still comes out."""
+    out = _bench({"FLEXAR_BENCH_BUDGET_S": "1"}, ["--size-mb", "16", "--config3-mb", "16", "--config4-max", "1M",
+                                                   "--config5-mb", "16"])
+    items = [d["item"] for d in out["dropped"]]
+    assert items[0] == "grid_sweep" and "cost_model_fit" in items, items
+    for k in ("config3", "config4", "config5", "small_msg"):
+        assert k in items and k not in out, (k, items)
+    assert out["value"] > 0 and out["cost_model_fit"] is None and out["bench_wall_s"] > 1
