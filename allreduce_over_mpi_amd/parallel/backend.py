@@ -54,6 +54,19 @@ def _redop_name(op) -> str | None:
     return None
 
 
+buf_missing = None  # a registration the communicator already dropped: not "only referred to"
+
+
+def _only_registration_refers(t) -> bool:
+    """True when nothing but the registration holding ``t`` refers to its memory: one reference to the
+    tensor (the registration's) and no other tensor or view on its storage (the storage's count is the
+    tensor's plus the temporary storage object of this query)."""
+    try:
+        return t._use_count() == 1 and torch._C._storage_Use_Count(t.untyped_storage()._cdata) == 2
+    except Exception:  # noqa: BLE001 - an API this torch lacks: never deregister on a guess
+        return False
+
+
 def _done_work(result):
     fut = torch.futures.Future()
     fut.set_result(result)
@@ -80,16 +93,22 @@ class FlexarProcessGroup(dist.ProcessGroup):
         self._streams = {}
         self.hierarchical = False
         self._grid = int(os.environ.get("FLEXAR_PG_GRID", "0") or 0)  # executor workgroups (0 = auto)
-        # zero copy for persistent buffers (DDP gradient buckets): during the first FLEXAR_PG_ZC_PROBES
-        # allreduces every rank agrees (one host MIN over gloo) whether its tensor is new and >= 1 MiB, and
-        # such tensors are registered collectively; later calls on them then switch to "+zc+push" by
-        # themselves (comm.hip, FLEXAR_ZC_AUTO). The probe count is the same on every rank, so the
-        # agreement round never diverges. Opt-in (FLEXAR_PG_ZC=1): a registration keeps its buffer alive,
-        # so buffers DDP replaces (its bucket rebuild after the first iteration) stay allocated.
-        self._zc_on = os.environ.get("FLEXAR_PG_ZC", "0") == "1"
+        # zero copy for persistent buffers (DDP gradient buckets), on by default (FLEXAR_PG_ZC=0 turns it
+        # off): during the first FLEXAR_PG_ZC_PROBES allreduces every rank agrees (one host MIN over gloo)
+        # whether its tensor is new and >= 1 MiB, and such tensors are registered collectively; later calls
+        # on them then switch to "+zc+push" by themselves (comm.hip, FLEXAR_ZC_AUTO). A registration keeps
+        # its tensor (so its memory cannot be reused under the peers' mappings); every FLEXAR_PG_ZC_SWEEP
+        # allreduces the ranks agree which registered tensors nothing but the registration refers to any more
+        # (DDP's bucket rebuild after the first iteration drops its first buckets) and deregister them
+        # together, which frees them and re-opens the probe for their replacements. Probe and sweep run at
+        # the same call counts on every rank, so the agreement rounds never diverge.
+        self._zc_on = os.environ.get("FLEXAR_PG_ZC", "1") == "1"
         self._zc_probes_left = int(os.environ.get("FLEXAR_PG_ZC_PROBES", "64") or 0)
         self._zc_seen = set()  # (data_ptr, nbytes) registered by this process group
+        self._zc_regs = []     # [(data_ptr, nbytes), registration id, tensor] in registration order
         self._zc_min = int(os.environ.get("FLEXAR_PG_ZC_MIN_BYTES", str(1 << 20)))
+        self._zc_sweep_every = max(1, int(os.environ.get("FLEXAR_PG_ZC_SWEEP", "32") or 32))
+        self._ar_calls = 0
 
     # ------------------------------------------------------------------ plumbing
     def getBackendName(self):
@@ -178,6 +197,10 @@ class FlexarProcessGroup(dist.ProcessGroup):
             return self._fallback(tensor_list).allreduce(tensor_list, opts)
         dev = tensor_list[0].device
         comm = self.comm(dev.index)
+        self._ar_calls += 1
+        if (self._zc_regs and self._ar_calls % self._zc_sweep_every == 0
+                and not torch.cuda.is_current_stream_capturing()):
+            self._zc_sweep(comm)
         if (self._zc_on and self._zc_probes_left > 0 and not self.hierarchical and self._world > 1
                 and not torch.cuda.is_current_stream_capturing()):  # no registration inside a graph capture
             self._zc_probe(comm, tensor_list)
@@ -216,11 +239,34 @@ class FlexarProcessGroup(dist.ProcessGroup):
         if int(flag.item()) != 1:
             return
         try:
-            comm.register(t)  # collective; the allocation is mapped by the peers
+            rid = comm.register(t)  # collective; the allocation is mapped by the peers
             self._zc_seen.add(key)
+            self._zc_regs.append([key, rid, t])
             self.stats["zc_registrations"] = self.stats.get("zc_registrations", 0) + 1
         except nv.FlexarError:  # refused on every rank together (readiness check, allocation cap): staging
             self._zc_on = False
+
+    def _zc_sweep(self, comm):
+        """Collective: deregister the registered tensors that no rank uses any more (only the registration
+        refers to them on every rank), so DDP's replaced buckets are freed instead of pinned."""
+        dead = torch.tensor([1 if _only_registration_refers(r[2]) else 0 for r in self._zc_regs], dtype=torch.int32)
+        o = AllreduceOptions()
+        o.reduceOp = dist.ReduceOp.MIN
+        self._gloo.allreduce([dead], o).wait()
+        freed = 0
+        for i in reversed(range(len(self._zc_regs))):
+            if int(dead[i]) == 1:
+                key, rid, _ = self._zc_regs.pop(i)
+                comm.deregister(rid)
+                self._zc_seen.discard(key)
+                freed += 1
+        if freed:
+            self.stats["zc_deregistrations"] = self.stats.get("zc_deregistrations", 0) + freed
+            self._zc_probes_left = max(self._zc_probes_left, 16)  # their replacements get registered
+
+    def zc_registered_bytes(self) -> int:
+        """Bytes currently held by zero-copy registrations of this process group."""
+        return sum(k[1] for k, _, _ in self._zc_regs)
 
     def _side_stream(self, dev):
         s = self._streams.get(dev.index)
@@ -427,6 +473,9 @@ class FlexarHookState:
         self.zero_copy = bool(zero_copy) and self.comm.world_size > 1 and hasattr(self.comm, "register")
         self._bucket_regs = {}  # bucket index -> (data_ptr, nbytes, registration id)
         self.registrations = 0  # buckets registered so far (first sight + DDP's one bucket rebuild)
+        self.deregistrations = 0
+        self._last_index = -1
+        self._iteration = 0
         grid = grid if grid is not None else int(os.environ.get("FLEXAR_HOOK_GRID", "0") or 0)
         if grid and hasattr(self.comm, "set_grid"):
             self.comm.set_grid(grid)
@@ -436,6 +485,11 @@ class FlexarHookState:
         if not self.zero_copy or buf.data_ptr() % 16:
             return self.algo
         key = bucket.index()
+        if key <= self._last_index:  # a new iteration: DDP calls the hook in bucket order
+            self._iteration += 1
+            if self._bucket_regs and (self._iteration <= 4 or self._iteration % 50 == 0):
+                self._sweep()
+        self._last_index = key
         nbytes = buf.numel() * buf.element_size()
         have = self._bucket_regs.get(key)
         if have is None or have[0] != buf.data_ptr() or have[1] != nbytes:
@@ -449,6 +503,20 @@ class FlexarHookState:
                 return self.algo
         proto = "+wt" if self.algo and "+wt" in self.algo else "+nts" if self.algo and "+nts" in self.algo else ""
         return "flat+zc+push" + proto
+
+    def _sweep(self):
+        """Collective (at the same iteration boundaries on every rank): drop the registrations of buckets DDP
+        no longer uses - a rebuild with fewer buckets leaves indices that never come back - once every rank
+        agrees that only the registration still refers to them."""
+        keys = sorted(self._bucket_regs)
+        regs = self.comm._regs
+        mine = bytes(1 if _only_registration_refers(regs.get(self._bucket_regs[k][2], buf_missing)) else 0
+                     for k in keys)
+        rows = self.comm._exchange(mine)
+        for i, k in enumerate(keys):
+            if all(len(r) == len(keys) and r[i] == 1 for r in rows):
+                self.comm.deregister(self._bucket_regs.pop(k)[2])
+                self.deregistrations += 1
 
     def stream(self, dev):
         s = self._streams.get(dev.index)

@@ -36,7 +36,14 @@ def _fallback_env(rank, fallback):
 def _train(rank, world, port, q, mode, model_kind="mlp", fallback="gloo"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
-                          FLEXAR_TIMEOUT_MS="20000", FLEXAR_PG_ZC="1", FLEXAR_PG_ZC_MIN_BYTES="65536")  # GPT-tiny buckets register
+                          FLEXAR_TIMEOUT_MS="20000", FLEXAR_PG_ZC_MIN_BYTES="65536")  # GPT-tiny buckets register
+        if mode == "backend_zcdefault":  # the backend's defaults: zero copy on, sweeps every 32 calls
+            os.environ.pop("FLEXAR_PG_ZC", None)
+            mode = "backend"
+            steps, report_regs = 8, True
+        else:
+            os.environ["FLEXAR_PG_ZC"] = "1"
+            steps, report_regs = 4, False
         _fallback_env(rank, fallback)
         import torch.distributed as dist
         import torch.nn as nn
@@ -74,7 +81,7 @@ def _train(rank, world, port, q, mode, model_kind="mlp", fallback="gloo"):
             out = m(x)
             return nn.functional.cross_entropy(out.reshape(-1, out.shape[-1]), y.reshape(-1))
 
-        for step in range(4):
+        for step in range(steps):
             if model_kind == "mlp":
                 x = torch.randn(16 * world, 64, generator=g).to(dev)
                 y = torch.randn(16 * world, 16, generator=g).to(dev)
@@ -98,6 +105,11 @@ def _train(rank, world, port, q, mode, model_kind="mlp", fallback="gloo"):
             used = 0  # the gradient buckets must have been registered (zero copy) by the backend's probe
         if mode == "zchook" and not state._bucket_regs:
             used = 0  # the zero-copy path must actually have registered the buckets
+        if report_regs:
+            pbytes = sum(p.numel() * p.element_size() for p in model.parameters())
+            used = {"calls": used, "registered_bytes": pg.zc_registered_bytes(), "param_bytes": pbytes,
+                    "registrations": pg.stats.get("zc_registrations", 0),
+                    "deregistrations": pg.stats.get("zc_deregistrations", 0)}
         dist.destroy_process_group()
         # numpy arrays travel by value (a torch CPU tensor would be shared through a descriptor of this exiting process)
         q.put((rank, err, used, None, [p.detach().cpu().numpy() for p in model.parameters()]))
@@ -155,6 +167,22 @@ def test_ddp_flexar_backend_matches_rccl_ddp(cuda):
     for r in range(2):
         for a, b in zip(ours[r], rccl[r]):
             assert (a == b).all(), (r, abs(a - b).max())
+
+
+def test_backend_zero_copy_default_stays_bounded(cuda):
+    """init_process_group("flexar") with the defaults (zero copy on): DDP's gradient
+    buckets are registered, DDP's bucket rebuild after the first iteration leaves the first buckets to the
+    registrations alone, and the collective sweep frees them - the registered bytes stay within one set of
+    buckets - while training stays bit-identical to DDP over RCCL."""
+    ours = _spawn(_train, 2, "backend_zcdefault", "gpt", "nccl")
+    rccl = {r: params for r, _, _, tb, params in _spawn(_train, 2, "nccl", "gpt", "nccl") if tb is None}
+    for rank, err, info, tb, params in ours:
+        assert tb is None, tb
+        assert info["calls"] > 0 and info["registrations"] > 0, info
+        # one bucket set: at most the gradients' bytes (+ one bucket of rounding), never both sets pinned
+        assert info["registered_bytes"] <= info["param_bytes"] + (1 << 20), info
+        for a, b in zip(params, rccl[rank]):
+            assert (a == b).all(), (rank, abs(a - b).max())
 
 
 def _colls(rank, world, port, q, fallback="gloo"):
