@@ -97,7 +97,7 @@ class FlexarProcessGroup(dist.ProcessGroup):
         # off): during the first FLEXAR_PG_ZC_PROBES allreduces every rank agrees (one host MIN over gloo)
         # whether its tensor is new and >= 1 MiB, and such tensors are registered collectively; later calls
         # on them then switch to "+zc+push" by themselves (comm.hip, FLEXAR_ZC_AUTO). A registration keeps
-        # its tensor (so its memory cannot be reused under the peers' mappings); every FLEXAR_PG_ZC_SWEEP
+        # its tensor (so its memory cannot be reused under the peers' mappings); every FLEXAR_PG_ZC_SWEEP (16)
         # allreduces the ranks agree which registered tensors nothing but the registration refers to any more
         # (DDP's bucket rebuild after the first iteration drops its first buckets) and deregister them
         # together, which frees them and re-opens the probe for their replacements. Probe and sweep run at
@@ -107,7 +107,7 @@ class FlexarProcessGroup(dist.ProcessGroup):
         self._zc_seen = set()  # (data_ptr, nbytes) registered by this process group
         self._zc_regs = []     # [(data_ptr, nbytes), registration id, tensor] in registration order
         self._zc_min = int(os.environ.get("FLEXAR_PG_ZC_MIN_BYTES", str(1 << 20)))
-        self._zc_sweep_every = max(1, int(os.environ.get("FLEXAR_PG_ZC_SWEEP", "32") or 32))
+        self._zc_sweep_every = max(1, int(os.environ.get("FLEXAR_PG_ZC_SWEEP", "16") or 16))
         self._ar_calls = 0
 
     # ------------------------------------------------------------------ plumbing

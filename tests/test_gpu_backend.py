@@ -37,8 +37,9 @@ def _train(rank, world, port, q, mode, model_kind="mlp", fallback="gloo"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
                           FLEXAR_TIMEOUT_MS="20000", FLEXAR_PG_ZC_MIN_BYTES="65536")  # GPT-tiny buckets register
-        if mode == "backend_zcdefault":  # the backend's defaults: zero copy on, sweeps every 32 calls
+        if mode == "backend_zcdefault":  # the backend's defaults: zero copy on (sweeps every 4 calls here)
             os.environ.pop("FLEXAR_PG_ZC", None)
+            os.environ["FLEXAR_PG_ZC_SWEEP"] = "4"
             mode = "backend"
             steps, report_regs = 8, True
         else:
@@ -181,6 +182,7 @@ def test_backend_zero_copy_default_stays_bounded(cuda):
         assert info["calls"] > 0 and info["registrations"] > 0, info
         # one bucket set: at most the gradients' bytes (+ one bucket of rounding), never both sets pinned
         assert info["registered_bytes"] <= info["param_bytes"] + (1 << 20), info
+        assert info["deregistrations"] > 0, info  # DDP's first bucket set was freed after its rebuild
         for a, b in zip(params, rccl[rank]):
             assert (a == b).all(), (rank, abs(a - b).max())
 
