@@ -173,6 +173,39 @@ int flexar_comm_create(int rank, int nranks, int device, size_t workspace_bytes,
 
 size_t flexar_handle_size(void) { return sizeof(CommHandle); }
 
+// The IPC handle of a communicator buffer. On ROCm 7 with dmabuf IPC, exporting a fresh allocation that
+// landed at the virtual address of an earlier, exported and since freed allocation (a previous
+// communicator of this process) intermittently fails with "invalid argument" (seen once in a 4-process
+// test on one GPU). The buffer is then replaced by a new allocation made while the old one is still held -
+// so it cannot come back at the same address - and the export is retried.
+static int exportable(flexar_comm* c, char** buf, size_t bytes, bool uncached, hipIpcMemHandle_t* h, const char* what) {
+  std::vector<char*> held;
+  hipError_t e = hipSuccess;
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    e = hipIpcGetMemHandle(h, *buf);
+    if (e == hipSuccess) break;
+    (void)hipGetLastError();
+    logf(LOG_WARN, c->rank, "export: hipIpcGetMemHandle(%s) failed (%s); re-allocating the %s", what,
+         hipGetErrorString(e), what);
+    char* nb = nullptr;
+    hipError_t a = uncached ? hipExtMallocWithFlags((void**)&nb, bytes, hipDeviceMallocUncached) : hipMalloc(&nb, bytes);
+    if (a != hipSuccess || hipMemset(nb, 0, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      if (nb) (void)hipFree(nb);
+      break;
+    }
+    held.push_back(*buf);
+    *buf = nb;
+  }
+  (void)hipDeviceSynchronize();
+  for (char* p : held) (void)hipFree(p);
+  if (e != hipSuccess) {
+    set_error(std::string("comm_export: hipIpcGetMemHandle(") + what + "): " + hipGetErrorString(e));
+    return FLEXAR_ERR_HIP;
+  }
+  return 0;
+}
+
 int flexar_comm_export(flexar_comm_t c, void* handle_out) {
   if (!c || !handle_out) { set_error("null argument"); return FLEXAR_ERR_INVALID; }
   FX_HIP(hipSetDevice(c->device));
@@ -183,8 +216,11 @@ int flexar_comm_export(flexar_comm_t c, void* handle_out) {
   h.rank = c->rank;
   h.nranks = c->nranks;
   h.ws_bytes = c->ws_bytes;
-  FX_HIP(hipIpcGetMemHandle(&h.stg, c->stg));
-  FX_HIP(hipIpcGetMemHandle(&h.flags, c->flags));
+  int rc = exportable(c, &c->stg, c->ws_bytes, false, &h.stg, "workspace");
+  if (!rc) rc = exportable(c, (char**)&c->flags, kFlagWords * sizeof(uint64_t), true, &h.flags, "flags");
+  if (rc) return rc;
+  c->peer_stg[c->rank] = c->stg;
+  c->peer_flags[c->rank] = c->flags;
   h.pid = (int32_t)getpid();
   h.device = c->device;
   gethostname(h.host, sizeof(h.host) - 1);
