@@ -42,6 +42,9 @@ def _train(rank, world, port, q, mode, model_kind="mlp", fallback="gloo"):
             os.environ["FLEXAR_PG_ZC_SWEEP"] = "4"
             mode = "backend"
             steps, report_regs = 8, True
+        elif mode == "nccl8":  # the RCCL reference of the 8-step run above
+            mode = "nccl"
+            steps, report_regs = 8, False
         else:
             os.environ["FLEXAR_PG_ZC"] = "1"
             steps, report_regs = 4, False
@@ -176,7 +179,7 @@ def test_backend_zero_copy_default_stays_bounded(cuda):
     registrations alone, and the collective sweep frees them - the registered bytes stay within one set of
     buckets - while training stays bit-identical to DDP over RCCL."""
     ours = _spawn(_train, 2, "backend_zcdefault", "gpt", "nccl")
-    rccl = {r: params for r, _, _, tb, params in _spawn(_train, 2, "nccl", "gpt", "nccl") if tb is None}
+    rccl = {r: params for r, _, _, tb, params in _spawn(_train, 2, "nccl8", "gpt", "nccl") if tb is None}
     for rank, err, info, tb, params in ours:
         assert tb is None, tb
         assert info["calls"] > 0 and info["registrations"] > 0, info
