@@ -569,6 +569,7 @@ int flexar_comm_destroy(flexar_comm_t c) {
     for (uint32_t* p : kv.second->d_chan) (void)hipFree(p);
   }
   if (c->msg_ws) (void)hipFree(c->msg_ws);
+  if (c->msg_epochs) (void)hipFree(c->msg_epochs);
   if (c->nccl && rccl().ok) (void)rccl().CommDestroy(c->nccl);
   if (c->st_buf) (void)hipFree(c->st_buf);
   if (c->cal_dev) (void)hipFree(c->cal_dev);

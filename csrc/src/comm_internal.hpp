@@ -243,6 +243,10 @@ struct flexar_comm {
   bool ipc = true;              // peer workspaces mapped (false: every call runs the message transport)
   ncclComm_t nccl = nullptr;
   char* msg_ws = nullptr;
+  // the message transport's executor segments are local-only programs whose number differs between ranks
+  // for tiny calls (empty blocks): they count calls in their own epoch array, never in `epochs`, which
+  // must advance in lockstep on every rank for the peer-memory protocols
+  uint64_t* msg_epochs = nullptr;
   size_t msg_ws_bytes = 0;
   std::map<std::string, std::unique_ptr<DevMsgPlan>> msg_cache;
   // registered caller buffers (zero-copy "+zc"): every rank registered its buffer of the same size in

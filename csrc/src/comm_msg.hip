@@ -58,6 +58,10 @@ int run_msg(flexar_comm* c, const AlgoSpec& s, Coll coll, const void* in, void* 
   DevMsgPlan* dp = nullptr;
   int rc = get_msg_plan(c, s, count, es, fs, coll, stride, &dp);
   if (rc) return rc;
+  if (!c->msg_epochs) {
+    FX_HIP(hipMalloc(&c->msg_epochs, kMaxGridBlocks * sizeof(uint64_t)));
+    FX_HIP(hipMemset(c->msg_epochs, 0, kMaxGridBlocks * sizeof(uint64_t)));
+  }
   if (dp->plan.stg_bytes > c->msg_ws_bytes) {  // grow (first calls only): nothing of ours may still read it
     FX_HIP(hipDeviceSynchronize());
     if (c->msg_ws) FX_HIP(hipFree(c->msg_ws));
@@ -87,7 +91,7 @@ int run_msg(flexar_comm* c, const AlgoSpec& s, Coll coll, const void* in, void* 
       x.local[BUF_STG] = c->msg_ws;
       for (int r = 0; r < c->nranks; ++r) x.peer_stg[r] = c->msg_ws;  // local-only program
       x.peer_flags[c->rank] = c->flags;
-      x.epochs = c->epochs;
+      x.epochs = c->msg_epochs;  // local-only segment: not part of the cross-rank epoch sequence
       x.stg_half_bytes = 0;
       x.err = c->err_dev;
       x.timeout_ticks = c->timeout_ticks;
@@ -99,7 +103,6 @@ int run_msg(flexar_comm* c, const AlgoSpec& s, Coll coll, const void* in, void* 
       la.stream = st;
       la.proto = PM_FENCE;
       if ((rc = launch_dtype(dtype, op_k, la))) return rc;
-      c->launches++;
       ++ex;
       continue;
     }

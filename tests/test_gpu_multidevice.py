@@ -20,6 +20,7 @@ parities, so a stale staging line cannot go unnoticed):
 """
 import os
 import socket
+import sys
 
 import pytest
 import torch
@@ -120,6 +121,7 @@ def _worker(rank, world, port, shared, q, transport="rccl", no_ipc=False, parts=
             return ((y.double().cpu() - want).abs().max() / (want.abs().max() + 1e-12)).item()
 
         def allreduce_case(spec, dtype, sizes, ops=("sum", "avg"), in_place=False):
+            print(f"[rank {rank}] allreduce {spec} {dtype} {sizes} in_place={in_place}", file=sys.stderr, flush=True)
             for size in sizes:
                 xs = inputs(size, 1, dtype)
                 ref = torch.stack([x.double() for x in xs]).sum(0)

@@ -11,6 +11,8 @@
 //   flexar_plan sweep [NMAX]         reference main.cpp: "#structures,microseconds" per N (CSV to stdout)
 //   flexar_plan dump SPEC N RANK [COUNT]   per-rank op program (Operations::print_ops equivalent)
 //   flexar_plan select N BYTES       the runtime's choice
+//   flexar_plan cost SPEC N BYTES [ESIZE]  what the compiled programs cost (hand-offs, link / HBM bytes)
+//                                    and the model's time, per rank
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -31,7 +33,8 @@ static std::string star(const std::vector<int>& w) {
 
 static int usage() {
   fprintf(stderr,
-          "usage: flexar_plan model N [bytes] | choose N | sweep [NMAX] | dump SPEC N RANK [COUNT] | select N BYTES\n");
+          "usage: flexar_plan model N [bytes] | choose N | sweep [NMAX] | dump SPEC N RANK [COUNT] | select N BYTES |"
+          " cost SPEC N BYTES [ESIZE]\n");
   return 2;
 }
 
@@ -91,6 +94,30 @@ int main(int argc, char** argv) {
     Planner pl(n, r, count, 4, 1.0f);
     if (!pl.build(s, &P, &err)) { fprintf(stderr, "%s\n", err.c_str()); return 1; }
     fputs(dump_program(P, r).c_str(), stdout);
+    return 0;
+  }
+  if (cmd == "cost" && argc >= 5) {
+    AlgoSpec s;
+    std::string err;
+    const int n = atoi(argv[3]);
+    const double bytes = atof(argv[4]);
+    const uint32_t es = argc > 5 ? (uint32_t)atoi(argv[5]) : 4;
+    if (!parse_algo(argv[2], n, &s, &err)) { fprintf(stderr, "%s\n", err.c_str()); return 1; }
+    if (s.kind == AlgoKind::AUTO) s = select_plan(m, n, bytes);
+    if (s.kind == AlgoKind::TREE && s.ag == AgMode::AUTO) s.ag = AgMode::PULL;
+    printf("%s on %d ranks, %.0f bytes of %u-byte elements, %d links: %.2f us\n", s.str().c_str(), n, bytes, es, m.links,
+           m.cost_us(s, n, bytes, es));
+    if (s.kind == AlgoKind::LL || s.kind == AlgoKind::DMA) return 0;
+    printf("%-6s %10s %16s %18s %16s %16s\n", "rank", "handoffs", "link_bytes", "busiest_link_bytes", "hbm_read",
+           "hbm_write");
+    for (int r = 0; r < n; ++r) {
+      Program P;
+      Planner pl(n, r, (uint64_t)(bytes / es), es, 1.0f);
+      if (!pl.build(s, &P, &err)) { fprintf(stderr, "%s\n", err.c_str()); return 1; }
+      const ProgramCost c = program_cost(P, (uint32_t)r, m.links);
+      printf("%-6d %10.0f %16.0f %18.0f %16.0f %16.0f\n", r, c.handoffs, c.link_bytes, c.link_time_bytes, c.hbm_read,
+             c.hbm_write);
+    }
     return 0;
   }
   if (cmd == "select" && argc >= 4) {
