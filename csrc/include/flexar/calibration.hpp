@@ -39,10 +39,14 @@ struct CalibPoint {
   double bytes;
 };
 
+// Every schedule family the selector can pick appears at a bandwidth-bound size too: a oneshot measured
+// only where it is latency-bound leaves its extra HBM bytes (every rank reduces the whole buffer: (2N + 1) S
+// against flat's ~4 S) unpriced, and the selector then picks it for 256 MiB (round-3 rehearsal, N = 2:
+// oneshot 533 us where flat+pull takes 430 us).
 inline std::vector<CalibPoint> calib_points(int nranks) {
-  std::vector<CalibPoint> p = {{"oneshot", 64 << 10},      {"flat+pull", 64 << 10}, {"ring", 256 << 10},
-                               {"oneshot", 1 << 20},       {"flat+pull", 4 << 20},  {"flat+pull", 32 << 20},
-                               {"ring", 32 << 20},         {"flat+push", 32 << 20}};
+  std::vector<CalibPoint> p = {{"oneshot", 64 << 10},  {"flat+pull", 64 << 10}, {"ring", 256 << 10},
+                               {"oneshot", 1 << 20},   {"flat+pull", 4 << 20},  {"flat+pull", 32 << 20},
+                               {"ring", 32 << 20},     {"flat+push", 32 << 20}, {"oneshot", 32 << 20}};
   if (nranks > 2 && !(nranks & (nranks - 1))) p.push_back({"rhd+pull", 32 << 20});
   return p;
 }
@@ -160,7 +164,7 @@ inline XgmiModel model_with_theta(XgmiModel m, const double theta[4]) {
 // Keyed by what the constants depend on: GPU architecture, world size, the agreed link count, the link
 // classes seen (ranks sharing a device time the shared HBM, not links), the protocol families the
 // self-test disabled, the library version and the measurement set's revision.
-constexpr int kCalibRevision = 1;
+constexpr int kCalibRevision = 2;  // 2: oneshot at 32 MiB joined the set
 
 inline std::string calib_key(const std::string& arch, int nranks, int links, const std::string& link_classes,
                              uint32_t disabled, const std::string& version) {
