@@ -27,6 +27,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -59,6 +60,7 @@ constexpr double kLLMaxBytes = 1 << 20;  // LL protocol only for latency-bound s
 // Reference: cost_model/CostModel.h:22-79 - a topology-independent bandwidth term (n-1)/n*s*bo plus a
 // memory term counting read/write steps per layer; both become these per-program counts.
 struct ProgramCost {
+  double stg_bytes = 0;  // staging the program needs per parity half (pieces when it exceeds the workspace)
   double handoffs = 0;
   double link_bytes = 0;
   double link_time_bytes = 0;
@@ -68,6 +70,7 @@ struct ProgramCost {
 
 inline ProgramCost program_cost(const Program& P, uint32_t rank, int links) {
   ProgramCost c;
+  c.stg_bytes = (double)P.stg_bytes();
   const double L = links < 1 ? 1.0 : (double)links;
   auto bytes_of = [&](const Loc& l, uint64_t len) -> double {
     const uint32_t sz = (P.wire && l.buf == BUF_STG && (l.pad & 1)) ? P.wsize : P.esize;
@@ -156,6 +159,7 @@ struct XgmiModel {
   double alpha_dma_us = 15.0;    // copy-engine path: stream fork/join + stream-memory wait/write per phase
   double dma_link_gbps = 50.0;   // one SDMA engine's peer-copy rate
   Partials partials = Partials::FP32;
+  double stg_cap = 0;            // staging bytes one launch may use (the communicator's parity half; 0 = unbounded)
 
   static XgmiModel from_env() {
     XgmiModel m;
@@ -198,7 +202,10 @@ struct XgmiModel {
     if (N > (int)kMaxRanks || s.msg) return analytic_features(s, N, S, f);
     ProgramCost pc;
     if (!cached_cost(s, N, S, esize, &pc)) return false;
-    f[1] = pc.handoffs;
+    // a program larger than the workspace runs as pieces: one launch and one hand-off chain each
+    const double pieces = stg_cap > 0 && pc.stg_bytes > stg_cap ? std::ceil(pc.stg_bytes / stg_cap) : 1.0;
+    f[0] = pieces;
+    f[1] = pc.handoffs * pieces;
     f[2] = pc.link_time_bytes / 1e3;
     f[3] = (pc.hbm_read + pc.hbm_write) / 1e3;
     return true;
@@ -239,6 +246,7 @@ struct XgmiModel {
       Planner pl((uint32_t)N, (uint32_t)r, count, esize, 1.0f);
       if (!pl.build(s, &P, &err)) { ok = false; break; }
       const ProgramCost c = program_cost(P, (uint32_t)r, links);
+      acc.stg_bytes = std::max(acc.stg_bytes, c.stg_bytes);
       acc.handoffs = std::max(acc.handoffs, c.handoffs);
       acc.link_bytes = std::max(acc.link_bytes, c.link_bytes);
       acc.link_time_bytes = std::max(acc.link_time_bytes, c.link_time_bytes);

@@ -164,6 +164,7 @@ int flexar_comm_create(int rank, int nranks, int device, size_t workspace_bytes,
   int rc = alloc_workspace(c.get(), ws);
   if (rc) return rc;
   c->resident = resident_blocks(device);
+  c->model.stg_cap = (double)c->exec_half;  // the selector prices pieces of programs larger than a half
   c->peer_stg[rank] = c->stg;
   c->peer_flags[rank] = c->flags;
   if (nranks == 1) c->connected = true;
@@ -876,7 +877,9 @@ int flexar_comm_reset_model(flexar_comm_t c) {
   if (!c) return FLEXAR_ERR_INVALID;
   std::lock_guard<std::mutex> lk(c->mu);
   const int links = c->model.links;
+  const double cap = c->model.stg_cap;
   c->model = XgmiModel::from_env();
+  c->model.stg_cap = cap;
   if (!c->links_from_env) c->model.links = links;
   c->memo_gen++;
   return 0;
