@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Effective HBM rate of one executor schedule, typed or not: N ranks in one launch on one GPU (LocalGroup),
+ITERS calls of SPEC on MIB MiB per rank, hipEvent-timed; the bytes are the program-cost model's (summed over
+the ranks, csrc/include/flexar/cost_model.hpp program_cost, which matches rocprofv3 FETCH/WRITE counters:
+profiles/r3_pmc_model). Run under `rocprofv3 --kernel-trace --stats` for per-kernel times.
+
+    python3 bench/typed_exec_probe.py SPEC DTYPE       # SPEC "fp8" = all_reduce_fp8 (flat, e4m3 wire, AVG)
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch
+
+    from allreduce_over_mpi_amd import _native as nv
+    from allreduce_over_mpi_amd.parallel import LocalGroup
+
+    spec, dtype = sys.argv[1], sys.argv[2]
+    n = int(os.environ.get("TEP_RANKS", "4"))
+    mib = int(os.environ.get("TEP_MIB", "100"))
+    iters = int(os.environ.get("TEP_ITERS", "10"))
+    dt = getattr(torch, dtype)
+    count = (mib << 20) // dt.itemsize
+    grp = LocalGroup(n, workspace_bytes=6 * (mib << 20) + (64 << 20))
+    g = torch.Generator(device="cuda").manual_seed(1)
+    xs = [torch.randn(count, device="cuda", generator=g).to(dt) for _ in range(n)]
+    ys = [torch.empty_like(x) for x in xs]
+    if spec == "fp8":
+        from allreduce_over_mpi_amd.ops.quant import fp8_amax
+
+        parts = [fp8_amax(x) for x in xs]
+        run = lambda: grp.all_reduce_fp8(xs, op="avg", outs=ys)  # noqa: E731
+        model_spec = "flat+pull+e4m3"
+        del parts
+    else:
+        run = lambda: grp.all_reduce(xs, outs=ys, algo=spec)  # noqa: E731
+        model_spec = spec
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        run()
+    b.record()
+    torch.cuda.synchronize()
+    us = a.elapsed_time(b) * 1e3 / iters
+    rd = wr = 0.0
+    for r in range(n):
+        c = nv.program_cost(model_spec, r, n, count, dtype, links=1)
+        rd += c["hbm_read"]
+        wr += c["hbm_write"]
+    grp.check()
+    print(json.dumps({"spec": spec, "dtype": dtype, "ranks": n, "mib_per_rank": mib, "us_per_call": round(us, 1),
+                      "model_hbm_MiB": round((rd + wr) / 2**20, 1),
+                      "effective_TBps": round((rd + wr) / (us * 1e-6) / 1e12, 3)}), flush=True)
+    grp.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -5,8 +5,8 @@ set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(pwd)}"
 cd "$R"; mkdir -p gpurun_out/pmc_model
 export FLEXAR_NO_BUILD=1
-SPECS="flat+pull:float32 flat+push:float32 ring:float32 rhd+pull:float32 tree:2,2+push:float32 oneshot:float32 \
-flat+zc+push:float32 ring+f32:bfloat16 ring+rw:bfloat16 rhd+pull+f32:bfloat16 rhd+pull+rw:bfloat16"
+SPECS="flat+pull@float32 flat+push@float32 ring@float32 rhd+pull@float32 tree:2,2+push@float32 oneshot@float32 \
+flat+zc+push@float32 ring+f32@bfloat16 ring+rw@bfloat16 rhd+pull+f32@bfloat16 rhd+pull+rw@bfloat16"
 run() {  # spec dtype counter
   (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc "$3" --output-format csv \
       -d "$R/gpurun_out/pmc_model/$1_$2_$3" -o run -- python3 "$R/bench/pmc_model_check.py" "$1" "$2" \
@@ -14,7 +14,7 @@ run() {  # spec dtype counter
 }
 rc=0
 for sd in $SPECS; do
-  spec=${sd%%:*}; dt=${sd##*:}
+  spec=${sd%@*}; dt=${sd##*@}
   run "$spec" "$dt" FETCH_SIZE && run "$spec" "$dt" WRITE_SIZE || { rc=$?; break; }
 done
 python3 - <<'PY' > gpurun_out/pmc_model/summary.txt
