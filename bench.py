@@ -63,9 +63,11 @@ sys.path.insert(0, REPO)
 BASELINE_BUSBW_256MIB = 3.15
 CHECK_SCALES = (1.0, 0.5, 0.25)  # powers of two: exact scaling of inputs and of the reference sum
 CALIB_SIZES = (64 << 10, 1 << 20, 8 << 20, 64 << 20)
-# budget fractions: an optional item runs only if the agreed elapsed time is below this share of the budget
-# (the lowest-priority item needs the most headroom, so it is the first to go)
-DROP_AT = {"cost_model_fit": 0.45, "config4_tail": 0.6, "grid_sweep": 0.3}
+# budget fractions: an optional item runs only if the agreed elapsed time is below this share of the budget.
+# A lower share = dropped sooner as the run eats its budget: the calibration mini-sweep first, then config
+# #4's tail sizes, then the grid sweep (priority order; the grid sweep, checked right after the tuner, goes
+# only when the tuner alone has spent three quarters of the budget)
+DROP_AT = {"cost_model_fit": 0.5, "config4_tail": 0.65, "grid_sweep": 0.75}
 COMPANION_AT = 0.85  # config3 / config4 head / config5 / small messages
 
 
