@@ -742,7 +742,7 @@ int flexar_comm_calibrate(flexar_comm_t c, int mode, char* json, size_t jlen) {
   std::string arch = prop.gcnArchName;
   arch = arch.substr(0, arch.find(':'));
   // the settings fingerprint too (grid cap, block size, chunking, tune table change what a schedule costs)
-  char fp[24];
+  char fp[48];
   snprintf(fp, sizeof(fp), ";settings=%016llx", (unsigned long long)comm_fingerprint(c));
   const std::string key = calib_key(arch, c->nranks, c->model.links, link_classes(c), c->disabled, flexar_version()) + fp;
   const std::string dir = calib_dir();
