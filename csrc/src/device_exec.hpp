@@ -90,47 +90,6 @@ __device__ FX_INLINE void st16(char* p, uint4 x) {
 #endif
 }
 
-// 4/8/16-byte global loads/stores into / out of a word array (the typed executor's narrow operands in
-// lane-interleaved groups, xfer_mx): nontemporal loads like ld16, the store policy like st16.
-typedef __attribute__((address_space(1))) unsigned int g_u32;
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(1))) u32x2 g_u32x2;
-template <int B>
-__device__ FX_INLINE void ldw(const char* p, uint32_t* w) {
-  static_assert(B == 4 || B == 8 || B == 16, "4, 8 or 16 bytes");
-  if constexpr (B == 16) {
-    const uint4 v = ld16(p);
-    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-  } else if constexpr (B == 8) {
-#if defined(FLEXAR_NT_LOADS)
-    const u32x2 v = __builtin_nontemporal_load((const g_u32x2*)p);
-#else
-    const u32x2 v = *(const g_u32x2*)p;
-#endif
-    w[0] = v.x; w[1] = v.y;
-  } else {
-#if defined(FLEXAR_NT_LOADS)
-    w[0] = __builtin_nontemporal_load((const g_u32*)p);
-#else
-    w[0] = *(const g_u32*)p;
-#endif
-  }
-}
-template <int B, bool NTS>
-__device__ FX_INLINE void stw(char* p, const uint32_t* w) {
-  static_assert(B == 4 || B == 8 || B == 16, "4, 8 or 16 bytes");
-  if constexpr (B == 16) {
-    st16<NTS>(p, uint4{w[0], w[1], w[2], w[3]});
-  } else if constexpr (B == 8) {
-    const u32x2 v = {w[0], w[1]};
-    if constexpr (NTS) __builtin_nontemporal_store(v, (g_u32x2*)p);
-    else *(g_u32x2*)p = v;
-  } else {
-    if constexpr (NTS) __builtin_nontemporal_store(w[0], (g_u32*)p);
-    else *(g_u32*)p = w[0];
-  }
-}
-
 // Executor protocol modes (template parameter PM of the executor):
 //   PM_FENCE      plain stores; SIGNAL = system release (buffer_wbl2 sc0 sc1), WAIT = system acquire
 //                 (buffer_inv sc0 sc1)
@@ -162,6 +121,53 @@ __device__ FX_INLINE uint4 ld16_sys(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 __device__ FX_INLINE void st16_sys(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 x) {
   u32x4 v = {x.x, x.y, x.z, x.w};
   __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxSys);
+}
+
+// Sub-chunks of a lane-interleaved typed group (xfer_mx): 4, 8 or 16 bytes moved between a buffer and
+// component j of a lane's packed group. The buffer descriptor and the sub-chunk's offset are uniform
+// (SGPRs); the lane's offset is ONE VGPR shared by every sub-chunk and source, so no per-access 64-bit
+// address is kept live. Component indices are compile-time after unrolling, so the group stays in
+// registers. Cache policy: plain (aux 0) or non-temporal (aux 2, "nt") like the global forms.
+__device__ FX_INLINE void set_word(uint4& u, int c, uint32_t x) {
+  if (c == 0) u.x = x;
+  else if (c == 1) u.y = x;
+  else if (c == 2) u.z = x;
+  else u.w = x;
+}
+__device__ FX_INLINE uint32_t get_word(const uint4& u, int c) { return c == 0 ? u.x : c == 1 ? u.y : c == 2 ? u.z : u.w; }
+#if defined(FLEXAR_NT_LOADS)
+constexpr int kAuxLd = 2;
+#else
+constexpr int kAuxLd = 0;
+#endif
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+template <int SB, int N>
+__device__ FX_INLINE void ld_sub(uint4 (&r)[N], int j, __amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
+  static_assert(SB == 4 || SB == 8 || SB == 16, "4, 8 or 16 bytes");
+  if constexpr (SB == 16) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, kAuxLd);
+    r[j] = uint4{v.x, v.y, v.z, v.w};
+  } else if constexpr (SB == 8) {
+    const i32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, kAuxLd);
+    set_word(r[(2 * j) / 4], (2 * j) % 4, (uint32_t)v.x);
+    set_word(r[(2 * j + 1) / 4], (2 * j + 1) % 4, (uint32_t)v.y);
+  } else {
+    set_word(r[j / 4], j % 4, (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, kAuxLd));
+  }
+}
+template <int SB, bool NTS, int N>
+__device__ FX_INLINE void st_sub(__amdgpu_buffer_rsrc_t rd, uint32_t voff, uint32_t soff, const uint4 (&r)[N], int j) {
+  static_assert(SB == 4 || SB == 8 || SB == 16, "4, 8 or 16 bytes");
+  constexpr int aux = NTS ? 2 : 0;
+  if constexpr (SB == 16) {
+    const u32x4 v = {r[j].x, r[j].y, r[j].z, r[j].w};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rd, voff, soff, aux);
+  } else if constexpr (SB == 8) {
+    const i32x2 v = {(int)get_word(r[(2 * j) / 4], (2 * j) % 4), (int)get_word(r[(2 * j + 1) / 4], (2 * j + 1) % 4)};
+    __builtin_amdgcn_raw_buffer_store_b64(v, rd, voff, soff, aux);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b32((int)get_word(r[j / 4], j % 4), rd, voff, soff, aux);
+  }
 }
 template <int B> struct UintOf;
 template <> struct UintOf<1> { using type = uint8_t; };
@@ -570,20 +576,34 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
     constexpr int SE = G / VM;
     const uint64_t span = nt * (uint64_t)G;
     const uint64_t nsg = vec ? n / span : 0;
-    auto ld_sub = [&](int k, uint64_t e0, uint4* raw_k, int j) {
-      uint32_t* w = reinterpret_cast<uint32_t*>(raw_k);
-      if (isw(k)) ldw<SE * (int)sizeof(W)>(s[k] + e0 * sizeof(W), w + j * SE * (int)sizeof(W) / 4);
-      else ldw<SE * (int)sizeof(T)>(s[k] + e0 * sizeof(T), w + j * SE * (int)sizeof(T) / 4);
-    };
+    constexpr int SBT = SE * (int)sizeof(T), SBW = SE * (int)sizeof(W);
+    const uint32_t lt = threadIdx.x * SBT, lw = threadIdx.x * SBW;  // the lane's offset, per element size
     uint64_t sg = 0;
     for (; sg + UU <= nsg; sg += UU) {
+      // descriptors over this iteration's UU super-groups (<= UU * 16 KiB * 4 B: 32-bit offsets)
+      __amdgpu_buffer_rsrc_t bs[K], bd[kMaxDst];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const uint64_t es = isw(k) ? sizeof(W) : sizeof(T);
+        bs[k] = rsrc_of(s[k] + sg * span * es, (uint64_t)UU * span * es);
+      }
+#pragma unroll
+      for (int dd = 0; dd < kMaxDst; ++dd) {
+        if (dd >= nd) continue;
+        const uint64_t es = (dm >> dd) & 1 ? sizeof(W) : sizeof(T);
+        bd[dd] = rsrc_of(d[dd] + sg * span * es, (uint64_t)UU * span * es);
+      }
       uint4 raw[UU][K][VM];
 #pragma unroll
       for (int u = 0; u < UU; ++u)
 #pragma unroll
         for (int k = 0; k < K; ++k)
 #pragma unroll
-          for (int j = 0; j < VM; ++j) ld_sub(k, (sg + u) * span + (j * nt + threadIdx.x) * SE, raw[u][k], j);
+          for (int j = 0; j < VM; ++j) {
+            const uint32_t e0 = (uint32_t)(u * span + j * nt * SE);  // uniform
+            if (isw(k)) ld_sub<SBW>(raw[u][k], j, bs[k], lw, e0 * (uint32_t)sizeof(W));
+            else ld_sub<SBT>(raw[u][k], j, bs[k], lt, e0 * (uint32_t)sizeof(T));
+          }
 #pragma unroll
       for (int u = 0; u < UU; ++u) {
         float acc[G];
@@ -593,13 +613,12 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
           if (dd >= nd) continue;
           uint4 y[VM];
           encode_dst(dd, acc, y);
-          const uint32_t* w = reinterpret_cast<const uint32_t*>(y);
           const bool wide = (dm >> dd) & 1;
 #pragma unroll
           for (int j = 0; j < VM; ++j) {
-            const uint64_t e0 = (sg + u) * span + (j * nt + threadIdx.x) * SE;
-            if (wide) stw<SE * (int)sizeof(W), NTS>(d[dd] + e0 * sizeof(W), w + j * SE * (int)sizeof(W) / 4);
-            else stw<SE * (int)sizeof(T), NTS>(d[dd] + e0 * sizeof(T), w + j * SE * (int)sizeof(T) / 4);
+            const uint32_t e0 = (uint32_t)(u * span + j * nt * SE);
+            if (wide) st_sub<SBW, NTS>(bd[dd], lw, e0 * (uint32_t)sizeof(W), y, j);
+            else st_sub<SBT, NTS>(bd[dd], lt, e0 * (uint32_t)sizeof(T), y, j);
           }
         }
       }

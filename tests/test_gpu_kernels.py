@@ -472,3 +472,47 @@ def test_group_all_to_all(cuda, groups, n):
                         want = torch.cat([ins[r][p * m:(p + 1) * m] for r in range(n)])
                         assert torch.equal(outs[p], want), (spec, dtype, m, p)
     grp.check()
+
+
+@pytest.mark.parametrize("dtype,spec", [(torch.bfloat16, "ring"), (torch.bfloat16, "rhd"), (torch.float16, "tree:2,2+push"),
+                                        (torch.float8_e4m3fn, "ring")])
+def test_group_typed_partials_large_slices(cuda, groups, dtype, spec):
+    """Workgroup slices large enough for the typed executor's lane-interleaved super-groups (>= 512 x G
+    elements per workgroup, device_exec.hpp xfer_mx) plus their contiguous-group and scalar tails: fp32
+    partials still round once (<= 1 ulp of the exact sum) and every rank agrees bit for bit."""
+    n = 4
+    grp = groups[n]
+    g = torch.Generator(device=cuda).manual_seed(5)
+    size = 8 * 1024 * 1024 + 4099  # ~2 M elements per ring block: ~32 K per workgroup at grid 64
+    xs = [(torch.randn(size, device=cuda, generator=g) * (2 if dtype == torch.float8_e4m3fn else 1)).to(dtype)
+          for _ in range(n)]
+    exact = torch.stack([x.double() for x in xs]).sum(0)
+    want = exact.float().clamp(-448, 448).to(dtype) if dtype == torch.float8_e4m3fn else exact.to(dtype)
+    for _ in range(2):
+        outs = grp.all_reduce([x.clone() for x in xs], "sum", algo=spec + "+f32")
+        torch.cuda.synchronize()
+        for o in outs:
+            assert torch.equal(o.view(torch.uint8), outs[0].view(torch.uint8)), "ranks disagree"
+        assert _ulps(outs[0], want) <= 1, _ulps(outs[0], want)
+    grp.check()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_group_fp8_wire_large_slices(cuda, groups, dtype):
+    """The fp8 wire's typed transfers over lane-interleaved super-groups (fp32 / bf16 next to e4m3): bit-exact
+    against the torch emulation of the same arithmetic, as for the small sizes above."""
+    n = 4
+    grp = groups[n]
+    g = torch.Generator(device=cuda).manual_seed(77)
+    xs = [(torch.randn(8 * 1024 * 1024 + 333, device=cuda, generator=g) * (r + 1)).to(dtype) for r in range(n)]
+    amax = max(float(x.float().abs().max()) for x in xs)
+    s = 448.0 / (n * amax * 1.0625)
+    want = _emulate_fp8_flat(xs, s, "avg")
+    for _ in range(2):
+        outs = grp.all_reduce_fp8([x.clone() for x in xs], op="avg")
+        torch.cuda.synchronize()
+        for o in outs:
+            assert torch.equal(o, outs[0]), "ranks disagree"
+        mism = (~torch.isclose(outs[0].float(), want.float(), rtol=1e-5, atol=0)).float().mean().item()
+        assert mism < 2e-3, mism
+    grp.check()
