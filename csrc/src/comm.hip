@@ -509,7 +509,13 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     if (roctx().push) roctx().push(("flexar allreduce " + s.str() + " " + std::to_string(count * es) + "B").c_str());
     c->calls++;
     c->bytes += count * es;
+    std::unique_ptr<DeviceTimer> tm(c->profile ? new DeviceTimer : nullptr);
+    if (tm) tm->start(st);
     rc = run_msg(c, s, Coll::ALLREDUCE, in, out, count, dtype, op, fs, 0, st);
+    if (tm) {
+      tm->stop(st);
+      c->prof_pending.push_back(ProfRec{s.str(), (uint64_t)count * es, std::move(tm)});
+    }
     if (roctx().pop) roctx().pop();
     return rc;
   }
@@ -520,7 +526,13 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     c->bytes += count * es;
     const char* ip = (const char*)in;
     char* op_ = (char*)out;
+    std::unique_ptr<DeviceTimer> tm(c->profile ? new DeviceTimer : nullptr);
+    if (tm) tm->start(st);
     rc = run_dma(&c, 1, &ip, &op_, count, dtype, op, fs, st);
+    if (tm) {
+      tm->stop(st);
+      c->prof_pending.push_back(ProfRec{s.str(), (uint64_t)count * es, std::move(tm)});
+    }
     if (roctx().pop) roctx().pop();
     return rc;
   }
@@ -535,10 +547,16 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     if (roctx().push) roctx().push(("flexar allreduce ll " + std::to_string(count * es) + "B").c_str());
     c->calls++;
     c->bytes += count * es;
+    std::unique_ptr<DeviceTimer> tm(c->profile ? new DeviceTimer : nullptr);
+    if (tm) tm->start(st);
     rc = launch_dtype(dtype, op, la);
     if (!rc) {
       c->launches++;
       remember(0, nullptr, la.grid);
+    }
+    if (tm) {
+      tm->stop(st);
+      c->prof_pending.push_back(ProfRec{s.str(), (uint64_t)count * es, std::move(tm)});
     }
     if (roctx().pop) roctx().pop();
     return rc;
