@@ -23,6 +23,9 @@ from collections import defaultdict
 from .. import _native as nv
 
 
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak: no schedule streams HBM faster (csrc/include/flexar/calibration.hpp)
+
+
 def fit_model(rows, nranks: int, links: int = 0, min_bytes: float = 0.0):
     """Least-squares fit of theta to measured rows ({"spec", "bytes", "us"}). Returns a dict with the
     parameters, the FLEXAR_MODEL string, the rows' relative errors and the winner agreement."""
@@ -46,8 +49,11 @@ def fit_model(rows, nranks: int, links: int = 0, min_bytes: float = 0.0):
     w = 1.0 / y  # relative error
     # column scaling keeps nnls well conditioned (features span microseconds to gigabytes)
     colscale = np.maximum(np.abs(A * w[:, None]).max(axis=0), 1e-30)
-    theta_s, _ = nnls(A * w[:, None] / colscale, y * w)
-    theta = theta_s / colscale
+    # theta >= lb: the HBM term is bounded by the part's peak, as in the native fit (calibration.hpp
+    # kHbmPeakGBps); theta = lb + phi, phi >= 0
+    lb = np.array([0.0, 0.0, 0.0, 1.0 / HBM_PEAK_GBPS])
+    phi_s, _ = nnls(A * w[:, None] / colscale, y * w - (A * w[:, None]) @ lb)
+    theta = lb + phi_s / colscale
     alpha_launch, alpha_sync, inv_link, inv_hbm = (float(v) for v in theta)
     # a parameter the data never exercised (zero column) or fitted to 0 keeps a finite bandwidth
     link_gbps = 1.0 / inv_link if inv_link > 1e-12 else 1e6

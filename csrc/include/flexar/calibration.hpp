@@ -64,7 +64,13 @@ struct CalibFit {
   bool ok = false;
 };
 
-// Least squares with theta >= 0 on the rows' RELATIVE errors (rows weighted by 1 / measured us): the
+// A physical prior on the HBM term: no schedule streams HBM faster than the part's peak (MI355X HBM3E,
+// 8 TB/s), so 1 / hbm_gbps >= 1 / kHbmPeakGBps. Without it, calls whose link and HBM byte counts are nearly
+// proportional (ranks sharing one device: the "links" ARE the HBM) leave the split between the two terms
+// unidentified and the fit may report an unphysical HBM rate (a round-3 rehearsal fitted 12.8 TB/s).
+constexpr double kHbmPeakGBps = 8000.0;
+
+// Least squares with theta >= lb on the rows' RELATIVE errors (rows weighted by 1 / measured us): the
 // non-negative optimum is the unconstrained optimum of the best support, so with four unknowns every
 // support (15 of them) is solved and the best feasible one kept. Columns are scaled to unit max for
 // conditioning. Deterministic: every rank fitting the same rows gets bit-identical theta.
@@ -92,8 +98,12 @@ inline CalibFit fit_theta(const std::vector<CalibRow>& rows, const XgmiModel& ba
     if (scale[j] <= 0) scale[j] = 1;
   for (auto& a : A)
     for (int j = 0; j < 4; ++j) a[j] /= scale[j];
+  // theta = lb + phi with phi >= 0: the lower bounds move to the right-hand side
+  const double lb[4] = {0, 0, 0, 1.0 / kHbmPeakGBps};
+  for (size_t i = 0; i < A.size(); ++i)
+    for (int j = 0; j < 4; ++j) y[i] -= A[i][j] * lb[j] * scale[j];
   double best_res = 1e300;
-  for (int mask = 1; mask < 16; ++mask) {
+  for (int mask = 0; mask < 16; ++mask) {
     int idx[4], k = 0;
     for (int j = 0; j < 4; ++j)
       if (mask & (1 << j)) idx[k++] = j;
@@ -118,7 +128,7 @@ inline CalibFit fit_theta(const std::vector<CalibRow>& rows, const XgmiModel& ba
       }
     }
     if (singular) continue;
-    double t[4] = {0, 0, 0, 0};
+    double t[4] = {0, 0, 0, 0};  // phi (scaled)
     bool feasible = true;
     for (int a = 0; a < k; ++a) {
       t[idx[a]] = M[a][k] / M[a][a];
@@ -133,7 +143,7 @@ inline CalibFit fit_theta(const std::vector<CalibRow>& rows, const XgmiModel& ba
     }
     if (res < best_res) {
       best_res = res;
-      for (int j = 0; j < 4; ++j) out.theta[j] = t[j] / scale[j];
+      for (int j = 0; j < 4; ++j) out.theta[j] = lb[j] + t[j] / scale[j];
       out.ok = true;
     }
   }
@@ -164,7 +174,7 @@ inline XgmiModel model_with_theta(XgmiModel m, const double theta[4]) {
 // Keyed by what the constants depend on: GPU architecture, world size, the agreed link count, the link
 // classes seen (ranks sharing a device time the shared HBM, not links), the protocol families the
 // self-test disabled, the library version and the measurement set's revision.
-constexpr int kCalibRevision = 2;  // 2: oneshot at 32 MiB joined the set
+constexpr int kCalibRevision = 3;  // 2: oneshot at 32 MiB joined the set; 3: HBM term bounded by the peak
 
 inline std::string calib_key(const std::string& arch, int nranks, int links, const std::string& link_classes,
                              uint32_t disabled, const std::string& version) {

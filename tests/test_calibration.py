@@ -143,3 +143,16 @@ def test_probe_agreement_rejects_different_settings():
     assert err and "different settings" in err
     _, err = _agree([_blob(0, 1, views[0]), _blob(1, 1, views[1], magic=1)])
     assert err and "malformed" in err
+
+
+@pytest.mark.parametrize("n,links", [(4, 1), (8, 7)])
+def test_fit_bounds_the_hbm_term_by_the_peak(n, links):
+    """Rows generated with an unphysical HBM rate (20 TB/s, what an unidentified link/HBM split can produce
+    on ranks sharing one device): both fits keep hbm_gbps at or below the part's 8 TB/s peak and agree."""
+    rows = _synthetic((9.0, 3.5, 55.0, 20000.0), n, links)
+    a = nv.calib_fit(rows, n, links)
+    b = fit_model(rows, n, links=links)
+    assert a["hbm_gbps"] <= 8000.0 * (1 + 1e-9), a
+    assert b["hbm_gbps"] <= 8000.0 * (1 + 1e-9), b
+    for k in ("alpha_launch_us", "alpha_sync_us", "link_gbps", "hbm_gbps"):
+        assert a[k] == pytest.approx(b[k], rel=1e-3), (k, a, b)
