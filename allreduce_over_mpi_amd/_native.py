@@ -62,6 +62,7 @@ def _sig(lib):
         "flexar_reduce_host": (i, [vp, c.POINTER(vp), i, sz, i, i, f]),
         "flexar_parse_ft_topo": (i, [cp, i, cp, sz]),
         "flexar_count_factorizations": (u64, [i]),
+        "flexar_ring_order": (i, [i, i, i, vp]),
         "flexar_enumerate_plans": (i, [i, cp, sz]),
         "flexar_model_cost_us": (d, [cp, i, d]),
         "flexar_select_plan": (i, [i, d, cp, sz]),
@@ -228,6 +229,15 @@ def parse_ft_topo(ft_topo: str | None, nranks: int) -> str:
 
 def count_factorizations(n: int) -> int:
     return int(lib().flexar_count_factorizations(n))
+
+
+def ring_order(nranks: int, channel: int, channels: int = 1) -> tuple[list[int], int]:
+    """(rank order of ring ``channel`` of a ``channels``-channel ring, the most channels N ranks allow)."""
+    buf = (ctypes.c_int * nranks)()
+    m = lib().flexar_ring_order(nranks, channel, channels, buf)
+    if m < 0:
+        raise ValueError("bad ring_order arguments")
+    return list(buf), int(m)
 
 
 def enumerate_plans(nranks: int) -> list[str]:

@@ -29,16 +29,23 @@ from .. import _native as nv
 def default_candidates(world: int, nbytes: int, esize: int = 4) -> list[str]:
     """The schedules worth measuring for ``nbytes`` on ``world`` ranks (bench.py, tools/flexar_tune.py and
     ``autotune`` share this list): latency protocols for small buffers, every flat-stage protocol, rings
-    on 1..4 arc-disjoint channels, RHD, the two-stage FlexTree factorizations and the copy engines. The
-    direction-balanced flat ("+bidir") joins the flat protocols: on xGMI its reduce-scatter reads and its
-    all-gather writes share the links' two directions. For 16/8-bit elements (``esize`` < 4) every multi-hop
-    schedule is measured twice: with fp32 partials (the default typed staging, one rounding) and rounded
-    per hop ("+rw", 16-bit partials on the links, up to +43 % fewer link bytes for a ring at N = 8)."""
+    on 1, 2 and 4 arc-disjoint channels and on N - 1 (the full mesh: ``ring:7`` at N = 8), RHD, the
+    two-stage FlexTree factorizations and the copy engines. The direction-balanced flat ("+bidir") joins the
+    flat protocols: on xGMI its reduce-scatter reads and its all-gather writes share the links' two
+    directions. For 16/8-bit elements (``esize`` < 4) every multi-hop schedule is measured twice: with fp32
+    partials (the default typed staging, one rounding) and rounded per hop ("+rw", 16-bit partials on the
+    links, up to +43 % fewer link bytes for a ring at N = 8)."""
     c = ["ll", "oneshot", "oneshot+wt"] if nbytes <= (1 << 20) else (["oneshot"] if nbytes <= (8 << 20) else [])
     c += ["flat+pull", "flat+push", "flat+pull+nts", "flat+push+nts", "flat+pull+wt", "flat+push+wt"]
     c += ["flat+bidir", "flat+bidir+nts", "flat+bidir+wt"]  # both link directions in one XFER
     maxc = len([d for d in range(1, world) if math.gcd(d, world) == 1])
     c += ["ring", "ring+wt"] + [f"ring:{k}{m}" for k in (2, 4) if k <= maxc for m in ("", "+wt")]
+    try:  # every outgoing link: N - 1 arc-disjoint rings where the full decomposition exists (ring:7 at N = 8)
+        full = nv.ring_order(world, 0, 1)[1]
+    except Exception:  # noqa: BLE001 - no native library: the circulant rings only
+        full = maxc
+    if full > 4:
+        c.append(f"ring:{full}")
     if world > 2 and (world & (world - 1)) == 0:
         c.append("rhd+pull")
     if world >= 8 and world % 4 == 0:

@@ -271,6 +271,7 @@ int flexar_direct_links(const int32_t* link_classes, const int32_t* hops, int nr
 int flexar_parse_ft_topo(const char* ft_topo, int nranks, char* out, size_t outlen);
 /* Number of ordered factorizations H(n) (reference topo_count/factor_count.py). */
 uint64_t flexar_count_factorizations(int n);
+int flexar_ring_order(int n, int channel, int C, int* order);
 /* Enumerate candidate plans for nranks as newline separated specs. */
 int flexar_enumerate_plans(int nranks, char* out, size_t outlen);
 /* Cost-model estimate (microseconds) of spec for (nranks, bytes). */

@@ -450,7 +450,7 @@ class Planner {
     for (int c = 0; c < C; ++c) {
       uint64_t c_off = std::min<uint64_t>(count, (uint64_t)c * per);
       uint64_t c_cnt = std::min<uint64_t>(count - c_off, per);
-      std::vector<int> ord = ring_order(N, c);
+      std::vector<int> ord = ring_order(N, c, C);
       uint32_t v = 0;
       for (uint32_t p = 0; p < N; ++p)
         if ((uint32_t)ord[p] == r) v = p;

@@ -18,6 +18,9 @@
 #include <algorithm>
 #include <cctype>
 #include <cstdlib>
+#include <functional>
+#include <map>
+#include <mutex>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -282,20 +285,97 @@ inline int gcd_int(int a, int b) { while (b) { int t = a % b; a = b; b = t; } re
 inline std::vector<int> ring_steps(int nranks) {
   std::vector<int> steps;
   if (nranks <= 1) return steps;
-  // interleave d and N-d so channel pairs use both directions of the same links last
   for (int d = 1; d < nranks; ++d)
     if (gcd_int(d, nranks) == 1) steps.push_back(d);
   return steps;
 }
-// arc-disjoint rings available, capped by the flag-slot budget (2 (N-1) slots per channel)
+
+// The circulant rings stop short of the full mesh when N is composite: at N = 8 only d = 1, 3, 5, 7 are
+// Hamiltonian, so 4 of a GPU's 7 xGMI links carry ring traffic (the even steps split the ranks by parity).
+// The complete digraph on N vertices does split into N - 1 arc-disjoint directed Hamiltonian cycles for
+// every N except 4 and 6 (Tillson, 1980), i.e. N - 1 rings that use every outgoing link of every GPU once.
+// Found by a deterministic backtracking search (cycle k leaves rank 0 over the arc 0 -> k + 1; ~10 us at
+// N = 8, ~60 ms at N = 16 in the worst case measured) with a step budget; empty when none is found (N = 4,
+// 6) or the budget runs out. Every rank computes the same cycles.
+inline std::vector<std::vector<int>> hamiltonian_decomposition(int n, long budget = 4000000) {
+  std::vector<std::vector<int>> cyc;
+  if (n < 2 || n > kMaxRanks) return cyc;
+  std::vector<char> used((size_t)n * n, 0);
+  for (int i = 0; i < n; ++i) used[(size_t)i * n + i] = 1;
+  long steps = 0;
+  std::vector<int> path;
+  std::vector<char> seen(n, 0);
+  // depth-first over (cycle index, partial path); returns true when all n - 1 cycles are placed
+  std::function<bool(int)> cycle_k;
+  std::function<bool(int)> extend = [&](int k) -> bool {
+    if (++steps > budget) return false;
+    const int u = path.back();
+    if ((int)path.size() == n) {
+      if (used[(size_t)u * n]) return false;
+      used[(size_t)u * n] = 1;
+      cyc.push_back(path);
+      if (cycle_k(k + 1)) return true;
+      cyc.pop_back();
+      used[(size_t)u * n] = 0;
+      return false;
+    }
+    for (int v = 1; v < n; ++v) {
+      if (seen[v] || used[(size_t)u * n + v]) continue;
+      used[(size_t)u * n + v] = 1, seen[v] = 1, path.push_back(v);
+      if (extend(k)) return true;
+      path.pop_back(), seen[v] = 0, used[(size_t)u * n + v] = 0;
+      if (steps > budget) return false;
+    }
+    return false;
+  };
+  cycle_k = [&](int k) -> bool {
+    if (k == n - 1) return true;
+    const int first = k + 1;
+    if (used[first]) return false;
+    std::vector<int> saved_path = path;
+    std::vector<char> saved_seen = seen;
+    path = {0, first};
+    std::fill(seen.begin(), seen.end(), 0);
+    seen[0] = seen[first] = 1;
+    used[first] = 1;
+    const bool ok = extend(k);
+    if (!ok) {
+      used[first] = 0;
+      path = saved_path;
+      seen = saved_seen;
+    }
+    return ok;
+  };
+  if (!cycle_k(0)) cyc.clear();
+  return cyc;
+}
+
+// Every rank and every plan of one N uses the same cycles: computed once per N.
+inline const std::vector<std::vector<int>>& full_rings(int n) {
+  static std::mutex mu;
+  static std::map<int, std::vector<std::vector<int>>> memo;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = memo.find(n);
+  if (it == memo.end()) it = memo.emplace(n, hamiltonian_decomposition(n)).first;
+  return it->second;
+}
+
+// arc-disjoint rings available (the full decomposition where it exists, else the circulant ones), capped
+// by the flag-slot budget (2 (N-1) slots per channel)
 inline int max_ring_channels(int nranks) {
   int n = (int)ring_steps(nranks).size();
+  if (nranks > 1) n = std::max(n, (int)full_rings(nranks).size());
   if (nranks > 1) n = std::min(n, (int)kProgSlots / (2 * (nranks - 1)));
   return n < 1 ? 1 : n;
 }
-// order[c][pos] = rank at position pos of ring c
-inline std::vector<int> ring_order(int nranks, int channel) {
+// order[pos] = rank at position pos of ring `channel` of a C-channel ring: the circulant rings while C fits
+// them (the orders every earlier plan used), else the cycles of the full decomposition.
+inline std::vector<int> ring_order(int nranks, int channel, int C = 1) {
   std::vector<int> st = ring_steps(nranks);
+  if (C > (int)st.size() && nranks > 1) {
+    const auto& full = full_rings(nranks);
+    if (C <= (int)full.size()) return full[channel % full.size()];
+  }
   int d = st.empty() ? 1 : st[channel % st.size()];
   std::vector<int> ord(nranks);
   for (int p = 0; p < nranks; ++p) ord[p] = (int)(((long)p * d) % nranks);

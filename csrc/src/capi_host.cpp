@@ -226,6 +226,14 @@ int flexar_parse_ft_topo(const char* ft_topo, int nranks, char* out, size_t outl
 }
 
 uint64_t flexar_count_factorizations(int n) { return count_factorizations(n); }
+// Rank order of ring `channel` of a C-channel ring on n ranks (the planner's ring_order); returns the
+// number of channels a ring on n ranks can have (max_ring_channels), or -1 on bad arguments.
+int flexar_ring_order(int n, int channel, int C, int* order) {
+  if (n < 1 || n > kMaxRanks || channel < 0 || C < 1 || !order) return -1;
+  const std::vector<int> o = ring_order(n, channel, C);
+  for (int i = 0; i < n; ++i) order[i] = o[i];
+  return max_ring_channels(n);
+}
 
 int flexar_enumerate_plans(int nranks, char* out, size_t outlen) {
   std::string s;

@@ -146,7 +146,7 @@ def _ulps(a: torch.Tensor, b: torch.Tensor) -> int:
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float8_e4m3fn])
-@pytest.mark.parametrize("spec", ["ring", "ring:4", "rhd", "tree:2,4", "tree:4,2+push", "tree:2,2,2+pull"])
+@pytest.mark.parametrize("spec", ["ring", "ring:4", "ring:7", "rhd", "tree:2,4", "tree:4,2+push", "tree:2,2,2+pull"])
 def test_group_typed_fp32_partials(cuda, groups, dtype, spec):
     """Multi-hop schedules of 16/8-bit inputs keep partial sums in fp32 staging (exec_mx_kernel with fp32
     wire operands): the device result is within 1 ulp of the exact sum rounded once, i.e. flat's result,

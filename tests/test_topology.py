@@ -132,7 +132,7 @@ def _remote_elems(dump, rank):
 def test_plans_move_bandwidth_optimal_bytes(nv, n):
     """every tree/ring/flat schedule moves 2(N-1)/N * S per rank (the reference's
     'key structural fact'); oneshot moves (N-1) * S. Checked on the compiled programs of every rank."""
-    count = 4096 * n
+    count = 16384 * n  # large enough that 16-element block rounding stays < 1 % (ring:7 splits 7 ways)
     specs = [p for p in nv.enumerate_plans(n) if p.startswith(("tree:", "ring"))]
     specs = [s for s in specs if not s.startswith("tree:") or
              __import__("math").prod(int(w) for w in s[5:].split(",")) == n]  # lonely trees fold extra data
