@@ -50,6 +50,9 @@ def _specs(world):
 
     chans = len([d for d in range(1, world) if __import__("math").gcd(d, world) == 1])
     specs += [f"ring:{c}" for c in (2, 4) if c <= chans]
+    full = nv.ring_order(world, 0, 1)[1]  # N - 1 arc-disjoint rings over the full mesh (ring:7 at N = 8)
+    if full > max(4, chans):
+        specs.append(f"ring:{full}")
     if world == 4:
         specs += ["tree:2,2+push", "tree:2,2+pull", "tree:2,2+push+wt", "rhd+rccl"]
     if world == 8:
