@@ -298,6 +298,18 @@ class Communicator:
             raise nv.FlexarError(1, nv.last_error())
         return float(v)
 
+    def recommended_bucket_bytes(self, efficiency: float = 0.9, zero_copy: bool = False) -> int:
+        """Gradient-bucket size for DDP / FSDP on this node (``DDP(bucket_cap_mb=b / 2**20)``): the smallest
+        size whose allreduce the calibrated selector prices at ``efficiency`` of its 1 GiB bandwidth
+        (utils/perf.py recommend_bucket_bytes). ``zero_copy``: price the registered-buffer form the backend
+        and the DDP hook run on persistent buckets. Identical on every rank (the model is agreed on)."""
+        from ..utils.perf import recommend_bucket_bytes
+
+        if self.world_size < 2:
+            return 1 << 20
+        spec = "flat+zc+push" if zero_copy else "auto"
+        return recommend_bucket_bytes(lambda b: self.predict_us(spec, b), efficiency)
+
     def calibrate(self, rows, install: bool = True) -> dict:
         """Fit the cost model to measured rows ({"spec", "bytes", "us"}: ``autotune``'s or
         tools/flexar_tune.py's) on this node's probed link count, and install it (every rank must pass the

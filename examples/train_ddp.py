@@ -30,7 +30,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--bf16", action="store_true", help="bf16 autocast (gradients stay fp32)")
-    ap.add_argument("--bucket-mb", type=float, default=100.0)
+    ap.add_argument("--bucket-mb", default="100",
+                    help="DDP bucket size in MiB, or 'auto': the smallest bucket the calibrated selector prices at "
+                         "90 %% of its 1 GiB bandwidth on this node (Communicator.recommended_bucket_bytes)")
     args = ap.parse_args()
 
     import torch
@@ -48,7 +50,15 @@ def main():
     cfg = PRESETS[args.model]
     torch.manual_seed(0)
     model = GPT(cfg).to(dev)
-    ddp = DDP(model, device_ids=[local], bucket_cap_mb=args.bucket_mb)
+    if args.bucket_mb == "auto":
+        from allreduce_over_mpi_amd.parallel import Communicator
+
+        probe = Communicator(device=local)  # collective: connect, self-test, calibrated (or cached) model
+        bucket_mb = probe.recommended_bucket_bytes(0.9, zero_copy=args.comm in ("backend", "zchook")) / 2**20
+        probe.close()
+    else:
+        bucket_mb = float(args.bucket_mb)
+    ddp = DDP(model, device_ids=[local], bucket_cap_mb=bucket_mb)
     if args.comm in ("hook", "fp8hook", "zchook"):
         hook = fb.flexar_fp8_compress_hook if args.comm == "fp8hook" else fb.flexar_allreduce_hook
         ddp.register_comm_hook(fb.FlexarHookState(zero_copy=args.comm == "zchook"), hook)
@@ -80,7 +90,8 @@ def main():
     if rank == 0:
         print(json.dumps({"comm": args.comm, "model": args.model, "params": params, "world": world,
                           "tokens_per_s": round(tokens / dt, 1), "ms_per_step": round(dt / args.steps * 1e3, 2),
-                          "final_loss": round(float(loss.item()), 4), "bf16": args.bf16}))
+                          "final_loss": round(float(loss.item()), 4), "bf16": args.bf16,
+                          "bucket_mb": bucket_mb}))
     dist.destroy_process_group()
 
 
