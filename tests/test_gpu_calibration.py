@@ -51,6 +51,7 @@ def _worker(rank, world, port, calib_dir, mode, q):
                 out[f"cal{i}"] = comm.calibration
                 out[f"hash{i}"] = int(comm._lib.flexar_comm_model_hash(comm._h))
                 out[f"topo{i}"] = comm.topology()
+                out[f"bucket{i}"] = (comm.recommended_bucket_bytes(0.9), comm.recommended_bucket_bytes(0.9, True))
                 # the calibrated model's own choice at a few sizes: exact integer sums
                 dev = torch.device("cuda", 0)
                 errs = []
@@ -102,9 +103,12 @@ def test_calibration_measures_caches_and_agrees(cuda, tmp_path, world):
     for r in range(world):
         assert out[r]["hash0"] == r0["hash0"] and out[r]["hash1"] == r0["hash1"]  # identical model everywhere
         assert out[r]["choice0"] == r0["choice0"]
+        assert out[r]["bucket0"] == r0["bucket0"] and out[r]["bucket1"] == r0["bucket1"]  # same bucket everywhere
         for i in range(3):
             assert out[r][f"err{i}"] == 0.0, (r, i, out[r])
             assert out[r][f"topo{i}"]["links_agreed"]
+    for b in r0["bucket0"]:
+        assert (1 << 20) <= b <= (1 << 30) and b % (1 << 20) == 0, r0["bucket0"]
     assert r0["hash0"] == r0["hash1"] != r0["hash2"]  # the cache reproduces the measured constants exactly
     cal = r0["cal0"]
     assert len(cal["rows"]) >= 6 and all(row[2] > 0 for row in cal["rows"])
