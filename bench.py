@@ -338,8 +338,10 @@ def main():
         return err <= tol, err
 
     def timed_fn(fn, iters, warm=1):
-        """Collective: per-call seconds (max over ranks) of fn, or None if it failed on any rank. Exactly one
-        barrier and one agreement on every rank whether or not this rank raised."""
+        """Collective: per-call seconds (max over ranks) of fn, or None if it failed on any rank. Exactly two
+        agreements on every rank whether or not this rank raised: a warm-up failure anywhere skips the timed
+        calls everywhere (the peers would otherwise wait out the device watchdog on every timed call), and
+        that first agreement is also the barrier that starts the clock together."""
         failed = 0.0
         try:
             for _ in range(warm):
@@ -348,7 +350,7 @@ def main():
         except nv.FlexarError:
             failed = 1.0
         if world > 1:
-            dist.barrier()
+            failed, = max_vec([failed])
         t0 = time.perf_counter()
         try:
             if not failed:
