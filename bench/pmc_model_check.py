@@ -6,6 +6,9 @@ model reads off the programs (csrc/include/flexar/cost_model.hpp program_cost, s
 
     rocprofv3 --pmc FETCH_SIZE --output-format csv -d OUT -o run -- python3 bench/pmc_model_check.py SPEC DTYPE
     python3 bench/pmc_model_check.py --predict SPEC DTYPE      # the model's bytes per dispatch (JSON)
+
+SPEC "fp8" = all_reduce_fp8 (flat, e4m3 wire, AVG), priced as "flat+pull+e4m3" (the amax kernel is a
+separate dispatch and not counted).
 """
 import json
 import os
@@ -23,8 +26,9 @@ def predict(spec, dtype):
     es = {"float32": 4, "bfloat16": 2}[dtype]
     n = (MIB << 20) // es
     tot = {"read": 0.0, "write": 0.0}
+    model_spec = "flat+pull+e4m3" if spec == "fp8" else spec
     for r in range(RANKS):
-        c = nv.program_cost(spec, r, RANKS, n, dtype, links=1)
+        c = nv.program_cost(model_spec, r, RANKS, n, dtype, links=1)
         tot["read"] += c["hbm_read"]
         tot["write"] += c["hbm_write"]
     return {"spec": spec, "dtype": dtype, "ranks": RANKS, "mib_per_rank": MIB, "read_MiB": tot["read"] / 2**20,
@@ -42,7 +46,10 @@ def run(spec, dtype):
     xs = [torch.randn(s // dt.itemsize, device="cuda").to(dt) for _ in range(RANKS)]
     ys = [torch.empty_like(x) for x in xs]
     for _ in range(3):
-        g.all_reduce(xs, outs=ys, algo=spec)
+        if spec == "fp8":
+            g.all_reduce_fp8(xs, op="avg", outs=ys)
+        else:
+            g.all_reduce(xs, outs=ys, algo=spec)
     torch.cuda.synchronize()
     g.check()
     g.close()
