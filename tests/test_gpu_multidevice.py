@@ -353,6 +353,15 @@ def test_acceptance_matrix(cuda, world, shared):
     _check(_run(world, shared), world, shared)
 
 
+@pytest.mark.timeout(900)
+@pytest.mark.skipif(_ngpu() >= 8, reason="the per-GPU n8 case of test_acceptance_matrix runs the whole matrix")
+def test_acceptance_matrix_n8_shared(cuda):
+    """The N = 8 schedules the driver's 8-GPU bench will time - the full-mesh ring:7 (Hamiltonian
+    decomposition), the mixed-radix trees 2,4 / 4,2 with push and pull, RHD, typed partials - with 8 ranks on
+    device 0, so a planner or protocol bug at N = 8 shows up before the first 8-GPU run."""
+    _check(_run(8, True, parts=("allreduce", "typed")), 8, True)
+
+
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("shared", [pytest.param(_ngpu() < 2, id="auto-device-map")])
 def test_rccl_fallback_when_ipc_is_unavailable(cuda, shared):
