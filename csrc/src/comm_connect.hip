@@ -105,6 +105,9 @@ int alloc_workspace(flexar_comm* c, size_t ws) {
   FX_HIP(hipHostMalloc((void**)&c->err_host, 64, hipHostMallocMapped));
   memset(c->err_host, 0, 64);
   FX_HIP(hipHostGetDevicePointer((void**)&c->err_dev, c->err_host, 0));
+  // the calibration's agreement vector: allocated here, so no collective step of flexar_comm_calibrate
+  // can be skipped by one rank's allocation failure (its peers would advance an epoch it never reaches)
+  FX_HIP(hipMalloc(&c->cal_dev, kCalAgreeMax * sizeof(double)));
   FX_HIP(hipDeviceSynchronize());
   return 0;
 }
@@ -682,8 +685,7 @@ int flexar_comm_probe_agree(flexar_comm_t c, const void* all) {
 // Element-wise MIN over the ranks of n doubles, through this communicator (a verified family: the call
 // runs after the self-test). Every rank makes the same calls.
 static int agree_min(flexar_comm* c, double* v, int n, hipStream_t st) {
-  if (n > 256) { set_error("calibration: agreement vector too long"); return FLEXAR_ERR_INVALID; }
-  if (!c->cal_dev) FX_HIP(hipMalloc(&c->cal_dev, 256 * sizeof(double)));
+  if (n > kCalAgreeMax || !c->cal_dev) { set_error("calibration: agreement vector"); return FLEXAR_ERR_INVALID; }
   FX_HIP(hipMemcpyAsync(c->cal_dev, v, n * sizeof(double), hipMemcpyHostToDevice, st));
   int rc = flexar_allreduce_ex(c, c->cal_dev, c->cal_dev, (size_t)n, FLEXAR_FLOAT64, FLEXAR_MIN, st, nullptr, 1.0f);
   if (rc) return rc;
@@ -736,11 +738,18 @@ int flexar_comm_calibrate(flexar_comm_t c, int mode, char* json, size_t jlen) {
   if (c->nranks == 1 || mode == 0) return report("{\"source\": \"off\"}");
   if (env_model && *env_model) return report("{\"source\": \"FLEXAR_MODEL\"}");
   if (!c->ipc) return report("{\"source\": \"off\", \"note\": \"message transport only\"}");
+  // From here on every rank makes the same sequence of collective calls whatever fails locally (a rank
+  // that skipped one would leave its peers an epoch ahead for good): local failures become "failed" flags
+  // carried by the agreements, never early returns.
   FX_HIP(hipSetDevice(c->device));
+  std::string arch = "unknown";
   hipDeviceProp_t prop;
-  FX_HIP(hipGetDeviceProperties(&prop, c->device));
-  std::string arch = prop.gcnArchName;
-  arch = arch.substr(0, arch.find(':'));
+  if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) {
+    arch = prop.gcnArchName;
+    arch = arch.substr(0, arch.find(':'));
+  } else {
+    (void)hipGetLastError();
+  }
   // the settings fingerprint too (grid cap, block size, chunking, tune table change what a schedule costs)
   char fp[48];
   snprintf(fp, sizeof(fp), ";settings=%016llx", (unsigned long long)comm_fingerprint(c));
@@ -748,14 +757,17 @@ int flexar_comm_calibrate(flexar_comm_t c, int mode, char* json, size_t jlen) {
   const std::string dir = calib_dir();
   const std::string path = dir.empty() ? std::string() : calib_path(dir, key);
   hipStream_t st = nullptr;
-  FX_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    st = nullptr;  // the null stream: the communicator orders its calls across streams itself
+  }
   const uint64_t saved_timeout = c->timeout_ticks, saved_calls = c->calls, saved_bytes = c->bytes;
   const bool saved_profile = c->profile;
   c->timeout_ticks = env_u64("FLEXAR_SELFTEST_TIMEOUT_MS", 2000) * 100000ull;
   c->profile = false;
   auto finish = [&](int rc) {
     (void)hipStreamSynchronize(st);
-    (void)hipStreamDestroy(st);
+    if (st) (void)hipStreamDestroy(st);
     c->have_last = false;
     c->timeout_ticks = saved_timeout;
     c->profile = saved_profile;
@@ -780,12 +792,27 @@ int flexar_comm_calibrate(flexar_comm_t c, int mode, char* json, size_t jlen) {
     const std::vector<CalibPoint> pts = calib_points(c->nranks);
     double maxb = 0;
     for (const auto& p : pts) maxb = std::max(maxb, p.bytes);
+    // scratch and timers first, agreed on: a rank without them must not skip calls its peers make
     char* buf = nullptr;
-    FX_HIP(hipMalloc(&buf, 2 * (size_t)maxb));
-    FX_HIP(hipMemsetAsync(buf, 0, 2 * (size_t)maxb, st));
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    FX_HIP(hipEventCreate(&e0));
-    FX_HIP(hipEventCreate(&e1));
+    double ready = hipMalloc(&buf, 2 * (size_t)maxb) == hipSuccess &&
+                   hipMemsetAsync(buf, 0, 2 * (size_t)maxb, st) == hipSuccess && hipEventCreate(&e0) == hipSuccess &&
+                   hipEventCreate(&e1) == hipSuccess ? 1.0 : 0.0;
+    if (ready == 0.0) (void)hipGetLastError();
+    if (const char* tf = getenv("FLEXAR_TEST_CALIB_FAIL"))  // tests only: this rank's scratch "failed"
+      if (atoi(tf) == c->rank) ready = 0.0;
+    rc = agree_min(c, &ready, 1, st);
+    auto release = [&]() {
+      if (e0) (void)hipEventDestroy(e0);
+      if (e1) (void)hipEventDestroy(e1);
+      if (buf) (void)hipFree(buf);
+    };
+    if (rc || ready == 0.0) {
+      release();
+      if (rc) return finish(rc);
+      finish(0);
+      return report("{\"source\": \"failed\", \"key\": \"" + key + "\", \"note\": \"calibration scratch unavailable on some rank\"}");
+    }
     std::vector<double> t(pts.size() + 1, 0.0);
     double failed = 0;
     for (size_t i = 0; i < pts.size(); ++i) {
@@ -815,9 +842,8 @@ int flexar_comm_calibrate(flexar_comm_t c, int mode, char* json, size_t jlen) {
       t[i] = -(double)ms * 1e3 / iters;  // negated: the MIN agreement below is a max over ranks
     }
     t[pts.size()] = -failed;
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    (void)hipFree(buf);
+    (void)hipStreamSynchronize(st);
+    release();
     rc = agree_min(c, t.data(), (int)t.size(), st);
     if (rc) return finish(rc);
     std::vector<CalibRow> rows;

@@ -152,6 +152,8 @@ inline uint64_t env_u64(const char* name, uint64_t dflt) {
 
 using namespace flexar;
 
+constexpr int kCalAgreeMax = 256;  // doubles in one calibration agreement (flexar_comm_calibrate)
+
 struct flexar_comm {
   int rank = 0, nranks = 1, device = 0;
   size_t ws_bytes = 0, half_bytes = 0;
@@ -236,7 +238,7 @@ struct flexar_comm {
   int links_local = 0;          // this rank's own probe result (model.links = the ranks' agreed minimum)
   bool links_agreed = false;    // flexar_comm_probe_agree ran
   std::string calib_json;       // the connect-time calibration's report (flexar_comm_calibrate)
-  double* cal_dev = nullptr;    // agreement scratch of the calibration (device, 256 doubles)
+  double* cal_dev = nullptr;    // agreement scratch of the calibration (device, kCalAgreeMax doubles)
   int resident = 0;             // executor workgroups resident at once on this GPU (occupancy x CUs)
   // message transport (msg_plan.hpp over RCCL): its own staging arena (never the IPC workspace, whose
   // parity halves peers may still read), the RCCL communicator, plans per call shape

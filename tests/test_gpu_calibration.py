@@ -4,6 +4,9 @@ Separate processes on one GPU (IPC, gloo bootstrap), like tests/test_gpu_ipc.py:
 * the first communicator measures calib_points() and installs identical constants on every rank (same
   model hash); a second communicator of the same shape loads them from the on-disk cache; FLEXAR_CALIB=0
   leaves the default model; the calibrated selector's choice still produces exact results;
+* a rank whose calibration scratch is unavailable (FLEXAR_TEST_CALIB_FAIL, test-only) still makes every
+  collective call of the calibration: every rank reports "failed", keeps the default model, and later calls
+  stay in step;
 * a rank that reports a different link class for its peers (FLEXAR_TEST_PROBE, test-only) makes EVERY
   rank fail at connect with a message naming the disagreement - not a watchdog timeout later.
 """
@@ -30,6 +33,8 @@ def _worker(rank, world, port, calib_dir, mode, q):
                           FLEXAR_TIMEOUT_MS="20000", FLEXAR_CALIB_DIR=calib_dir)
         if mode == "probe":
             os.environ["FLEXAR_TEST_PROBE"] = "1:class=pcie"
+        if mode == "scratch":
+            os.environ["FLEXAR_TEST_CALIB_FAIL"] = str(world - 1)  # that rank's calibration scratch "fails"
         import torch.distributed as dist
 
         torch.cuda.set_device(0)
@@ -44,6 +49,21 @@ def _worker(rank, world, port, calib_dir, mode, q):
                 out["error"] = None
             except nv.FlexarError as e:
                 out["error"] = str(e)
+        elif mode == "scratch":
+            os.environ["FLEXAR_CALIB"] = "force"
+            comm = Communicator(workspace_bytes=64 << 20)
+            out["cal"] = comm.calibration
+            dev = torch.device("cuda", 0)
+            errs = []
+            for algo in (None, "ll", "oneshot", "flat", "ring"):  # epochs still in lockstep on every rank
+                for n in (1000, 1 << 18):
+                    x = (torch.arange(n, device=dev, dtype=torch.int32) % 977 + rank).float()
+                    y = comm.all_reduce(x.clone(), algo=algo)
+                    want = (torch.arange(n, device=dev, dtype=torch.int32) % 977).float() * world + world * (world - 1) / 2
+                    errs.append(float((y - want).abs().max().item()))
+            out["err"] = max(errs)
+            comm.check()
+            comm.close()
         else:
             for i, calib in enumerate(("1", "1", "0")):
                 os.environ["FLEXAR_CALIB"] = calib
@@ -121,3 +141,11 @@ def test_probe_disagreement_fails_at_connect(cuda, tmp_path):
     for r in range(2):
         e = out[r]["error"]
         assert e and "disagree on the machine shape" in e, (r, e)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_calibration_local_failure_keeps_ranks_in_step(cuda, tmp_path, world):
+    out = _run(world, "scratch", str(tmp_path))
+    for r in range(world):
+        assert out[r]["cal"]["source"] == "failed", (r, out[r]["cal"])
+        assert out[r]["err"] == 0.0, (r, out[r])
