@@ -7,6 +7,9 @@ set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(pwd)}"
 cd "$R"; mkdir -p gpurun_out
 export FLEXAR_NO_BUILD=1 FLEXAR_BENCH_SHARED_GPU=1 FLEXAR_BENCH_SHARED_RCCL=1
+# 8 processes x the default 4 hardware queues oversubscribe the GPU's compute queues: the command processor
+# then time-slices the processes and every cross-rank hand-off waits for a queue switch (~12 ms per call)
+export GPU_MAX_HW_QUEUES="${REHEARSE_HW_QUEUES:-2}"
 timeout -k 10 700 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
     --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 8 --steps 10 --warmup 3 \
     > gpurun_out/rehearse_rccl_n8.log 2>&1 && echo "rehearse rccl n=8 ok"

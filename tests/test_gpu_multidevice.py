@@ -102,6 +102,8 @@ def _worker(rank, world, port, shared, q, transport="rccl", no_ipc=False, parts=
         if shared:  # every rank on device 0: co-resident grids, one NCCL_HOSTID per rank (RCCL over loopback)
             os.environ.update(FLEXAR_MAX_GRID=str(max(8, 256 // (2 * world))), NCCL_HOSTID=f"flexar-md-rank{rank}",
                               NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+            if world > 4:  # 8 processes x 4 hardware queues would be time-sliced by the command processor
+                os.environ.setdefault("GPU_MAX_HW_QUEUES", "2")
         if no_ipc:
             os.environ["FLEXAR_FAULT_NO_IPC"] = "1"  # every peer mapping fails: the RCCL fallback carries all
         import torch.distributed as dist
@@ -356,10 +358,11 @@ def test_acceptance_matrix(cuda, world, shared):
 @pytest.mark.timeout(900)
 @pytest.mark.skipif(_ngpu() >= 8, reason="the per-GPU n8 case of test_acceptance_matrix runs the whole matrix")
 def test_acceptance_matrix_n8_shared(cuda):
-    """The N = 8 schedules the driver's 8-GPU bench will time - the full-mesh ring:7 (Hamiltonian
-    decomposition), the mixed-radix trees 2,4 / 4,2 with push and pull, RHD, typed partials - with 8 ranks on
-    device 0, so a planner or protocol bug at N = 8 shows up before the first 8-GPU run."""
-    _check(_run(8, True, parts=("allreduce", "typed")), 8, True)
+    """The whole matrix at N = 8 with 8 ranks on device 0 - the schedules the driver's 8-GPU bench will time
+    (full-mesh ring:7 from the Hamiltonian decomposition, mixed-radix trees 2,4 / 4,2 with push and pull,
+    RHD, typed partials, fp8, zero copy, the other collectives, DDP) - so a planner or protocol bug at N = 8
+    shows up before the first 8-GPU run."""
+    _check(_run(8, True), 8, True)
 
 
 @pytest.mark.timeout(600)
