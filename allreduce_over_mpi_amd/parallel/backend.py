@@ -32,7 +32,7 @@ import torch
 import torch.distributed as dist
 from torch._C._distributed_c10d import _create_work_from_future
 from torch._C._distributed_c10d import (AllgatherOptions, AllreduceCoalescedOptions, AllreduceOptions, AllToAllOptions,
-                                        BarrierOptions, BroadcastOptions, ReduceScatterOptions)
+                                        BarrierOptions, BroadcastOptions, ReduceOptions, ReduceScatterOptions)
 
 from .. import _native as nv
 from .comm import Communicator, store_exchange
@@ -305,6 +305,26 @@ class FlexarProcessGroup(dist.ProcessGroup):
             return self._on_side([t], lambda c: c.broadcast(t.view(torch.uint8) if t.dtype == torch.bool else t,
                                                             root=root), tensor_list)
         return self._fallback(tensor_list).broadcast(tensor_list, opts)
+
+    def reduce(self, tensor_list, opts=ReduceOptions()):
+        """``dist.reduce``: the flexar allreduce, in place on the root and out of place everywhere else, so
+        the non-root tensors stay unchanged (ncclReduce semantics). xGMI links are point-to-point: the
+        all-gather half that a tree reduce would skip runs on the non-roots' own incoming links in parallel
+        with the root's, so a reduce costs one allreduce (reference counterpart: none, the reference only
+        reduces to all, mpi_mod.hpp:1167)."""
+        opname = _redop_name(opts.reduceOp)
+        if len(tensor_list) != 1 or tensor_list[0].dtype == torch.bool or self.algo == "rccl" or \
+                not self._flexar_ok(tensor_list, opname):
+            return self._fallback(tensor_list).reduce(tensor_list, opts)
+        t = tensor_list[0]
+        root = opts.rootRank
+
+        def run(c):
+            if self._rank == root:
+                c.all_reduce(t, op=opname, algo=self.algo)
+            else:
+                c.all_reduce(t, op=opname, out=torch.empty_like(t), algo=self.algo)
+        return self._on_side([t], run, tensor_list)
 
     def allgather(self, output_tensors, input_tensor, opts=AllgatherOptions()):
         """List form (``dist.all_gather``): flexar all-gather into one packed buffer, then unpacked."""

@@ -35,6 +35,9 @@ def _worker(rank, world, port, q):
         dist.broadcast(b, src=0)
         outs = [torch.zeros(2) for _ in range(world)]
         dist.all_gather(outs, torch.full((2,), float(rank)))
+        r = torch.full((3,), float(rank + 1))
+        dist.reduce(r, dst=1)  # CPU tensors: the fallback group's reduce (gloo leaves non-roots undefined)
+        assert rank != 1 or r.tolist() == [3.0] * 3, r
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, x.tolist(), int(y.item()), float(b.item()), [o.tolist() for o in outs], None))
