@@ -434,6 +434,21 @@ class FlexarProcessGroup(dist.ProcessGroup):
         return self._fallback([input]).alltoall_base(output, input, output_split_sizes, input_split_sizes, opts)
 
     def alltoall(self, output_tensors, input_tensors, opts=AllToAllOptions()):
+        """List form (``dist.all_to_all``): equal-sized chunks are packed into one buffer and exchanged by
+        the flexar direct all-to-all, then unpacked; anything else goes to the fallback group."""
+        ts = list(input_tensors) + list(output_tensors)
+        if len(input_tensors) == self._world and len(output_tensors) == self._world and \
+                len({(t.numel(), t.dtype, t.device) for t in ts}) == 1 and ts[0].dtype != torch.bool and \
+                self._flexar_ok([ts[0]], "sum") and self._flat_comm_ok(ts[0]):
+            m = ts[0].numel()
+
+            def run(c):
+                flat_in = torch.cat([t.reshape(-1) for t in input_tensors])
+                flat_out = torch.empty_like(flat_in)
+                c.all_to_all(flat_in, flat_out)
+                for r, o in enumerate(output_tensors):
+                    o.copy_(flat_out[r * m:(r + 1) * m].view_as(o))
+            return self._on_side(ts, run, list(output_tensors))
         return self._fallback(input_tensors).alltoall(output_tensors, input_tensors, opts)
 
     def send(self, tensors, dst, tag=0):

@@ -242,6 +242,11 @@ def _colls(rank, world, port, q, fallback="gloo"):
         bc = torch.arange(100003, device=dev, dtype=torch.float32) * (rank + 1)
         dist.broadcast(bc, src=1)
         e8 = (bc - torch.arange(100003, device=dev).float() * 2).abs().max().item()
+        # list-form all-to-all (packed into one flexar exchange)
+        a2l_in = [torch.full((2, 3), float(10 * rank + p), device=dev) for p in range(world)]
+        a2l_out = [torch.empty(2, 3, device=dev) for _ in range(world)]
+        dist.all_to_all(a2l_out, a2l_in)
+        e12 = max((o - float(10 * p + rank)).abs().max().item() for p, o in enumerate(a2l_out))
         # dist.reduce: the root gets the sum, every other rank's tensor stays as it was
         rd = torch.arange(70001, device=dev, dtype=torch.float32) * (rank + 1)
         dist.reduce(rd, dst=world - 1)
@@ -260,7 +265,7 @@ def _colls(rank, world, port, q, fallback="gloo"):
         dist.barrier()
         used = dist.group.WORLD.stats["flexar_allreduce"]
         dist.destroy_process_group()
-        q.put((rank, max(e1, e2, e3, e4, e5, e6, e7, e8, e9, e10, e11), used, None))
+        q.put((rank, max(e1, e2, e3, e4, e5, e6, e7, e8, e9, e10, e11, e12), used, None))
     except Exception:
         import traceback
 
@@ -271,7 +276,7 @@ def _colls(rank, world, port, q, fallback="gloo"):
 def test_backend_reduce_scatter_all_gather(cuda, fallback):
     for rank, err, used, tb in _spawn(_colls, 2, fallback):
         assert tb is None, tb
-        assert err == 0.0 and used >= 10, (rank, err, used)
+        assert err == 0.0 and used >= 11, (rank, err, used)
 
 
 def test_rccl_algo_routing_single_rank():
