@@ -603,6 +603,20 @@ def main():
 
     algbw = algbw_gbps(nbytes, t_step)
     busbw = busbw_gbps(nbytes, t_step, world)
+    # this rank's HBM traffic per step over the step time: the timed schedule's bytes from the program-cost
+    # model (which matches rocprofv3 FETCH/WRITE_SIZE within 2.2 %, profiles/r3_pmc_model); N = 1: the copy
+    hbm_tbps = None
+    try:
+        if world == 1:
+            hbm_bytes = 2.0 * nbytes
+        elif flex and algo != "rccl":
+            pc = nv.program_cost(desc.split(" ")[0], rank, world, count, args.dtype)
+            hbm_bytes = pc["hbm_read"] + pc["hbm_write"]
+        else:
+            hbm_bytes = None
+        hbm_tbps = round(hbm_bytes / t_step / 1e12, 3) if hbm_bytes else None
+    except Exception:  # noqa: BLE001 - a schedule the model does not price: the field stays empty
+        hbm_tbps = None
     value = busbw  # rccl-tests busbw; 0 at N = 1 by definition (see the module docstring)
     readiness = None
     if world > 1 and isinstance(comm, Communicator):
@@ -640,6 +654,7 @@ def main():
         "busbw_GBps": round(busbw, 2),
         "algbw_GBps": round(algbw, 2),
         "aggregate_busbw_GBps": round(busbw * world, 2),
+        "hbm_TBps_per_rank": hbm_tbps,  # HBM traffic of the timed schedule / step time (MI355X peak ~8 TB/s)
         "rccl_busbw_GBps": rccl_busbw,
         "fallback": fallback,
         "tuner": tune_log or None,
