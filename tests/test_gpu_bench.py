@@ -43,6 +43,7 @@ def test_bench_json_and_fallback_chain_two_ranks(cuda):
     assert len(rejected) == 1 and "FLEXAR_BENCH_REJECT_FIRST" in next(iter(rejected.values())), rejected
     assert out["fallback"] is None and out["config"]["algorithm"] not in rejected, out["config"]
     assert out["readiness"]["disabled"] == "", out["readiness"]  # the rebuilt communicator kept every family
+    assert out["hbm_TBps_per_rank"] and 0 < out["hbm_TBps_per_rank"] < 10, out["hbm_TBps_per_rank"]
 
 
 def _bench(extra_env, args, timeout=300):
