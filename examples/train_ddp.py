@@ -43,6 +43,13 @@ def main():
     from allreduce_over_mpi_amd.parallel import backend as fb
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    if int(os.environ.get("LOCAL_WORLD_SIZE", "1")) > ndev:  # more ranks than GPUs (a 1-GPU rehearsal)
+        local %= ndev
+        # RCCL refuses two ranks of one host on one GPU; a host id per rank makes it treat them as separate
+        # hosts (loopback sockets), as bench.py's shared-GPU rehearsal does
+        os.environ.setdefault("NCCL_HOSTID", f"train-ddp-rank{os.environ.get('RANK', '0')}")
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist.init_process_group("flexar" if args.comm == "backend" else "nccl")
