@@ -605,18 +605,22 @@ def main():
     busbw = busbw_gbps(nbytes, t_step, world)
     # this rank's HBM traffic per step over the step time: the timed schedule's bytes from the program-cost
     # model (which matches rocprofv3 FETCH/WRITE_SIZE within 2.2 %, profiles/r3_pmc_model); N = 1: the copy
-    hbm_tbps = None
+    # and the peer traffic the same way: all bytes this rank's program moves over links (remote loads +
+    # stores), and the busiest link's bytes summed over the phases (what bounds the schedule on xGMI)
+    hbm_tbps = link_rate = None
     try:
         if world == 1:
             hbm_bytes = 2.0 * nbytes
         elif flex and algo != "rccl":
             pc = nv.program_cost(desc.split(" ")[0], rank, world, count, args.dtype)
             hbm_bytes = pc["hbm_read"] + pc["hbm_write"]
+            link_rate = {"all_links_GBps": round(pc["link_bytes"] / t_step / 1e9, 2),
+                         "busiest_link_GBps": round(pc["link_time_bytes"] / t_step / 1e9, 2)}
         else:
             hbm_bytes = None
         hbm_tbps = round(hbm_bytes / t_step / 1e12, 3) if hbm_bytes else None
-    except Exception:  # noqa: BLE001 - a schedule the model does not price: the field stays empty
-        hbm_tbps = None
+    except Exception:  # noqa: BLE001 - a schedule the model does not price: the fields stay empty
+        hbm_tbps = link_rate = None
     value = busbw  # rccl-tests busbw; 0 at N = 1 by definition (see the module docstring)
     readiness = None
     if world > 1 and isinstance(comm, Communicator):
@@ -655,6 +659,7 @@ def main():
         "algbw_GBps": round(algbw, 2),
         "aggregate_busbw_GBps": round(busbw * world, 2),
         "hbm_TBps_per_rank": hbm_tbps,  # HBM traffic of the timed schedule / step time (MI355X peak ~8 TB/s)
+        "peer_traffic_per_rank": link_rate,  # program-cost link bytes / step time (N > 1)
         "rccl_busbw_GBps": rccl_busbw,
         "fallback": fallback,
         "tuner": tune_log or None,
