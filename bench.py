@@ -696,6 +696,20 @@ def _x4(lo, hi):
     return out
 
 
+def _recover(comm):
+    """After a failure every rank agreed on (so every rank has synchronised): forget the recorded watchdog
+    timeout, so the next section's calls start clean instead of failing on the stale error (epochs advance
+    once per call on every rank, aborted or not: DESIGN.md §12)."""
+    try:
+        import torch
+
+        torch.cuda.synchronize()
+        if hasattr(comm, "clear_error"):
+            comm.clear_error()
+    except Exception:  # noqa: BLE001 - best effort: the section already reports the failure
+        pass
+
+
 def run_config5(comm, world, dev, dist, timed_fn, max_vec, host_ref, args, rank):
     """BASELINE config #5: the fused-scale fp8 gradient allreduce. fp32 256 MiB per rank in and out, OCP
     e4m3 on the links, AVG: one amax pass + ONE executor launch whose first transfer quantises with the
@@ -725,8 +739,11 @@ def run_config5(comm, world, dev, dist, timed_fn, max_vec, host_ref, args, rank)
     failed, = max_vec([failed])
     if failed:
         out["error"] = err if isinstance(err, str) else "failed on a peer"
+        _recover(comm)
         return out
     t = timed_fn(lambda: comm.all_reduce_fp8(x, op="avg", out=y), 10, 2)
+    if t is None:
+        _recover(comm)
     errs = max_vec([err])
     out.update(flexar_us=round(t * 1e6, 1) if t else None,
                flexar_busbw_GBps=round(busbw_gbps(4 * n, t, world), 2) if t else None,
@@ -778,8 +795,11 @@ def run_config3(comm, world, rank, dev, dist, timed_fn, max_vec, host_ref, args)
         if failed:
             row["error"] = err if isinstance(err, str) else "failed on a peer"
             out["variants"][spec] = row
+            _recover(comm)
             continue
         t = timed_fn(lambda: comm.all_reduce(x, out=y, algo=a), 5, 1)
+        if t is None:
+            _recover(comm)
         e = max_vec([err])[0]
         row.update(us=round(t * 1e6, 1) if t else None, busbw_GBps=round(busbw_gbps(n * 2, t, world), 2) if t else None,
                    max_rel_err=round(e, 6), correct=e <= 2e-2 * math.sqrt(world) * 4)
@@ -940,6 +960,8 @@ def run_sweep(comm, world, rank, dev, dtype, op, dist, max_over_ranks, lo, hi, w
         y = torch.empty_like(x)
         iters = max(3, min(50, int(2e8 // max(b, 1))))
         tf = timed_fn(lambda: comm.all_reduce(x, out=y, op=op), iters, 2)
+        if tf is None:  # failed on some rank (agreed inside timed_fn): the next size starts clean
+            _recover(comm)
         # integers up to 2^24 (fp32) / 2048 (fp16) / 256 (bf16) are exact, and so is every partial sum below them
         limit = {torch.float32: 1 << 24, torch.float16: 2048, torch.bfloat16: 256}.get(dtype, 0)
         exact = op == "sum" and 250 * world + world * (world - 1) // 2 <= limit
