@@ -81,10 +81,10 @@ def autotune(comm, sizes: Optional[Sequence[int]] = None, dtype=None, candidates
     group = comm.group
     host_ref = dist.get_backend(group) == "gloo"
 
-    def agree_max(v: float) -> float:
-        t = torch.tensor([v], dtype=torch.float64, device="cpu" if host_ref else dev)
+    def agree_max(*v: float) -> list:
+        t = torch.tensor(list(v), dtype=torch.float64, device="cpu" if host_ref else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
-        return float(t.item())
+        return [float(a) for a in t.tolist()]
 
     table, rows = [], []
     tol = {torch.float32: 1e-5, torch.bfloat16: 2e-2, torch.float16: 4e-3}.get(dtype, 1e-5) * 4 * math.sqrt(world)
@@ -99,7 +99,9 @@ def autotune(comm, sizes: Optional[Sequence[int]] = None, dtype=None, candidates
         reps = iters or max(3, min(100, int(2e8 // max(nbytes, 1))))
         best, best_t = None, float("inf")
         for spec in (candidates or default_candidates(world, n * es)):
-            failed, t = 0.0, float("inf")
+            # exactly two agreements per candidate on every rank, whatever raised where: a rank that failed
+            # its checks must not skip a collective its peers make (they would pair with its next one)
+            failed, t = 0.0, 0.0
             try:
                 for sc in (1.0, 0.5, 0.25):
                     xs = x if sc == 1.0 else (x.float() * sc).to(dtype)
@@ -108,7 +110,11 @@ def autotune(comm, sizes: Optional[Sequence[int]] = None, dtype=None, candidates
                     if float((y.float() - ref * sc).abs().max().item()) > tol * scale * sc:
                         failed = 1.0
                 comm.check()
-                if agree_max(failed) == 0.0:
+            except nv.FlexarError:
+                failed = 1.0
+            failed, = agree_max(failed)
+            if failed == 0.0:
+                try:
                     torch.cuda.synchronize()
                     dist.barrier(group=group)
                     t0 = time.perf_counter()
@@ -117,15 +123,15 @@ def autotune(comm, sizes: Optional[Sequence[int]] = None, dtype=None, candidates
                     torch.cuda.synchronize()
                     t = (time.perf_counter() - t0) / reps
                     comm.check()
-            except nv.FlexarError:
-                failed = 1.0
-            if agree_max(failed) != 0.0:
+                except nv.FlexarError:
+                    failed = 1.0
+            t, failed = agree_max(t, failed)
+            if failed != 0.0:
                 torch.cuda.synchronize()
                 comm.clear_error()  # every rank is here, nothing in flight: a timeout must not poison the rest
                 if verbose and comm.rank == 0:
                     print(f"[autotune] {n * es:>11d} B  {spec:16s} excluded (wrong or failed on a rank)", flush=True)
                 continue
-            t = agree_max(t)
             rows.append({"spec": spec, "bytes": n * es, "us": t * 1e6})
             if verbose and comm.rank == 0:
                 print(f"[autotune] {n * es:>11d} B  {spec:16s} {t * 1e6:10.2f} us  "

@@ -96,3 +96,68 @@ def test_profile_stats(cuda, monkeypatch):
     assert sum(v["calls"] for v in st["profile"].values()) == 3
     assert all(v["ms"] > 0 for v in st["profile"].values())
     c.close()
+
+
+def _late_peer_autotune_worker(rank, world, port, q):
+    import os
+
+    try:
+        # rank 1 signals slot 1 (the flat schedules' closing hand-off) 1 s late against a 300 ms watchdog: rank
+        # 0 times out at its last wait and raises in its checks while rank 1 completes every call - the
+        # one-rank failure that used to make autotune's ranks skip different collectives
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
+                          FLEXAR_TIMEOUT_MS="300", FLEXAR_SELFTEST="0", FLEXAR_CALIB="0",
+                          FLEXAR_FAULT_INJECT="delay:1:1:1000000")
+        import torch.distributed as dist
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from allreduce_over_mpi_amd.parallel import Communicator
+        from allreduce_over_mpi_amd.parallel.autotune import autotune
+
+        comm = Communicator(workspace_bytes=32 << 20)
+        table = autotune(comm, sizes=[1 << 20], candidates=["flat+pull", "flat+push", "ll"], iters=2, install=False,
+                         calibrate=False)
+        torch.cuda.synchronize()
+        comm.clear_error()
+        dist.barrier()
+        comm.close()
+        dist.destroy_process_group()
+        q.put((rank, table, None))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_autotune_agrees_when_one_rank_times_out(cuda):
+    """A candidate that fails on ONE rank only (its watchdog fired while the peer completed) is excluded on
+    every rank: each candidate makes exactly two agreements on every rank, so no rank's collectives pair
+    with a peer's later ones. The flat schedules end on the delayed hand-off; LL has no SIGNAL and passes."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_late_peer_autotune_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(2):
+            rank, table, tb = q.get(timeout=240)
+            assert tb is None, tb
+            res[rank] = table
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    specs = {r: [t[1] for t in tab] for r, tab in res.items()}
+    assert specs[0] == specs[1], specs  # the same winners on both ranks
+    assert specs[0] in ([], ["ll"]), specs  # the flat candidates were excluded everywhere
