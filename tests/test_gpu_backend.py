@@ -423,3 +423,47 @@ def test_fsdp2_over_flexar(cuda):
         assert tb is None, tb
         assert used and used > 0, "flexar collectives were not used"
         assert err < 1e-5, (rank, err)
+
+
+def _funcol(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
+                          FLEXAR_TIMEOUT_MS="20000")
+        _fallback_env(rank, "gloo")
+        import torch.distributed as dist
+        import torch.distributed._functional_collectives as funcol
+
+        from allreduce_over_mpi_amd.parallel import backend as fb  # noqa: F401
+
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        dist.init_process_group("flexar", rank=rank, world_size=world)
+        tri = sum(r + 1 for r in range(world))
+        # the functional collectives (DTensor / tensor parallelism, torch.compile-traceable): all_reduce,
+        # reduce_scatter_tensor and all_gather_tensor through the "flexar" process group
+        a = funcol.wait_tensor(funcol.all_reduce(torch.full((4099,), float(rank + 1), device=dev), "sum",
+                                                 dist.group.WORLD))
+        rs = funcol.wait_tensor(funcol.reduce_scatter_tensor(
+            torch.arange(world * 1000, device=dev, dtype=torch.float32) * (rank + 1), "sum", 0, dist.group.WORLD))
+        ag = funcol.wait_tensor(funcol.all_gather_tensor(torch.full((513,), float(rank), device=dev), 0,
+                                                         dist.group.WORLD))
+        torch.cuda.synchronize()
+        err = max((a - tri).abs().max().item(),
+                  (rs - torch.arange(rank * 1000, (rank + 1) * 1000, device=dev).float() * tri).abs().max().item(),
+                  (ag - torch.arange(world, device=dev).float().repeat_interleave(513)).abs().max().item())
+        used = dist.group.WORLD.stats["flexar_allreduce"]
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, err, used, None))
+    except Exception:
+        import traceback
+
+        q.put((rank, None, None, traceback.format_exc()))
+
+
+def test_functional_collectives_over_flexar(cuda):
+    """torch.distributed._functional_collectives (what DTensor, tensor parallelism and torch.compile issue)
+    dispatch into the "flexar" backend's allreduce / reduce-scatter / all-gather."""
+    for rank, err, used, tb in _spawn(_funcol, 2):
+        assert tb is None, tb
+        assert err == 0.0 and used >= 3, (rank, err, used)
