@@ -696,3 +696,32 @@ def test_ipc_zero_copy_registered_buffers(cuda, world):
         assert errs.pop("regs_left") == 0
         for key, err in errs.items():
             assert err < 1e-4, (rank, key, err)
+
+
+@pytest.mark.skipif(not os.environ.get("FLEXAR_SOAK"), reason="soak run: FLEXAR_SOAK=<calls> (scripts/gpu_soak.sh)")
+@pytest.mark.timeout(1000)
+@pytest.mark.parametrize("world,fault", [(4, ""), (8, ""), (4, "delay:2:0:150")])
+def test_ipc_soak(cuda, world, fault):
+    """The randomized call sequence at length (FLEXAR_SOAK calls, e.g. 600): every collective, algorithm,
+    size, stream and in/out-of-place mix, exact results, N = 4 and 8 on one GPU."""
+    import torch.multiprocessing as mp
+
+    if world > 4:
+        os.environ["GPU_MAX_HW_QUEUES"] = "2"  # inherited by the spawned ranks (DESIGN.md §20)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    calls = int(os.environ["FLEXAR_SOAK"])
+    procs = [ctx.Process(target=_stress_worker, args=(r, world, port, calls, q, fault)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=900) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank, bad, tb in res:
+        assert tb is None, tb
+        assert not bad, (rank, len(bad), bad[:5])
