@@ -228,7 +228,12 @@ int choose_grid(flexar_comm* c, uint64_t bytes, uint32_t nchan) {
   }
   if (g < (int)nchan) g = (int)nchan;
   g = (g + nchan - 1) / nchan * nchan;  // whole channels
-  const int cap = std::max((int)nchan, std::min(std::max(c->max_grid, c->grid_override), (int)kMaxGridBlocks));
+  int cap = std::max((int)nchan, std::min(std::max(c->max_grid, c->grid_override), (int)kMaxGridBlocks));
+  // Never more workgroups than the GPU keeps resident at once: workgroup b spins on workgroup b of every peer,
+  // and the dispatch order is not defined, so a grid beyond residency could leave a peer's b queued behind
+  // workgroups that wait for it (a watchdog timeout instead of a result). Co-residency makes the protocol
+  // placement-independent (set_grid / FLEXAR_MAX_GRID above it are clamped here).
+  if (c->resident > 0) cap = std::max((int)nchan, std::min(cap, c->resident));
   if (g > cap) g = cap / (int)nchan * (int)nchan;  // round down rather than exceed the cap
   return g;
 }

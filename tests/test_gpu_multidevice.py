@@ -15,7 +15,8 @@ parities, so a stale staging line cannot go unnoticed):
 * all_reduce_fp8 (fused pre/post-scale, e4m3 wire) against a torch emulation of the same arithmetic;
 * reduce-scatter / all-gather / all-to-all / broadcast (staging and zero copy);
 * zero-copy allreduce over registered buffers;
-* executor grids of 512 and 1024 workgroups when ranks do not share a device;
+* executor grid requests of 256, 512 and 1024 workgroups when ranks do not share a device (clamped to
+  the resident workgroups);
 * DDP GPT-tiny over a "flexar" process group against one model trained on the whole batch.
 """
 import os
@@ -218,12 +219,17 @@ def _worker(rank, world, port, shared, q, transport="rccl", no_ipc=False, parts=
             ref = torch.stack([x.double() for x in xs]).sum(0)
             results[("zc_reduce_scatter", None)] = rel(rs_out, ref[rank * m:(rank + 1) * m])
         if ("all" in parts or "grids" in parts) and not shared:
-            for g in (512, 1024):
+            # grids from 256 up to past residency: a request beyond the workgroups the GPU keeps resident is
+            # clamped to them (comm.hip choose_grid), so the flag protocol never depends on dispatch order
+            resident = int(comm.topology()["resident_blocks"])
+            for g in (256, 512, 1024):
                 comm.set_grid(g)
                 for spec in ("flat", "flat+push+nts", "ring"):
                     allreduce_case(spec, torch.float32, (1 << 22,), ops=("sum",))
                     results[("grid", g, spec)] = results.pop(("allreduce", spec, str(torch.float32), 1 << 22, "sum",
                                                               False))
+                used = int(comm.describe(1 << 22, torch.float32).split("grid=")[1].split()[0])
+                results[("grid_clamped", g)] = 0.0 if used <= max(resident, 1) else float(used)
             comm.set_grid(0)
         comm.check()
         results["readiness"] = (comm.topology(), list(comm.selftest_failed))
