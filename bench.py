@@ -284,11 +284,19 @@ def main():
             log(rank, f"zero-copy candidates skipped: {e}")
             return False
 
+    def quiesce():
+        """Collective, after a communicator's close: no rank allocates, exports or maps the next communicator's
+        memory while a peer still holds mappings of the old one (IPC imports of freed workspaces and
+        registered buffers are all closed everywhere first)."""
+        if world > 1:
+            max_over_ranks(0.0)
+
     def rebuild(why):
         """Collective: a failed call may leave epochs / flags inconsistent - start from a fresh communicator."""
         nonlocal comm, fallback
         comm.close()
         torch.cuda.synchronize()
+        quiesce()
         comm = make_comm() or RcclOnly(dist)
         if isinstance(comm, RcclOnly):
             fallback = f"flexar communicator could not be rebuilt ({why})"
@@ -502,6 +510,7 @@ def main():
         elif attempt > 0:  # the failed attempt may have left epochs / flags inconsistent
             comm.close()
             torch.cuda.synchronize()
+            quiesce()
             comm = make_comm() or RcclOnly(dist)
             if isinstance(comm, RcclOnly):
                 rejected[algo] = "the flexar communicator could not be rebuilt"

@@ -24,6 +24,23 @@ def _port():
     return p
 
 
+def _diag(r, name):
+    """Why a bench run failed: its whole output is kept under gpurun_out/ (merged back from the GPU box), and
+    the message carries the bench's last progress lines and every error-looking line, not just the tail
+    (the tail of an aborted rank is RCCL's crash dump)."""
+    text = (r.stdout or "") + "\n" + (r.stderr or "")
+    try:
+        os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(REPO, "gpurun_out", f"test_bench_{name}.log"), "w") as f:
+            f.write(text)
+    except OSError:
+        pass
+    lines = text.splitlines()
+    progress = [ln for ln in lines if ln.startswith("[bench]")][-15:]
+    errors = [ln for ln in lines if any(k in ln.lower() for k in ("error", "fault", "illegal", "abort", "exception"))]
+    return "\n".join(["-- progress:"] + progress + ["-- errors:"] + errors[:25] + ["-- tail:", text[-1500:]])
+
+
 def test_bench_json_and_fallback_chain_two_ranks(cuda):
     env = dict(os.environ, FLEXAR_BENCH_SHARED_GPU="1", FLEXAR_BENCH_SHARED_RCCL="1", FLEXAR_BENCH_REJECT_FIRST="1",
                FLEXAR_NO_BUILD="1")
@@ -31,7 +48,7 @@ def test_bench_json_and_fallback_chain_two_ranks(cuda):
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(REPO, "bench.py"),
            "--gpus", "2", "--steps", "3", "--warmup", "1", "--size-mb", "16", "--no-calibrate", "--no-small"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110, cwd=REPO)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _diag(r, "fallback")
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     out = json.loads(lines[0])
@@ -52,7 +69,7 @@ def _bench(extra_env, args, timeout=300):
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(REPO, "bench.py"),
            "--gpus", "2", "--steps", "3", "--warmup", "1", *args]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=REPO)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _diag(r, "sections")
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     return json.loads(lines[0])
