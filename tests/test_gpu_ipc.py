@@ -725,3 +725,68 @@ def test_ipc_soak(cuda, world, fault):
     for rank, bad, tb in res:
         assert tb is None, tb
         assert not bad, (rank, len(bad), bad[:5])
+
+
+def _rebuild_worker(rank, world, port, cycles, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
+                          FLEXAR_TIMEOUT_MS="20000")
+        import torch.distributed as dist
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from allreduce_over_mpi_amd.parallel import Communicator
+
+        # the same buffers, registered by one communicator after another (what bench.py's fallback chain does
+        # when it rebuilds): every cycle closes the communicator, with its IPC imports of the peers' buffers and
+        # workspace, and maps the same allocations again in a fresh one
+        n = 4 << 20
+        x = torch.empty(n, device="cuda")
+        y = torch.empty(n, device="cuda")
+        bad = []
+        for cyc in range(cycles):
+            comm = Communicator(workspace_bytes=64 << 20)
+            comm.register_many([x, y])
+            for spec in ("flat+zc+push", "flat+zc", "flat+pull", "ll"):
+                m = n if spec != "ll" else 4096
+                x[:m].copy_(torch.arange(m, device="cuda", dtype=torch.float32) % 97 + rank + cyc)
+                comm.all_reduce(x[:m], out=y[:m], algo=spec)
+                torch.cuda.synchronize()
+                want = (torch.arange(m, device="cuda", dtype=torch.float32) % 97) * world + world * (world - 1) / 2 \
+                    + world * cyc
+                if not torch.equal(y[:m], want):
+                    bad.append((cyc, spec))
+            comm.check()
+            comm.close()
+            dist.barrier()  # every rank has closed before any rank maps the next communicator
+        dist.destroy_process_group()
+        q.put((rank, bad, None))
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.skipif(not os.environ.get("FLEXAR_SOAK"), reason="soak run: FLEXAR_SOAK (scripts/gpu_soak.sh)")
+@pytest.mark.timeout(600)
+def test_ipc_communicator_rebuild_cycles(cuda):
+    """20 communicator rebuilds over the same registered buffers (close -> fresh communicator -> register the
+    same allocations -> zero-copy and staging allreduces), every result exact."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rebuild_worker, args=(r, 2, port, 20, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=500) for _ in range(2)]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank, bad, tb in res:
+        assert tb is None, tb
+        assert not bad, (rank, bad[:5])
