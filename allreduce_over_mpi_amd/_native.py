@@ -45,6 +45,10 @@ def _sig(lib):
         "flexar_comm_export": (i, [vp, vp]),
         "flexar_comm_connect": (i, [vp, vp]),
         "flexar_comm_destroy": (i, [vp]),
+        "flexar_comm_destroy_local": (i, [vp]),
+        "flexar_comm_resync": (i, [vp]),
+        "flexar_host_barrier_run": (i, [cp, i, i, i, c.c_uint64, i]),
+        "flexar_comm_selftest_note": (i, [vp, cp, sz]),
         "flexar_comm_rank": (i, [vp]),
         "flexar_comm_size": (i, [vp]),
         "flexar_comm_set_algo": (i, [vp, cp]),
@@ -115,6 +119,8 @@ def _sig(lib):
         "flexar_direct_links": (i, [c.POINTER(c.c_int32), c.POINTER(c.c_int32), i, i]),
         "flexar_probe_blob_size": (sz, []),
         "flexar_probe_agree": (i, [vp, i, c.POINTER(i)]),
+        "flexar_probe_agree_resident": (i, [vp, i, c.POINTER(i), c.POINTER(i)]),
+        "flexar_settings_fingerprint": (c.c_uint64, [i]),
         "flexar_comm_probe_export": (i, [vp, vp]),
         "flexar_comm_probe_agree": (i, [vp, vp]),
         "flexar_comm_calibrate": (i, [vp, i, cp, sz]),
@@ -180,6 +186,14 @@ def _load_fastcall(l):
     addr = lambda f: ctypes.cast(f, ctypes.c_void_p).value  # noqa: E731
     AR, RS, AG = addr(l.flexar_allreduce_ex), addr(l.flexar_reduce_scatter), addr(l.flexar_all_gather)
     FAST = m
+
+
+def log_warn(msg: str):
+    """A warning on stderr in the native logger's format (silenced by FLEXAR_LOG_LEVEL=error)."""
+    if os.environ.get("FLEXAR_LOG_LEVEL", "warn").lower() not in ("error", "none", "off"):
+        import sys
+
+        print(f"[flexar W] {msg}", file=sys.stderr, flush=True)
 
 
 def last_error() -> str:

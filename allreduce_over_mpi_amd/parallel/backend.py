@@ -320,10 +320,15 @@ class FlexarProcessGroup(dist.ProcessGroup):
         root = opts.rootRank
 
         def run(c):
+            # every rank runs the SAME call shape - out of place into a fresh buffer - so every rank resolves
+            # the same schedule: the zero-copy choice depends on whether BOTH buffers lie inside registrations,
+            # and a root reducing in place on a registered tensor would pick it alone. A fresh
+            # buffer is never inside a live registration (registrations hold their tensors).
+            tmp = torch.empty_like(t)
+            algo = None if self.algo and "+zc" in self.algo else self.algo  # tmp is never registered
+            c.all_reduce(t, op=opname, out=tmp, algo=algo)
             if self._rank == root:
-                c.all_reduce(t, op=opname, algo=self.algo)
-            else:
-                c.all_reduce(t, op=opname, out=torch.empty_like(t), algo=self.algo)
+                t.copy_(tmp)
         return self._on_side([t], run, tensor_list)
 
     def allgather(self, output_tensors, input_tensor, opts=AllgatherOptions()):

@@ -111,6 +111,48 @@ class Communicator:
         self.rank, self.world_size = int(rank), int(world_size)
         self.device = torch.cuda.current_device() if device is None else int(device)
         self.group = group
+        self._h = ctypes.c_void_p()
+        self._hi = 0
+        self.retried = None  # why the first attempt of an auto-transport connect failed (it was retried)
+        transport = transport or os.environ.get("FLEXAR_TRANSPORT", "auto")
+        if transport not in ("auto", "ipc", "rccl"):
+            raise nv.FlexarError(1, f"unknown transport {transport!r} (auto | ipc | rccl)")
+        if self.world_size > 1 and exchange is None:
+            def exchange(data: bytes):
+                gathered = [None] * self.world_size
+                dist.all_gather_object(gathered, data, group=group)
+                return gathered
+        # transport "auto": a failure every rank agreed on at connect or in the readiness gate (a HIP error
+        # in the self-test, no verified protocol) closes the communicator collectively and builds it once
+        # more in this process; the second failure is final
+        attempts = 2 if transport == "auto" and self.world_size > 1 else 1
+        for attempt in range(attempts):
+            try:
+                self._open(workspace_bytes, exchange, transport)
+                break
+            except nv.FlexarError as e:
+                self.close()
+                if attempt + 1 == attempts or not getattr(e, "agreed", False):
+                    raise
+                self.retried = str(e)
+                nv.log_warn(f"rank {self.rank}: communicator creation failed on every rank ({e}); "
+                            "closed collectively, building it once more")
+        self._rccl_default = False
+        self._rccl_group = None
+        env_algo = os.environ.get("FLEXAR_ALGO", "")
+        if algo or env_algo == "rccl":
+            self.set_algo(algo or env_algo)
+
+    @staticmethod
+    def _agreed(err: "nv.FlexarError") -> "nv.FlexarError":
+        """Mark an error every rank raises identically (after an exchange): the collective retry may run."""
+        err.agreed = True
+        return err
+
+    def _open(self, workspace_bytes, exchange, transport):
+        """Create, export, connect and verify the native communicator (collective)."""
+        import torch
+
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
             nv.check(self._lib.flexar_comm_create(self.rank, self.world_size, self.device, int(workspace_bytes),
@@ -118,53 +160,42 @@ class Communicator:
         self._h = h
         self._hi = int(h.value or 0)  # the handle as an int, for the fast-call path
         self.selftest_failed = []
+        self.selftest_notes = {}
         self.calibration = None
         self.transport_note = None
         self._exchange = None
         self._regs = {}
         self._zc_ok = None  # zero-copy readiness: None = not checked yet (first register())
         self._zc_testing = False
-        if self.world_size > 1:
-            hs = int(self._lib.flexar_handle_size())
-            buf = ctypes.create_string_buffer(hs)
-            nv.check(self._lib.flexar_comm_export(self._h, buf), "comm_export")
-            if exchange is None:
-                def exchange(data: bytes):
-                    gathered = [None] * self.world_size
-                    dist.all_gather_object(gathered, data, group=group)
-                    return gathered
-            self._exchange = exchange
-            allb = b"".join(exchange(bytes(buf.raw)))
-            transport = transport or os.environ.get("FLEXAR_TRANSPORT", "auto")
-            if transport not in ("auto", "ipc", "rccl"):
-                raise nv.FlexarError(1, f"unknown transport {transport!r} (auto | ipc | rccl)")
-            rc = self._lib.flexar_comm_connect(self._h, allb)
-            # agreement round (also the barrier: everyone has mapped everyone before the first collective);
-            # a rank that failed to map a peer must not leave the others waiting in a later collective
-            msg = b"" if rc == 0 else f"{rc}:rank {self.rank}: {nv.last_error()}".encode()
-            bad = [m.decode(errors="replace") for m in exchange(msg) if m]
-            # no peer memory (a failed peer mapping = HIP error 3; no P2P path between the GPUs or ranks on
-            # different hosts = unsupported 2) falls back to the message transport; settings mismatches
-            # (invalid 1) stay errors
-            mapping_only = bool(bad) and all(b.split(":", 1)[0] in ("2", "3") for b in bad)
-            fallback = bool(bad) and transport == "auto" and mapping_only and self._lib.flexar_rccl_available()
-            if bad and not fallback:
-                self.close()
-                raise nv.FlexarError(rc or 5, "comm_connect: " + "; ".join(b.split(":", 1)[1] for b in bad))
-            if transport == "rccl" or fallback:
-                self._init_msg(exchange)
-                if fallback:
-                    nv.check(self._lib.flexar_comm_connect_msg_only(self._h), "connect_msg_only")
-                    self.transport_note = "IPC unavailable (" + "; ".join(b.split(":", 1)[1] for b in bad) + \
-                                          "): every call runs over the RCCL message transport"
-            self._agree_probe(exchange)
-            self._readiness(exchange)
-            self._calibrate(exchange)
-        self._rccl_default = False
-        self._rccl_group = None
-        env_algo = os.environ.get("FLEXAR_ALGO", "")
-        if algo or env_algo == "rccl":
-            self.set_algo(algo or env_algo)
+        if self.world_size == 1:
+            return
+        hs = int(self._lib.flexar_handle_size())
+        buf = ctypes.create_string_buffer(hs)
+        nv.check(self._lib.flexar_comm_export(self._h, buf), "comm_export")
+        self._exchange = exchange
+        allb = b"".join(exchange(bytes(buf.raw)))
+        rc = self._lib.flexar_comm_connect(self._h, allb)
+        # agreement round (also the barrier: everyone has mapped everyone before the first collective);
+        # a rank that failed to map a peer must not leave the others waiting in a later collective
+        msg = b"" if rc == 0 else f"{rc}:rank {self.rank}: {nv.last_error()}".encode()
+        bad = [m.decode(errors="replace") for m in exchange(msg) if m]
+        # no peer memory (a failed peer mapping = HIP error 3; no P2P path between the GPUs or ranks on
+        # different hosts = unsupported 2) falls back to the message transport; settings mismatches
+        # (invalid 1) stay errors
+        mapping_only = bool(bad) and all(b.split(":", 1)[0] in ("2", "3") for b in bad)
+        fallback = bool(bad) and transport == "auto" and mapping_only and self._lib.flexar_rccl_available()
+        if bad and not fallback:
+            err = nv.FlexarError(rc or 5, "comm_connect: " + "; ".join(b.split(":", 1)[1] for b in bad))
+            raise self._agreed(err) if mapping_only else err  # settings mismatches would only fail again
+        if transport == "rccl" or fallback:
+            self._init_msg(exchange)
+            if fallback:
+                nv.check(self._lib.flexar_comm_connect_msg_only(self._h), "connect_msg_only")
+                self.transport_note = "IPC unavailable (" + "; ".join(b.split(":", 1)[1] for b in bad) + \
+                                      "): every call runs over the RCCL message transport"
+        self._agree_probe(exchange)
+        self._readiness(exchange)
+        self._calibrate(exchange)
 
     def _init_msg(self, exchange):
         """Create the RCCL communicator of the message transport (collective): rank 0's unique id is
@@ -177,7 +208,6 @@ class Communicator:
         bad = [m.decode(errors="replace") for m in exchange(b"" if rc == 0 else
                                                             f"rank {self.rank}: {nv.last_error()}".encode()) if m]
         if bad:
-            self.close()
             raise nv.FlexarError(7, "message transport: " + "; ".join(bad))
 
     def _agree_probe(self, exchange):
@@ -189,9 +219,7 @@ class Communicator:
         nv.check(self._lib.flexar_comm_probe_export(self._h, blob), "probe_export")
         rc = self._lib.flexar_comm_probe_agree(self._h, b"".join(exchange(bytes(blob.raw))))
         if rc:  # deterministic on identical inputs: every rank fails the same way
-            err = nv.last_error()
-            self.close()
-            raise nv.FlexarError(rc, "comm_connect: " + err)
+            raise nv.FlexarError(rc, "comm_connect: " + nv.last_error())
 
     def _calibrate(self, exchange):
         """Connect-time calibration of the cost model (flexar_comm_calibrate; FLEXAR_CALIB = 0 | 1 (default:
@@ -235,7 +263,11 @@ class Communicator:
         def run(fam):
             """One family's exact allreduces, started together (a barrier first: a rank that arrives seconds
             late - e.g. still finishing RCCL set-up - would otherwise trip its peers' short watchdog and shift
-            every later family out of step); returns the families that failed on ANY rank."""
+            every later family out of step); returns the families that failed on ANY rank.
+
+            A HIP error on a rank fails the family there, with the error named (flexar_comm_selftest_note), and
+            the downgrade chain goes on; only an error that left the device unusable (rc != 0) ends creation,
+            with every rank's message, on every rank."""
             nonlocal late_ms
             exchange(b"")
             if late_ms:
@@ -245,17 +277,27 @@ class Communicator:
                 late_ms = 0.0
             failed = ctypes.c_uint32(0)
             rc = self._lib.flexar_comm_selftest(self._h, fam, ctypes.byref(failed))
-            msg = f"{rc}:{failed.value}:{nv.last_error() if rc else ''}".encode()
+            note = nv.last_error() if rc else self._selftest_note()
+            msg = f"{rc}:{failed.value}:{note}".encode()
             rows = [m.decode(errors="replace").split(":", 2) for m in exchange(msg)]  # also the barrier
             errs = [f"rank {r}: {e}" for r, (c, _, e) in enumerate(rows) if c != "0"]
             if errs:
-                self.close()
+                # the device is unusable on those ranks (a sticky HIP error): a retry could not run either
                 raise nv.FlexarError(3, "self-test: " + "; ".join(errs))
             m = 0
-            for _, f, _ in rows:
+            for r, (_, f, e) in enumerate(rows):
                 m |= int(f)
-            if m:  # every rank has finished every call of this family: forget its watchdog state
-                nv.check(self._lib.flexar_comm_clear_error(self._h), "clear_error")
+                if e:
+                    self.selftest_notes.setdefault(r, []).append(e)
+            if m:
+                if self.rank == 0:
+                    nv.log_warn("self-test: family " + ",".join(nv.family_names(m)) + " failed: " +
+                                "; ".join(f"rank {r}: {e}" for r, (_, f, e) in enumerate(rows) if e))
+                # every rank has finished every call of this family (the exchange above): a launch that never
+                # ran left its rank's epochs behind, so the protocol state is reset on every rank, and nobody
+                # starts the next family before every rank has reset
+                nv.check(self._lib.flexar_comm_resync(self._h), "resync")
+                exchange(b"")
             return m
 
         mask = 0
@@ -273,15 +315,19 @@ class Communicator:
             self.selftest_recovered = nv.family_names(mask & ~again)
             mask = again
         if mask:
-            # every rank has finished every self-test call (the exchange above): forget the watchdog state
-            nv.check(self._lib.flexar_comm_clear_error(self._h), "clear_error")
             nv.check(self._lib.flexar_comm_set_disabled(self._h, mask), "set_disabled")
             self.selftest_failed = nv.family_names(mask)
             exchange(b"")  # nobody issues a production call before every rank installed the mask
             tested = sum(nv.FAMILIES[n] for n in self.topology()["selftested"].split(",") if n in nv.FAMILIES)
             if tested & ~mask == 0:
-                self.close()
-                raise nv.FlexarError(2, "no device protocol passed the connect-time self-test on this node")
+                raise self._agreed(nv.FlexarError(2, "no device protocol passed the connect-time self-test on this "
+                                                     "node: " + "; ".join(f"rank {r}: {' / '.join(v)}"
+                                                                          for r, v in self.selftest_notes.items())))
+
+    def _selftest_note(self) -> str:
+        b = ctypes.create_string_buffer(1024)
+        self._lib.flexar_comm_selftest_note(self._h, b, 1024)
+        return b.value.decode(errors="replace")
 
     def topology(self) -> dict:
         """Connect-time probe: per-peer PCI bus id, device, link class and hop count; self-test state."""
@@ -640,16 +686,23 @@ class Communicator:
                                             algo.encode() if algo else None), "broadcast")
         return dst
 
-    def close(self):
+    def close(self, collective: bool = True):
+        """Tear the communicator down. Collective (every rank, in the same order, like creation): the
+        library drains this rank's calls, agrees with every peer that all calls have finished, closes the
+        peer mappings (workspaces and registrations), agrees that every rank has unmapped, and only then
+        frees (flexar_comm_destroy). ``collective=False`` (garbage collection) skips the agreements and
+        leaves this rank's exported buffers allocated until the process exits."""
         if getattr(self, "_h", None) is not None and self._h.value:
             self._hi = 0
-            self._lib.flexar_comm_destroy(self._h)  # also closes the registrations' peer mappings
-            self._h = ctypes.c_void_p()
+            h, self._h = self._h, ctypes.c_void_p()
             self._regs = {}
+            rc = (self._lib.flexar_comm_destroy if collective else self._lib.flexar_comm_destroy_local)(h)
+            if rc and collective:
+                nv.log_warn(f"rank {self.rank}: close: {nv.last_error()}")
 
     def __del__(self):
         try:
-            self.close()
+            self.close(collective=False)  # GC order differs per rank: never wait for peers here
         except Exception:
             pass
 

@@ -121,6 +121,104 @@ class Budget:
         return False
 
 
+def configure_env(world: int, rank: int, local: int, environ) -> tuple:
+    """The environment of one bench rank, set before HIP initialises; returns (local device, shared,
+    shared_rccl). One GPU per rank (the driver's N-GPU run) gets nothing shared-GPU-specific: no hardware
+    queue cap and no grid clamp (tests/test_bench_launch.py pins this).
+
+    FLEXAR_BENCH_SHARED_GPU=1: rehearsal of the multi-rank flow with every rank on device 0 (a 1-GPU box).
+    By default the reference result and barriers use gloo and the RCCL comparison is skipped; the numbers
+    measure one shared HBM, not xGMI. FLEXAR_BENCH_SHARED_RCCL=1 (with SHARED_GPU): the driver's own flow on
+    one GPU - "nccl" process group, RCCL reference and comparator, the '+rccl' message-transport candidates.
+    RCCL refuses two ranks on one GPU of one host, so every rank gets its own NCCL_HOSTID: RCCL then treats
+    the ranks as separate hosts and carries their messages over its socket transport on loopback (RCCL
+    numbers are not xGMI figures)."""
+    shared = environ.get("FLEXAR_BENCH_SHARED_GPU", "0") == "1"
+    shared_rccl = shared and world > 1 and environ.get("FLEXAR_BENCH_SHARED_RCCL", "0") == "1"
+    if shared_rccl:
+        environ["NCCL_HOSTID"] = f"flexar-bench-rank{rank}"  # must differ per rank
+        environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        environ.setdefault("NCCL_IB_DISABLE", "1")
+    if shared:
+        local = 0
+        # 8 processes x HIP's default 4 hardware queues oversubscribe the GPU's compute queues: the command
+        # processor then time-slices the processes and every cross-rank hand-off waits for a queue switch
+        # (measured: 28.6 ms instead of 1.0 ms per 256 MiB call at N = 8). Set before HIP initialises.
+        if world > 4:
+            environ.setdefault("GPU_MAX_HW_QUEUES", "2")
+        # every rank's workgroups must be co-resident on the one GPU (they spin on each other)
+        environ.setdefault("FLEXAR_MAX_GRID", str(max(8, 256 // (2 * world))))
+    return local, shared, shared_rccl
+
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(n: int, child_argv, python=None, timeout_s=None) -> int:
+    """`bench.py --gpus N` with no launcher (WORLD_SIZE unset): start the N ranks here, one process per GPU,
+    like the reference's driver is started by mpiexec and reads MPI_Comm_size (allreduce_over_mpi/
+    benchmark.cpp:48-52). This process makes NO GPU call (HIP is initialised only in the children, which
+    are started as new processes, never exec'd over this one); each child gets RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR / MASTER_PORT, rank 0's stdout (the JSON line) is passed through, every other
+    rank's stdout goes to stderr. A failed rank ends the others; the exit code is the first failure's."""
+    import subprocess
+    import threading
+
+    port = _free_port()
+    procs, lines = [], []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([python or sys.executable] + list(child_argv), env=env,
+                                      stdout=subprocess.PIPE, text=True))
+
+    def pump(r):  # every rank's stdout, line by line (a full pipe must never stall a rank)
+        for line in procs[r].stdout:
+            if r == 0 and line.lstrip().startswith("{"):
+                lines.append(line)
+            else:
+                sys.stderr.write(line)
+
+    pumps = [threading.Thread(target=pump, args=(r,), daemon=True) for r in range(n)]
+    for t in pumps:
+        t.start()
+    t0 = time.monotonic()
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        failed = [c for c in codes if c not in (None, 0)]
+        if failed and not rc:
+            rc = failed[0]
+            print(f"[bench] a rank exited with {rc}: stopping the others", file=sys.stderr, flush=True)
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+        if all(c is not None for c in codes):
+            break
+        if timeout_s and time.monotonic() - t0 > timeout_s:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            rc = rc or 124
+        time.sleep(0.05)
+    for t in pumps:
+        t.join(timeout=10)
+    js = lines
+    if js and rc == 0:
+        print(js[-1].rstrip("\n"), flush=True)
+    elif rc == 0:
+        print("[bench] rank 0 printed no JSON line", file=sys.stderr, flush=True)
+        rc = 1
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -147,6 +245,9 @@ def main():
                     help="Communicator transport at N > 1 (rccl: IPC + the '+rccl' message transport candidates)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: this process starts the N ranks itself (and never touches the GPU)
+        sys.exit(self_launch(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -161,30 +262,10 @@ def main():
     import torch
     import torch.distributed as dist
 
-    # FLEXAR_BENCH_SHARED_GPU=1: rehearsal of the multi-rank flow with every rank on device 0 (a 1-GPU
-    # box). By default the reference result and barriers use gloo and the RCCL comparison is skipped; the
-    # numbers measure one shared HBM, not xGMI.
-    shared = os.environ.get("FLEXAR_BENCH_SHARED_GPU", "0") == "1"
-    # FLEXAR_BENCH_SHARED_RCCL=1 (with SHARED_GPU): the driver's own flow on one GPU - "nccl" process group,
-    # RCCL reference and comparator, the '+rccl' message-transport candidates. RCCL refuses two ranks on one
-    # GPU of one host, so every rank gets its own NCCL_HOSTID: RCCL then treats the ranks as separate hosts
-    # and carries their messages over its socket transport on loopback (RCCL numbers are not xGMI figures).
-    shared_rccl = shared and world > 1 and os.environ.get("FLEXAR_BENCH_SHARED_RCCL", "0") == "1"
+    local, shared, shared_rccl = configure_env(world, rank, local, os.environ)
     host_ref = shared and not shared_rccl  # gloo process group: references and reductions on the host
-    if shared_rccl:
-        os.environ["NCCL_HOSTID"] = f"flexar-bench-rank{rank}"  # must differ per rank
-        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
-        os.environ.setdefault("NCCL_IB_DISABLE", "1")
     if shared:
-        local = 0
-        # 8 processes x HIP's default 4 hardware queues oversubscribe the GPU's compute queues: the command
-        # processor then time-slices the processes and every cross-rank hand-off waits for a queue switch
-        # (measured: 28.6 ms instead of 1.0 ms per 256 MiB call at N = 8). Set before HIP initialises.
-        if world > 4:
-            os.environ.setdefault("GPU_MAX_HW_QUEUES", "2")
         args.no_rccl = args.no_rccl or not shared_rccl
-        # every rank's workgroups must be co-resident on the one GPU (they spin on each other)
-        os.environ.setdefault("FLEXAR_MAX_GRID", str(max(8, 256 // (2 * world))))
     ndev = torch.cuda.device_count()
     if not shared and ndev and local >= ndev:
         # a launcher that restricts each rank to its own GPU (HIP_VISIBLE_DEVICES per rank): that GPU is device 0
@@ -284,19 +365,13 @@ def main():
             log(rank, f"zero-copy candidates skipped: {e}")
             return False
 
-    def quiesce():
-        """Collective, after a communicator's close: no rank allocates, exports or maps the next communicator's
-        memory while a peer still holds mappings of the old one (IPC imports of freed workspaces and
-        registered buffers are all closed everywhere first)."""
-        if world > 1:
-            max_over_ranks(0.0)
-
     def rebuild(why):
-        """Collective: a failed call may leave epochs / flags inconsistent - start from a fresh communicator."""
+        """Collective: a failed call may leave epochs / flags inconsistent - start from a fresh communicator.
+        close() is collective in the library (flexar_comm_destroy agrees with every peer that all calls have
+        finished and that every rank has unmapped before anything is freed), so the next communicator's
+        memory is never allocated, exported or mapped while a peer still maps the old one."""
         nonlocal comm, fallback
         comm.close()
-        torch.cuda.synchronize()
-        quiesce()
         comm = make_comm() or RcclOnly(dist)
         if isinstance(comm, RcclOnly):
             fallback = f"flexar communicator could not be rebuilt ({why})"
@@ -508,9 +583,7 @@ def main():
             torch.cuda.synchronize()
             comm = RcclOnly(dist)
         elif attempt > 0:  # the failed attempt may have left epochs / flags inconsistent
-            comm.close()
-            torch.cuda.synchronize()
-            quiesce()
+            comm.close()  # collective teardown (see rebuild)
             comm = make_comm() or RcclOnly(dist)
             if isinstance(comm, RcclOnly):
                 rejected[algo] = "the flexar communicator could not be rebuilt"

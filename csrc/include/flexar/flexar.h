@@ -86,7 +86,13 @@ size_t flexar_handle_size(void);
 int flexar_comm_export(flexar_comm_t comm, void* handle_out);
 /* all_handles: nranks * flexar_handle_size() bytes, rank-major. */
 int flexar_comm_connect(flexar_comm_t comm, const void* all_handles);
+/* Collective teardown (every rank of a connected communicator): drains this rank's work, agrees with
+ * every peer (a host shared-memory page) that all calls have finished, closes the peer mappings, agrees
+ * that every rank has unmapped, then frees. A peer that does not arrive within FLEXAR_TIMEOUT_MS leaves
+ * this rank's exported buffers allocated and returns FLEXAR_ERR_TIMEOUT (the communicator is gone). */
 int flexar_comm_destroy(flexar_comm_t comm);
+/* Non-collective teardown (garbage collection): no agreement; exported buffers stay allocated. */
+int flexar_comm_destroy_local(flexar_comm_t comm);
 int flexar_comm_rank(flexar_comm_t comm);
 int flexar_comm_size(flexar_comm_t comm);
 
@@ -154,6 +160,11 @@ int flexar_comm_clear_error(flexar_comm_t comm);
  * them with flexar_comm_set_disabled: calls then move to a verified family (ll -> oneshot,
  * fence -> +wt -> dma) or fail with FLEXAR_ERR_UNSUPPORTED when none is left. */
 int flexar_comm_selftest(flexar_comm_t comm, uint32_t families, uint32_t* failed_out);
+/* Why families failed on this rank in the last self-test (HIP errors named); "" = none failed. */
+int flexar_comm_selftest_note(flexar_comm_t comm, char* buf, size_t buflen);
+/* Collective protocol reset (every rank, between two agreements that no call is in flight / every rank
+ * has reset): flags, epochs, staging and the error word back to their state after connect. */
+int flexar_comm_resync(flexar_comm_t comm);
 int flexar_comm_set_disabled(flexar_comm_t comm, uint32_t families);
 /* Message transport (RCCL ncclSend/ncclRecv + local executor segments; family 16): algorithm suffix "+rccl",
  * or every call when IPC mapping is unavailable. RCCL is resolved at run time (the process's librccl). */
@@ -198,6 +209,8 @@ size_t flexar_probe_blob_size(void);
 int flexar_comm_probe_export(flexar_comm_t comm, void* out);
 int flexar_comm_probe_agree(flexar_comm_t comm, const void* all_blobs);
 int flexar_probe_agree(const void* all_blobs, int nranks, int* links_out); /* host-only check of the blobs */
+int flexar_probe_agree_resident(const void* all_blobs, int nranks, int* links_out, int* resident_out);
+uint64_t flexar_settings_fingerprint(int with_calib); /* env settings hash (1 = connect form, 0 = cache form) */
 /* Connect-time calibration (collective, after the self-test): mode 0 off, 1 cached-or-measure, 2 measure.
  * Times fixed executor schedules, max over ranks, fits and installs the cost model; caches it on disk per
  * (arch, N, links, link classes, disabled families, version). Writes a JSON report. */
@@ -260,6 +273,9 @@ void flexar_device_free(void* p);
 int flexar_kernel_info(int dtype, int op, int kind, int proto, int* blocks_per_cu, int* vgprs);
 
 /* ---- host-only planning utilities (no GPU needed) ------------------------ */
+/* The collective-teardown agreement alone (tests): `phases` host barriers of `nranks` processes on the
+ * shared-memory page `name`. 0, or FLEXAR_ERR_TIMEOUT with the straggler in flexar_last_error(). */
+int flexar_host_barrier_run(const char* name, int rank, int nranks, int phases, uint64_t timeout_ms, int delay_ms);
 /* Readiness downgrade chain (see flexar_comm_selftest) applied to `spec` for nranks with the given
  * failed-family mask; writes the spec a call would run, or returns FLEXAR_ERR_UNSUPPORTED. */
 int flexar_downgrade_spec(const char* spec, int nranks, uint32_t disabled, int allow_dma, char* out, size_t outlen);

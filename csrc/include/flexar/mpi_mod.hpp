@@ -424,6 +424,8 @@ inline HostComm* host_comm(MPI_Comm comm) {
 }
 
 // ---- device buffers: flexar GPU communicator bootstrapped over MPI ------------------------------
+// Deleted by MPI when the communicator's attributes go (MPI_Comm_free / MPI_Finalize, collective): the
+// device communicator's teardown agrees with its peers by itself (flexar_comm_destroy, host_barrier.hpp).
 struct DevHolder {
   flexar_comm_t c = nullptr;
   ~DevHolder() {
@@ -475,15 +477,25 @@ inline flexar_comm_t device_comm(MPI_Comm comm) {
   if (size > 1 && !(getenv("FLEXAR_SELFTEST") && strcmp(getenv("FLEXAR_SELFTEST"), "0") == 0)) {
     // one family at a time behind a barrier, and a failed family once more before it is disabled (a rank
     // arriving past its peers' short watchdog must not shift every later family out of step)
+    // A HIP error on one rank fails that family there (named by flexar_comm_selftest_note) and the
+    // downgrade chain goes on; only an error that left a device unusable (non-zero rc, agreed on) ends here
     auto run = [&](uint32_t fam) -> uint32_t {
       uint32_t failed = 0, any = 0;
       MPI_Barrier(comm);
-      if (flexar_comm_selftest(d->c, fam, &failed)) {
-        fprintf(stderr, "[flexar] rank %d self-test: %s\n", rank, flexar_last_error());
-        abort();
+      int rc = flexar_comm_selftest(d->c, fam, &failed), worst = 0;
+      if (rc) fprintf(stderr, "[flexar] rank %d self-test: %s\n", rank, flexar_last_error());
+      MPI_Allreduce(&rc, &worst, 1, MPI_INT, MPI_MAX, comm);
+      if (worst) abort();
+      if (failed) {
+        char note[512];
+        flexar_comm_selftest_note(d->c, note, sizeof(note));
+        fprintf(stderr, "[flexar] rank %d self-test: %s\n", rank, note);
       }
       MPI_Allreduce(&failed, &any, 1, MPI_UINT32_T, MPI_BOR, comm);
-      if (any) flexar_comm_clear_error(d->c);  // every rank is past this family's calls
+      if (any) {  // every rank is past this family's calls: reset the protocol state, then start together
+        flexar_comm_resync(d->c);
+        MPI_Barrier(comm);
+      }
       return any;
     };
     uint32_t any = 0;
@@ -495,7 +507,6 @@ inline flexar_comm_t device_comm(MPI_Comm comm) {
       any = again;
     }
     if (any) {
-      flexar_comm_clear_error(d->c);  // every rank is past its self-test calls (the allreduce above)
       flexar_comm_set_disabled(d->c, any);
       fprintf(stderr, "[flexar] rank %d: protocol families failing the self-test disabled: %s\n", rank,
               family_names(any).c_str());

@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 
 #include "flexar/topology.hpp"
@@ -158,12 +159,18 @@ struct ProbeBlob {
   uint64_t fingerprint;   // settings fingerprint, recomputed after the probe
   int8_t cls[16];         // link class of every peer as this rank sees it
   int8_t hops[16];
+  int32_t resident;       // executor workgroups this rank's GPU keeps resident (0 = unknown)
+  int32_t reserved;
 };
 constexpr uint32_t kProbeMagic = 0xF1E8B10Bu;
 
 // Returns true and the agreed link count, or false with a message naming the disagreement.
-inline bool probe_agree(const ProbeBlob* all, int nranks, int* links_out, std::string* why) {
-  int links = 1 << 30;
+// `resident_out` (optional): the minimum of the ranks' known resident-workgroup counts (0 = none known) -
+// the grid clamp must be the same on every rank, or the per-workgroup flag protocol pairs workgroups that
+// do not exist on the peer.
+inline bool probe_agree(const ProbeBlob* all, int nranks, int* links_out, std::string* why,
+                        int* resident_out = nullptr) {
+  int links = 1 << 30, resident = 0;
   for (int r = 0; r < nranks; ++r) {
     const ProbeBlob& a = all[r];
     if (a.magic != kProbeMagic || a.rank != r) {
@@ -176,6 +183,7 @@ inline bool probe_agree(const ProbeBlob* all, int nranks, int* links_out, std::s
       return false;
     }
     links = std::min(links, (int)a.links);
+    if (a.resident > 0) resident = resident ? std::min(resident, (int)a.resident) : (int)a.resident;
     for (int p = 0; p < nranks; ++p) {
       if (p == r) continue;
       const int8_t rp = a.cls[p], pr = all[p].cls[r];
@@ -190,6 +198,7 @@ inline bool probe_agree(const ProbeBlob* all, int nranks, int* links_out, std::s
     }
   }
   if (links_out) *links_out = links < 1 ? 1 : links;
+  if (resident_out) *resident_out = resident;
   return true;
 }
 
@@ -209,11 +218,23 @@ inline const char* const* fingerprint_vars() {
                             nullptr};
   return v;
 }
-inline uint64_t env_fingerprint(const std::string& extra) {
+// FLEXAR_CALIB as the mode it selects: unset and "1" behave the same, "off" is "0", "2" is "force".
+inline std::string calib_mode_name(const char* e) {
+  const std::string v = e ? e : "";
+  if (v == "0" || v == "off") return "0";
+  if (v == "force" || v == "2") return "force";
+  return "1";
+}
+// `with_calib` = false: the fingerprint the calibration cache is keyed by - the calibration mode decides
+// whether the cache is read, not what a schedule costs, so a forced run writes the cache default runs read
+// (ADVICE r3). Ranks still agree on the (normalised) mode through the connect-time fingerprint.
+inline uint64_t env_fingerprint(const std::string& extra, bool with_calib = true) {
   uint64_t h = fnv1a(extra);
   for (const char* const* v = fingerprint_vars(); *v; ++v) {
+    const bool calib = !strcmp(*v, "FLEXAR_CALIB");
+    if (calib && !with_calib) continue;
     const char* e = getenv(*v);
-    h = fnv1a(std::string(*v) + "=" + (e ? e : "") + ";", h);
+    h = fnv1a(std::string(*v) + "=" + (calib ? calib_mode_name(e) : std::string(e ? e : "")) + ";", h);
   }
   return h;
 }

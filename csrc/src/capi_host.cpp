@@ -20,6 +20,7 @@
 #include "flexar/planner.hpp"
 #include "flexar/readiness.hpp"
 #include "flexar/zc_policy.hpp"
+#include "host_barrier.hpp"
 #include "internal.hpp"
 
 namespace flexar {
@@ -546,6 +547,19 @@ int flexar_probe_agree(const void* blobs, int nranks, int* links_out) {
   if (!probe_agree(v.data(), nranks, links_out, &why)) { set_error(why); return FLEXAR_ERR_INVALID; }
   return 0;
 }
+// Settings fingerprint of this process's environment (readiness.hpp env_fingerprint, no tune table):
+// with_calib = 1 is the connect-time form, 0 the calibration cache's.
+uint64_t flexar_settings_fingerprint(int with_calib) { return env_fingerprint("", with_calib != 0); }
+
+// The same, also returning the agreed resident-workgroup count (0 = no rank knew its own).
+int flexar_probe_agree_resident(const void* blobs, int nranks, int* links_out, int* resident_out) {
+  if (!blobs || nranks < 1 || nranks > 16) { set_error("bad arguments"); return FLEXAR_ERR_INVALID; }
+  std::vector<ProbeBlob> v(nranks);
+  memcpy(v.data(), blobs, sizeof(ProbeBlob) * nranks);
+  std::string why;
+  if (!probe_agree(v.data(), nranks, links_out, &why, resident_out)) { set_error(why); return FLEXAR_ERR_INVALID; }
+  return 0;
+}
 
 // ---- calibration helpers (calibration.hpp), host-only: the device measurement is flexar_comm_calibrate ----
 static std::vector<CalibRow> calib_rows(int nrows, const char* specs_nl, const double* bytes, const double* us) {
@@ -620,6 +634,42 @@ int flexar_reduce_host(void* dst, const void* const* srcs, int nsrc, size_t coun
   if (!dst || !srcs || nsrc < 1) { set_error("bad reduce arguments"); return FLEXAR_ERR_INVALID; }
   float fs = scale * (op == FLEXAR_AVG ? 1.0f / (float)nsrc : 1.0f);
   return dispatch_dtype_op<HostReduce>(dtype, op, dst, srcs, nsrc, count, fs);
+}
+
+
+// The teardown agreement (host_barrier.hpp) on its own, for CPU tests: join `name` as `rank` of `nranks`,
+// pass `phases` barriers, sleeping `delay_ms` before each. Returns 0, or FLEXAR_ERR_TIMEOUT naming the
+// straggler (flexar_last_error). Rank 0 removes the name after the first barrier.
+int flexar_host_barrier_run(const char* name, int rank, int nranks, int phases, uint64_t timeout_ms, int delay_ms) {
+  if (!name || nranks < 1 || nranks > (int)kMaxRanks || rank < 0 || rank >= nranks) {
+    set_error("bad arguments");
+    return FLEXAR_ERR_INVALID;
+  }
+  HostBarrier hb;
+  std::string err;
+  if (!hb.join(name, rank, nranks, &err)) {
+    set_error(err);
+    return FLEXAR_ERR_STATE;
+  }
+  for (int p = 0; p < phases; ++p) {
+    if (delay_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(delay_ms));
+    int late = -1;
+    uint64_t mx = 0;
+    // odd phases also exchange a value: the maximum of rank * 1000 + phase is the last rank's
+    const bool ok = (p & 1) ? hb.exchange_max((uint64_t)rank * 1000 + p, &mx, timeout_ms, &late)
+                            : hb.arrive_and_wait(timeout_ms, &late);
+    if (!ok) {
+      hb.unlink();
+      set_error("phase " + std::to_string(p) + ": rank " + std::to_string(late) + " did not arrive");
+      return FLEXAR_ERR_TIMEOUT;
+    }
+    if ((p & 1) && mx != (uint64_t)(nranks - 1) * 1000 + p) {
+      set_error("phase " + std::to_string(p) + ": exchanged maximum " + std::to_string(mx));
+      return FLEXAR_ERR_STATE;
+    }
+    if (p == 0 && rank == 0) hb.unlink();
+  }
+  return 0;
 }
 
 }  // extern "C"

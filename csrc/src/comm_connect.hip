@@ -1,7 +1,9 @@
 // flexar communicator lifecycle: create, export, connect (readiness gate), self-test, configuration
 // setters, topology report, destroy. Reference counterpart: FlexTree_Context and the lazily created
 // scratch buffer (allreduce_over_mpi/mpi_mod.hpp:216-243, 931-950).
+#include <atomic>
 #include <chrono>
+#include <random>
 
 #include "comm_internal.hpp"
 
@@ -9,11 +11,11 @@ namespace flexar {
 
 // Settings fingerprint exchanged in the handle (readiness.hpp): environment knobs + workspace size +
 // the loaded tune table.
-uint64_t comm_fingerprint(flexar_comm* c) {
+uint64_t comm_fingerprint(flexar_comm* c, bool with_calib) {
   std::string extra = "ws=" + std::to_string(c->ws_bytes) + ";";
   for (auto& n : c->tune.rows)
     for (auto& row : n.second) extra += std::to_string(n.first) + " " + std::to_string(row.first) + " " + row.second + ";";
-  return env_fingerprint(extra);
+  return env_fingerprint(extra, with_calib);
 }
 
 // Self-test pattern (flexar_comm_selftest): rank r contributes (r + 1) * p(i), p(i) in [1, 1000], so
@@ -171,6 +173,22 @@ int flexar_comm_create(int rank, int nranks, int device, size_t workspace_bytes,
   c->peer_stg[rank] = c->stg;
   c->peer_flags[rank] = c->flags;
   if (nranks == 1) c->connected = true;
+  {
+    std::random_device rd;
+    c->nonce = ((uint64_t)rd() << 32) ^ rd() ^ ((uint64_t)getpid() << 17) ^
+               (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+  }
+  // FLEXAR_TEST_SELFTEST_HIP="RANK:FAMILIES[:COMMS]" (tests only): the self-test launches of those families
+  // fail with a real HIP launch error on that rank (an invalid block size: not sticky, the device stays
+  // usable), in the first COMMS multi-rank communicators this process creates (default: all of them)
+  static std::atomic<int> created{0};
+  const int serial = nranks > 1 ? created.fetch_add(1) : -1;
+  if (const char* t = getenv("FLEXAR_TEST_SELFTEST_HIP")) {
+    int rk = -1, comms = 1 << 30;
+    unsigned fams = 0;
+    if (sscanf(t, "%d:%u:%d", &rk, &fams, &comms) >= 2 && rk == rank && serial >= 0 && serial < comms)
+      c->test_hip_fail = fams;
+  }
   *out = c.release();
   return 0;
 }
@@ -233,6 +251,7 @@ int flexar_comm_export(flexar_comm_t c, void* handle_out) {
     snprintf(h.bus, sizeof(h.bus), "dev%d", c->device);
   }
   h.fingerprint = comm_fingerprint(c);
+  h.nonce = c->nonce;
   memcpy(handle_out, &h, sizeof(h));
   return 0;
 }
@@ -247,6 +266,16 @@ int flexar_comm_connect(flexar_comm_t c, const void* all) {
   FX_HIP(hipSetDevice(c->device));
   const CommHandle* hs = (const CommHandle*)all;
   const CommHandle& me = hs[c->rank];
+  // Join the teardown agreement first (every rank gets the same handle bytes, so every rank that reaches
+  // connect joins, whatever fails below): flexar_comm_destroy is collective from here on.
+  if (!c->hb && c->nranks > 1 && hs[0].magic == kHandleMagic && hs[0].nranks == c->nranks) {
+    char name[96];
+    snprintf(name, sizeof(name), "/flexar.%d.%016llx", (int)hs[0].pid, (unsigned long long)hs[0].nonce);
+    std::unique_ptr<HostBarrier> hb(new HostBarrier);
+    std::string err;
+    if (hb->join(name, c->rank, c->nranks, &err)) c->hb = std::move(hb);
+    else logf(LOG_WARN, c->rank, "connect: %s: teardown falls back to deferred frees", err.c_str());
+  }
   for (int r = 0; r < c->nranks; ++r) {
     const CommHandle& h = hs[r];
     const std::string who = "rank " + std::to_string(r);
@@ -364,12 +393,26 @@ int flexar_comm_connect(flexar_comm_t c, const void* all) {
 // hand-off never becomes visible fails in seconds instead of hanging. Returns the mask of families
 // that failed ON THIS RANK; the caller ORs the masks of all ranks and installs the result with
 // flexar_comm_set_disabled (a family is usable only if it passed everywhere).
+//
+// A HIP error on this rank (a failed launch, a failed kernel) fails the family it happened in, with the
+// error named in flexar_comm_selftest_note(), as long as the device is still usable; every rank still
+// makes every collective call of the family. Only a sticky error (hipDeviceSynchronize fails too: the
+// device context is gone) returns FLEXAR_ERR_HIP. After any failure the caller agrees on it and runs the
+// collective flexar_comm_resync before the next family: a launch that never ran leaves this rank's
+// epochs behind its peers'.
 int flexar_comm_selftest(flexar_comm_t c, uint32_t families, uint32_t* failed_out) {
   if (!c || !failed_out) { set_error("null argument"); return FLEXAR_ERR_INVALID; }
   if (!c->connected) { set_error("communicator not connected"); return FLEXAR_ERR_STATE; }
   *failed_out = 0;
+  c->selftest_note.clear();
   if (c->nranks == 1) return 0;
   FX_HIP(hipSetDevice(c->device));
+  // HIP keeps a failed call's error for the thread until it is read: one left by an earlier, unrelated
+  // call (the framework, a teardown) must not be taken for a self-test launch failure (round 3's driver
+  // record: "self-test: HIP error" with no name). Name it and drop it.
+  if (const hipError_t stale = hipGetLastError(); stale != hipSuccess)
+    logf(LOG_WARN, c->rank, "self-test: cleared a HIP error an earlier call left in this thread: %s",
+         hipGetErrorString(stale));
   const uint64_t n = 65536 + 77;  // 256 KiB + an odd tail: several workgroups, a scalar tail, LL-sized
   if (!c->st_buf) {
     FX_HIP(hipMalloc(&c->st_buf, 2 * n * sizeof(int)));
@@ -393,6 +436,11 @@ int flexar_comm_selftest(flexar_comm_t c, uint32_t families, uint32_t* failed_ou
     families &= PF_MSG;
     *failed_out |= PF_ALL;
   }
+  std::string note;
+  auto fail = [&](uint32_t fam, const std::string& why) {
+    *failed_out |= fam;
+    if (note.size() < 480) note += (note.empty() ? "" : "; ") + why;
+  };
   int* in = c->st_buf;
   int* out = c->st_buf + n;
   const int N = c->nranks;
@@ -403,22 +451,40 @@ int flexar_comm_selftest(flexar_comm_t c, uint32_t families, uint32_t* failed_ou
     c->selftested |= k.fam;
     logf(LOG_INFO, c->rank, "self-test: %s", k.spec);
     for (int call = 0; call < 3 && !rc; ++call) {
+      const std::string at = std::string(k.spec) + " call " + std::to_string(call);
       const uint32_t salt = (uint32_t)(call * 131 + k.fam * 17);
-      hipLaunchKernelGGL(selftest_fill, dim3(64), dim3(256), 0, st, in, out, n, c->rank, salt);
-      if ((rc = hipGetLastError() != hipSuccess ? FLEXAR_ERR_HIP : 0)) break;
-      int e = flexar_allreduce_ex(c, in, out, n, FLEXAR_INT32, FLEXAR_SUM, st, k.spec, 1.0f);
-      if (e == FLEXAR_ERR_TIMEOUT || e == FLEXAR_ERR_STATE) {
-        *failed_out |= k.fam;  // a previous call of this family timed out
-      } else if (e) {
-        rc = e;
-        break;
-      }
-      *c->st_bad = 0;
+      const bool inject = (c->test_hip_fail & k.fam) != 0;  // tests: an invalid block size
+      hipLaunchKernelGGL(selftest_fill, dim3(64), dim3(inject ? 4096 : 256), 0, st, in, out, n, c->rank, salt);
+      const hipError_t le = hipGetLastError();
+      if (le != hipSuccess) fail(k.fam, at + ": selftest_fill launch: " + hipGetErrorString(le));
+      // the collective call is made whatever happened above: every rank makes every call of the family
+      set_error("");
+      const int e = flexar_allreduce_ex(c, in, out, n, FLEXAR_INT32, FLEXAR_SUM, st, k.spec, 1.0f);
+      if (e) fail(k.fam, at + ": " + (*flexar_last_error() ? flexar_last_error() : "error " + std::to_string(e)));
+      __atomic_store_n(c->st_bad, 0u, __ATOMIC_RELEASE);
       hipLaunchKernelGGL(selftest_check, dim3(64), dim3(256), 0, st, out, n, N, salt, c->st_bad_dev);
-      if (hipStreamSynchronize(st) != hipSuccess) { rc = FLEXAR_ERR_HIP; break; }
-      if (__atomic_load_n(c->st_bad, __ATOMIC_ACQUIRE) != 0) *failed_out |= k.fam;
-      if (__atomic_load_n(c->err_host, __ATOMIC_ACQUIRE) != 0) {
-        *failed_out |= k.fam;
+      const hipError_t ce = hipGetLastError();
+      if (ce != hipSuccess) fail(k.fam, at + ": selftest_check launch: " + hipGetErrorString(ce));
+      const hipError_t se = hipStreamSynchronize(st);
+      if (se != hipSuccess) {
+        (void)hipGetLastError();
+        const hipError_t de = hipDeviceSynchronize();
+        (void)hipGetLastError();
+        if (de != hipSuccess) {  // sticky: nothing more can run in this process
+          set_error("self-test " + at + ": hipStreamSynchronize: " + hipGetErrorString(se) +
+                    "; the device is unusable (hipDeviceSynchronize: " + hipGetErrorString(de) + ")");
+          rc = FLEXAR_ERR_HIP;
+          break;
+        }
+        fail(k.fam, at + ": hipStreamSynchronize: " + hipGetErrorString(se));
+        continue;
+      }
+      if (le == hipSuccess && ce == hipSuccess && !e) {
+        const uint32_t bad = __atomic_load_n(c->st_bad, __ATOMIC_ACQUIRE);
+        if (bad) fail(k.fam, at + ": " + std::to_string(bad) + " of " + std::to_string(n) + " sums wrong");
+      }
+      if (const uint32_t w = __atomic_load_n(c->err_host, __ATOMIC_ACQUIRE)) {
+        if (!(*failed_out & k.fam)) fail(k.fam, at + ": device watchdog (word " + std::to_string(w) + ")");
         __atomic_store_n(c->err_host, 0u, __ATOMIC_RELEASE);  // every rank still makes every call
       }
     }
@@ -426,6 +492,7 @@ int flexar_comm_selftest(flexar_comm_t c, uint32_t families, uint32_t* failed_ou
   }
   (void)hipStreamSynchronize(st);
   (void)hipStreamDestroy(st);
+  (void)hipGetLastError();  // a family's failure is reported above, never at the caller's next launch
   c->have_last = false;  // `st` is gone (and synchronised): the next call must not order behind it
   c->timeout_ticks = saved_timeout;
   c->disabled = saved_disabled;
@@ -433,10 +500,40 @@ int flexar_comm_selftest(flexar_comm_t c, uint32_t families, uint32_t* failed_ou
   c->calls = saved_calls;
   c->bytes = saved_bytes;
   c->memo_gen = saved_gen + 1;
-  if (rc == FLEXAR_ERR_HIP && std::string(flexar_last_error()).empty()) set_error("self-test: HIP error");
-  logf(*failed_out ? LOG_WARN : LOG_INFO, c->rank, "self-test: ran %s, failed on this rank: %s",
-       family_names(c->selftested).c_str(), family_names(*failed_out).c_str());
+  c->selftest_note = note;
+  if (!rc) set_error("");
+  logf(*failed_out ? LOG_WARN : LOG_INFO, c->rank, "self-test: ran %s, failed on this rank: %s%s%s",
+       family_names(c->selftested).c_str(), family_names(*failed_out).c_str(), note.empty() ? "" : " - ",
+       note.c_str());
   return rc;
+}
+
+// Why families failed on this rank in the last self-test ("" = none did).
+int flexar_comm_selftest_note(flexar_comm_t c, char* buf, size_t buflen) {
+  if (!c || !buf || !buflen) return FLEXAR_ERR_INVALID;
+  snprintf(buf, buflen, "%s", c->selftest_note.c_str());
+  return c->selftest_note.size() < buflen ? 0 : FLEXAR_ERR_NOMEM;
+}
+
+// Collective recovery of the peer-memory protocol state (every rank, after an agreement that every
+// rank's calls have completed, and followed by one that every rank has reset before any rank issues a
+// call): this rank's flags, call epochs, staging (LL / amax granules) and error word return to their
+// state after connect. Needed after a call that did not launch on some rank (its epochs fell behind its
+// peers'); a plain watchdog timeout only needs flexar_comm_clear_error.
+int flexar_comm_resync(flexar_comm_t c) {
+  if (!c) return FLEXAR_ERR_INVALID;
+  FX_HIP(hipSetDevice(c->device));
+  FX_HIP(hipDeviceSynchronize());
+  FX_HIP(hipMemset(c->flags, 0, kFlagWords * sizeof(uint64_t)));
+  FX_HIP(hipMemset(c->epochs, 0, kMaxGridBlocks * sizeof(uint64_t)));
+  FX_HIP(hipMemset(c->stg, 0, c->ws_bytes));
+  if (c->msg_epochs) FX_HIP(hipMemset(c->msg_epochs, 0, kMaxGridBlocks * sizeof(uint64_t)));
+  FX_HIP(hipDeviceSynchronize());
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->launches = 0;
+  c->have_last = false;
+  __atomic_store_n(c->err_host, 0u, __ATOMIC_RELEASE);
+  return 0;
 }
 
 // Cost-model time (us) of `spec` on this communicator's model (links from the connect-time probe).
@@ -536,10 +633,48 @@ int flexar_comm_topology(flexar_comm_t c, char* buf, size_t buflen) {
   return j.size() < buflen ? 0 : FLEXAR_ERR_NOMEM;
 }
 
-int flexar_comm_destroy(flexar_comm_t c) {
-  if (!c) return 0;
+}  // extern "C"
+
+namespace flexar {
+
+// Exported buffers a teardown could not agree on (a peer never reached it, or a local destroy): a peer
+// may still map them, so they stay allocated - their virtual addresses are then never handed out again
+// while that mapping lives (a fresh allocation exported at a still-mapped address is what ROCm's dmabuf
+// IPC mishandles, see exportable()). Bounded: beyond kGraveMax entries the oldest is freed.
+static std::mutex g_grave_mu;
+static std::vector<std::pair<int, void*>> g_grave;  // (device, pointer)
+constexpr size_t kGraveMax = 16;
+
+static void grave_keep(int device, void* p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_grave_mu);
+  g_grave.emplace_back(device, p);
+  while (g_grave.size() > kGraveMax) {
+    (void)hipSetDevice(g_grave.front().first);
+    (void)hipFree(g_grave.front().second);
+    g_grave.erase(g_grave.begin());
+  }
+}
+
+// Teardown. Collective (`agree`, the default): after this rank's own work has drained, the ranks agree
+// (host_barrier.hpp) that every rank has finished every call of the communicator, each closes its
+// mappings of the peers' workspaces and registrations, and they agree again that every rank has
+// unmapped before anything is freed - no rank can then allocate, export or map new memory while a peer
+// still holds a mapping of this communicator's. A peer that does not arrive within FLEXAR_TIMEOUT_MS
+// (or a local destroy) leaves this rank's exported buffers parked (grave_keep) instead of freed.
+static int destroy_impl(flexar_comm* c, bool agree) {
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
+  const uint64_t timeout_ms = std::max<uint64_t>(1000, c->timeout_ticks / 100000ull);
+  int rc = 0;
+  bool agreed = false;
+  std::string why;
+  if (c->hb && agree) {
+    int late = -1;
+    agreed = c->hb->arrive_and_wait(timeout_ms, &late);
+    if (!agreed) why = "rank " + std::to_string(late) + " did not reach the teardown within " +
+                       std::to_string(timeout_ms) + " ms";
+  }
   // teardown keeps going past failures; FLEXAR_LOG_LEVEL=info names them
   auto ipc_close = [&](void* p, const char* what, int r) {
     const hipError_t e = hipIpcCloseMemHandle(p);
@@ -554,6 +689,7 @@ int flexar_comm_destroy(flexar_comm_t c) {
     if (c->opened[r]) {
       ipc_close(c->peer_stg[r], "workspace", r);
       ipc_close(c->peer_flags[r], "flags", r);
+      c->opened[r] = false;
     }
   for (auto& kv : c->ipc_maps) ipc_close(kv.second.first, "registration", -1);
   c->ipc_maps.clear();
@@ -578,16 +714,47 @@ int flexar_comm_destroy(flexar_comm_t c) {
   if (c->st_buf) (void)hipFree(c->st_buf);
   if (c->cal_dev) (void)hipFree(c->cal_dev);
   if (c->st_bad) (void)hipHostFree(c->st_bad);
-  (void)hipFree(c->stg);
-  (void)hipFree(c->flags);
+  if (agreed) {
+    int late = -1;
+    agreed = c->hb->arrive_and_wait(timeout_ms, &late);  // every rank has unmapped this rank's buffers
+    if (!agreed) why = "rank " + std::to_string(late) + " did not finish unmapping within " +
+                       std::to_string(timeout_ms) + " ms";
+  }
+  // peers may map stg / flags only once this rank has exported them, and only through a connect that
+  // joined the agreement (hb); without an agreement they stay parked
+  const bool exported = c->nranks > 1 && !c->group_member;
+  if (agreed || !exported) {
+    (void)hipFree(c->stg);
+    (void)hipFree(c->flags);
+  } else {
+    grave_keep(c->device, c->stg);
+    grave_keep(c->device, c->flags);
+    if (agree && c->hb) {
+      set_error("destroy: " + why + "; this rank's workspace stays allocated until the process exits");
+      logf(LOG_WARN, c->rank, "destroy: %s; keeping this rank's exported workspace allocated", why.c_str());
+      rc = FLEXAR_ERR_TIMEOUT;
+    }
+  }
+  if (c->hb) c->hb->unlink();  // every rank joined long before (connect): the name is no longer needed
+  c->hb.reset();
   (void)hipFree(c->epochs);
   (void)hipHostFree(c->err_host);
   delete c;
   // teardown ignores failures (e.g. closing a mapping a peer already released), but HIP keeps the last one
   // as the thread's sticky error, and the caller's framework would report it at its next kernel launch
   (void)hipGetLastError();
-  return 0;
+  return rc;
 }
+
+}  // namespace flexar
+
+extern "C" {
+
+int flexar_comm_destroy(flexar_comm_t c) { return c ? destroy_impl(c, true) : 0; }
+
+// Non-collective teardown (garbage collection, a process that is abandoning its peers): no agreement;
+// this rank's exported buffers stay allocated for the process's lifetime (bounded, see grave_keep).
+int flexar_comm_destroy_local(flexar_comm_t c) { return c ? destroy_impl(c, false) : 0; }
 
 int flexar_comm_rank(flexar_comm_t c) { return c ? c->rank : -1; }
 int flexar_comm_size(flexar_comm_t c) { return c ? c->nranks : -1; }
@@ -654,6 +821,7 @@ int flexar_comm_probe_export(flexar_comm_t c, void* out) {
   b.links = c->links_local > 0 ? c->links_local : 1;
   b.links_fixed = c->links_from_env ? c->model.links : 0;
   b.fingerprint = comm_fingerprint(c);
+  b.resident = c->resident;
   for (int r = 0; r < c->nranks && r < 16; ++r) {
     b.cls[r] = (int8_t)(r == c->rank ? LINK_SAME : c->link_cls[r]);
     b.hops[r] = (int8_t)c->link_hops[r];
@@ -668,14 +836,15 @@ int flexar_comm_probe_agree(flexar_comm_t c, const void* all) {
   if (!c || !all) { set_error("null argument"); return FLEXAR_ERR_INVALID; }
   std::vector<ProbeBlob> v(c->nranks);
   memcpy(v.data(), all, sizeof(ProbeBlob) * c->nranks);
-  int links = 1;
+  int links = 1, resident = 0;
   std::string why;
-  if (!probe_agree(v.data(), c->nranks, &links, &why)) {
+  if (!probe_agree(v.data(), c->nranks, &links, &why, &resident)) {
     set_error(why);
     return FLEXAR_ERR_INVALID;
   }
   std::lock_guard<std::mutex> lk(c->mu);
   if (!c->links_from_env) c->model.links = links;
+  if (resident > 0) c->resident = resident;  // one grid clamp on every rank
   c->links_agreed = true;
   c->memo_gen++;
   return 0;
@@ -752,7 +921,7 @@ int flexar_comm_calibrate(flexar_comm_t c, int mode, char* json, size_t jlen) {
   }
   // the settings fingerprint too (grid cap, block size, chunking, tune table change what a schedule costs)
   char fp[48];
-  snprintf(fp, sizeof(fp), ";settings=%016llx", (unsigned long long)comm_fingerprint(c));
+  snprintf(fp, sizeof(fp), ";settings=%016llx", (unsigned long long)comm_fingerprint(c, false));
   const std::string key = calib_key(arch, c->nranks, c->model.links, link_classes(c), c->disabled, flexar_version()) + fp;
   const std::string dir = calib_dir();
   const std::string path = dir.empty() ? std::string() : calib_path(dir, key);
@@ -821,13 +990,19 @@ int flexar_comm_calibrate(flexar_comm_t c, int mode, char* json, size_t jlen) {
       if (!parse_algo(pts[i].spec, c->nranks, &s, &err) || (c->disabled & proto_family(s))) continue;
       const size_t n = (size_t)(pts[i].bytes / 4);
       const int iters = (int)std::max(5.0, std::min(50.0, 2e8 / pts[i].bytes));
+      // every rank makes every call of the point whatever failed before: the first failure is
+      // kept, later calls still run (or return at once on a recorded timeout); launch counts that still
+      // diverged are repaired by the resync below
       int e = 0;
-      for (int k = 0; k < 2 && !e; ++k)
-        e = flexar_allreduce_ex(c, buf, buf + (size_t)maxb, n, FLEXAR_FLOAT32, FLEXAR_SUM, st, pts[i].spec.c_str(), 1.0f);
-      if (!e) e = hipEventRecord(e0, st) == hipSuccess ? 0 : FLEXAR_ERR_HIP;
-      for (int k = 0; k < iters && !e; ++k)
-        e = flexar_allreduce_ex(c, buf, buf + (size_t)maxb, n, FLEXAR_FLOAT32, FLEXAR_SUM, st, pts[i].spec.c_str(), 1.0f);
-      if (!e) e = hipEventRecord(e1, st) == hipSuccess ? 0 : FLEXAR_ERR_HIP;
+      auto call = [&]() {
+        const int r = flexar_allreduce_ex(c, buf, buf + (size_t)maxb, n, FLEXAR_FLOAT32, FLEXAR_SUM, st,
+                                          pts[i].spec.c_str(), 1.0f);
+        if (r && !e) e = r;
+      };
+      for (int k = 0; k < 2; ++k) call();
+      if (hipEventRecord(e0, st) != hipSuccess && !e) e = FLEXAR_ERR_HIP;
+      for (int k = 0; k < iters; ++k) call();
+      if (hipEventRecord(e1, st) != hipSuccess && !e) e = FLEXAR_ERR_HIP;
       if (!e) e = hipStreamSynchronize(st) == hipSuccess ? 0 : FLEXAR_ERR_HIP;
       float ms = 0;
       if (!e) e = hipEventElapsedTime(&ms, e0, e1) == hipSuccess ? 0 : FLEXAR_ERR_HIP;
@@ -844,6 +1019,26 @@ int flexar_comm_calibrate(flexar_comm_t c, int mode, char* json, size_t jlen) {
     t[pts.size()] = -failed;
     (void)hipStreamSynchronize(st);
     release();
+    // A failed call can leave this rank with fewer launches than its peers (a recorded timeout returns
+    // before launching), so the device agreement below could pair the wrong epochs. The ranks first agree
+    // on the host (host_barrier.hpp); after any failure every rank resets its protocol state and they
+    // meet again before the next device call.
+    if (c->hb) {
+      uint64_t any = 0;
+      int late = -1;
+      const uint64_t tmo = std::max<uint64_t>(1000, saved_timeout / 100000ull);
+      if (!c->hb->exchange_max(failed != 0 ? 1 : 0, &any, tmo, &late)) {
+        set_error("calibration: rank " + std::to_string(late) + " did not reach the failure agreement");
+        return finish(FLEXAR_ERR_TIMEOUT);
+      }
+      if (any) {
+        if ((rc = flexar_comm_resync(c)) != 0) return finish(rc);
+        if (!c->hb->arrive_and_wait(tmo, &late)) {
+          set_error("calibration: rank " + std::to_string(late) + " did not finish the resync");
+          return finish(FLEXAR_ERR_TIMEOUT);
+        }
+      }
+    }
     rc = agree_min(c, t.data(), (int)t.size(), st);
     if (rc) return finish(rc);
     std::vector<CalibRow> rows;

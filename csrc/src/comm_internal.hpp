@@ -24,6 +24,7 @@
 #include <string>
 #include <vector>
 
+#include "host_barrier.hpp"
 #include "launch.hpp"
 #include "flexar/calibration.hpp"
 #include "flexar/cost_model.hpp"
@@ -62,6 +63,7 @@ struct CommHandle {
   char host[64];
   char bus[32];          // PCI bus id of the rank's GPU (hipDeviceGetPCIBusId): resolves the peer device
   uint64_t fingerprint;  // settings every rank must agree on (readiness.hpp env_fingerprint)
+  uint64_t nonce;        // random per communicator: rank 0's names the teardown agreement page
 };
 
 struct DevProgram {
@@ -271,6 +273,11 @@ struct flexar_comm {
   int* st_buf = nullptr;        // self-test buffers (device)
   uint32_t* st_bad = nullptr;   // self-test mismatch counter (host-mapped)
   uint32_t* st_bad_dev = nullptr;
+  std::string selftest_note;    // why a family failed on this rank (HIP errors named), last self-test
+  uint32_t test_hip_fail = 0;   // FLEXAR_TEST_SELFTEST_HIP: families whose self-test launch fails here
+  // collective teardown (host_barrier.hpp): joined at connect, agreed on in flexar_comm_destroy
+  uint64_t nonce = 0;
+  std::unique_ptr<HostBarrier> hb;
 };
 
 namespace flexar {
@@ -313,7 +320,7 @@ int reduce_chain(char* dst, char* dst2, const char* const* srcs, int nsrc, uint6
 int run_dma(flexar_comm* const* cs, int ncomm, const char* const* ins, char* const* outs, uint64_t count, int dtype,
             int op, float fs, hipStream_t st);
 // comm_connect.hip: lifecycle, readiness, calibration
-uint64_t comm_fingerprint(flexar_comm* c);
+uint64_t comm_fingerprint(flexar_comm* c, bool with_calib = true);
 int resident_blocks(int device);
 int check_err(flexar_comm* c);
 int validate_call(flexar_comm* c, int dtype, int op, float scale);

@@ -95,9 +95,9 @@ def test_corrupt_cache_is_a_miss(tmp_path):
     assert nv.calib_load(str(p), key) is None
 
 
-def _blob(rank, links, cls, fp=1234, fixed=0, magic=0xF1E8B10B):
+def _blob(rank, links, cls, fp=1234, fixed=0, magic=0xF1E8B10B, resident=0):
     c = list(cls) + [0] * (16 - len(cls))
-    return struct.pack("<IiiiQ16b16b", magic, rank, links, fixed, fp, *c, *([1] * 16))
+    return struct.pack("<IiiiQ16b16bii", magic, rank, links, fixed, fp, *c, *([1] * 16), resident, 0)
 
 
 def _agree(blobs):
@@ -156,3 +156,31 @@ def test_fit_bounds_the_hbm_term_by_the_peak(n, links):
     assert b["hbm_gbps"] <= 8000.0 * (1 + 1e-9), b
     for k in ("alpha_launch_us", "alpha_sync_us", "link_gbps", "hbm_gbps"):
         assert a[k] == pytest.approx(b[k], rel=1e-3), (k, a, b)
+
+
+def test_probe_agreement_installs_the_minimum_resident_grid():
+    """the executor grid is clamped to the resident workgroups; every rank must clamp alike, so the
+    minimum over the ranks that know their count is agreed on (0 = unknown, ignored)."""
+    n = 3
+    cls = lambda r: [SAME if p == r else XGMI for p in range(n)]  # noqa: E731
+    links, resident = ctypes.c_int(0), ctypes.c_int(-1)
+    blobs = b"".join(_blob(r, 2, cls(r), resident=res) for r, res in enumerate((1024, 768, 0)))
+    assert nv.lib().flexar_probe_agree_resident(blobs, n, ctypes.byref(links), ctypes.byref(resident)) == 0
+    assert (links.value, resident.value) == (2, 768)
+    blobs = b"".join(_blob(r, 2, cls(r)) for r in range(n))
+    assert nv.lib().flexar_probe_agree_resident(blobs, n, ctypes.byref(links), ctypes.byref(resident)) == 0
+    assert resident.value == 0
+
+
+def test_calib_mode_does_not_change_the_cache_key(monkeypatch):
+    """FLEXAR_CALIB=force writes the cache that default runs read; unset and "1" are one mode."""
+    keys = {}
+    for v in (None, "1", "force", "0"):
+        if v is None:
+            monkeypatch.delenv("FLEXAR_CALIB", raising=False)
+        else:
+            monkeypatch.setenv("FLEXAR_CALIB", v)
+        keys[v] = (nv.lib().flexar_settings_fingerprint(0), nv.lib().flexar_settings_fingerprint(1))
+    assert len({k[0] for k in keys.values()}) == 1  # cache-key form: no calibration mode in it
+    assert keys[None][1] == keys["1"][1] != keys["force"][1] != keys["0"][1]  # connect form: normalised mode
+

@@ -252,6 +252,16 @@ def _colls(rank, world, port, q, fallback="gloo"):
         dist.reduce(rd, dst=world - 1)
         k = sum(r + 1 for r in range(world)) if rank == world - 1 else rank + 1
         e11 = (rd - torch.arange(70001, device=dev).float() * k).abs().max().item()
+        # dist.reduce on a tensor the zero-copy probe registered: the root must not pick the
+        # registered-buffer schedule while the other ranks stage (that mismatch hangs until the watchdog)
+        big = torch.full((1 << 19,), float(rank + 1), device=dev)  # 2 MiB: above FLEXAR_PG_ZC_MIN_BYTES
+        for _ in range(3):
+            dist.all_reduce(big)
+            big.fill_(float(rank + 1))
+        registered = dist.group.WORLD.stats.get("zc_registrations", 0)
+        dist.reduce(big, dst=0)
+        k2 = sum(r + 1 for r in range(world)) if rank == 0 else rank + 1
+        e13 = (big - k2).abs().max().item() if registered else 1.0
         torch.cuda.synchronize()
         e10 = 0.0
         if fallback == "nccl":  # point-to-point (pipeline stages) has no flexar program: RCCL by default
@@ -265,7 +275,7 @@ def _colls(rank, world, port, q, fallback="gloo"):
         dist.barrier()
         used = dist.group.WORLD.stats["flexar_allreduce"]
         dist.destroy_process_group()
-        q.put((rank, max(e1, e2, e3, e4, e5, e6, e7, e8, e9, e10, e11, e12), used, None))
+        q.put((rank, max(e1, e2, e3, e4, e5, e6, e7, e8, e9, e10, e11, e12, e13), used, None))
     except Exception:
         import traceback
 

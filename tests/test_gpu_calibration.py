@@ -67,7 +67,10 @@ def _worker(rank, world, port, calib_dir, mode, q):
         else:
             for i, calib in enumerate(("1", "1", "0")):
                 os.environ["FLEXAR_CALIB"] = calib
-                comm = Communicator(workspace_bytes=128 << 20)
+                try:  # no caller barrier between close() and the next communicator: the library agrees on it
+                    comm = Communicator(workspace_bytes=128 << 20)
+                except Exception as e:
+                    raise RuntimeError(f"creating communicator {i} (FLEXAR_CALIB={calib}) failed") from e
                 out[f"cal{i}"] = comm.calibration
                 out[f"hash{i}"] = int(comm._lib.flexar_comm_model_hash(comm._h))
                 out[f"topo{i}"] = comm.topology()
