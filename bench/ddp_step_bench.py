@@ -1,17 +1,22 @@
 #!/usr/bin/env python3
-"""DDP training step with gradients allreduced by flexar: the staging hook vs the zero-copy hook.
+"""DDP training step, gradients allreduced four ways:
 
-    python bench/ddp_step_bench.py                 # 2 processes sharing GPU 0 (rehearsal), gpt-small
-    DDPB_RANKS=4 DDPB_MODEL=gpt-medium python bench/ddp_step_bench.py
+    python bench/ddp_step_bench.py                  # 2 processes sharing GPU 0 (rehearsal), gpt-small
+    DDPB_RANKS=4 DDPB_MODES=pg,hook python bench/ddp_step_bench.py
 
-Each rank trains the same GPT (random init, synthetic tokens) under DistributedDataParallel over a gloo
-process group. The gradient buckets are reduced by `flexar_allreduce_hook`, in two modes:
-- `hook`: the auto-selected schedule through the IPC staging workspace;
-- `zchook`: every bucket is registered on first sight and reduced by "flat+zc+push", with no staging.
+- `pg`:     ``init_process_group("flexar")`` with its defaults: DDP's own reducer calls the flexar c10d
+            backend, whose zero-copy probe agrees (gloo MIN) on registering each new bucket during the first
+            calls and sweeps dead registrations every 16 calls;
+- `pg_nozc`: the same with ``FLEXAR_PG_ZC=0`` (no probe, no sweeps: staging schedules only);
+- `hook`:   a gloo process group plus ``flexar_allreduce_hook`` (FlexarHookState; staging schedules);
+- `nccl`:   RCCL (``init_process_group("nccl")``; the ranks share one GPU, so each gets its own
+            NCCL_HOSTID and RCCL carries the bytes over loopback sockets - the step time is not an xGMI figure).
 
-Both modes run overlapped with backward. One JSON line per mode gives ms per step and tokens/s. On one shared
-GPU the allreduce competes with the other ranks' backward kernels for the same HBM, which is where fewer
-HBM bytes per allreduce show up.
+Each rank trains the same GPT (random init, synthetic tokens, bf16 autocast, fp32 gradients, 25 MB
+buckets). One JSON line per mode: ms per step (max over ranks), tokens/s, and the HOST time per allreduce
+call (perf_counter around the backend's allreduce / the hook; for `nccl` a hook that issues
+``dist.all_reduce(async_op=True)``, i.e. what DDP's reducer does), so per-call host overhead such as the
+zero-copy probe's blocking gloo rounds shows up separately from the device time.
 """
 import json
 import os
@@ -35,6 +40,10 @@ def worker(rank, world, port, mode, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                           FLEXAR_MAX_GRID=str(max(8, 256 // (2 * world))), FLEXAR_TIMEOUT_MS="20000")
+        if mode == "pg_nozc":
+            os.environ["FLEXAR_PG_ZC"] = "0"
+        if mode in ("pg", "pg_nozc", "nccl"):  # RCCL for the backend's fallbacks / the nccl mode
+            os.environ.update(NCCL_HOSTID=f"ddpb-rank{rank}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
         import torch
         import torch.distributed as dist
         from torch.nn.parallel import DistributedDataParallel as DDP
@@ -44,13 +53,50 @@ def worker(rank, world, port, mode, q):
 
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        host = {"calls": 0, "s": 0.0}
+        if mode in ("pg", "pg_nozc"):
+            orig = fb.FlexarProcessGroup.allreduce
+
+            def timed_allreduce(self, *a, **k):
+                t0 = time.perf_counter()
+                try:
+                    return orig(self, *a, **k)
+                finally:
+                    host["calls"] += 1
+                    host["s"] += time.perf_counter() - t0
+
+            fb.FlexarProcessGroup.allreduce = timed_allreduce
+            dist.init_process_group("flexar", rank=rank, world_size=world)
+        elif mode == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
         cfg = PRESETS[os.environ.get("DDPB_MODEL", "gpt-small")]
         torch.manual_seed(0)
         model = GPT(cfg).to(dev)
         ddp = DDP(model, device_ids=[0], bucket_cap_mb=float(os.environ.get("DDPB_BUCKET_MB", "25")))
-        state = fb.FlexarHookState(zero_copy=mode == "zchook")
-        ddp.register_comm_hook(state, fb.flexar_allreduce_hook)
+        state = None
+        if mode == "hook":
+            state = fb.FlexarHookState()
+
+            def hook(st, bucket):
+                t0 = time.perf_counter()
+                fut = fb.flexar_allreduce_hook(st, bucket)
+                host["calls"] += 1
+                host["s"] += time.perf_counter() - t0
+                return fut
+
+            ddp.register_comm_hook(state, hook)
+        elif mode == "nccl":
+            def nccl_hook(_, bucket):
+                t0 = time.perf_counter()
+                buf = bucket.buffer().div_(world)
+                fut = dist.all_reduce(buf, async_op=True).get_future().then(lambda f: f.value()[0])
+                host["calls"] += 1
+                host["s"] += time.perf_counter() - t0
+                return fut
+
+            ddp.register_comm_hook(None, nccl_hook)
         opt = torch.optim.AdamW(ddp.parameters(), lr=3e-4)
         gen = torch.Generator().manual_seed(1000 + rank)
         batch = int(os.environ.get("DDPB_BATCH", "4"))
@@ -69,21 +115,25 @@ def worker(rank, world, port, mode, q):
             step()
         torch.cuda.synchronize()
         dist.barrier()
+        host.update(calls=0, s=0.0)
         steps = int(os.environ.get("DDPB_STEPS", "10"))
         t0 = time.perf_counter()
         for _ in range(steps):
             loss = step()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        t = torch.tensor([dt])
+        t = torch.tensor([dt, host["s"] / max(1, host["calls"])], device=dev if mode == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        dt, host_call = float(t[0]), float(t[1])
         params = sum(p.numel() for p in model.parameters())
         res = {"mode": mode, "model": os.environ.get("DDPB_MODEL", "gpt-small"), "params": params, "ranks": world,
                "ms_per_step": round(dt / steps * 1e3, 2), "tokens_per_s": round(steps * batch * cfg.seq * world / dt, 1),
-               "loss": round(float(loss.item()), 4), "hook_calls": state.calls,
-               "zero_copy_buckets": len(state._bucket_regs),
-               "registrations": state.registrations}
+               "allreduce_calls_per_step": round(host["calls"] / steps, 2),
+               "host_us_per_allreduce": round(host_call * 1e6, 1), "loss": round(float(loss.item()), 4)}
+        if mode in ("pg", "pg_nozc"):
+            pg = dist.group.WORLD
+            res["zc_registrations"] = pg.stats.get("zc_registrations", 0)
+            res["fallback_calls"] = pg.stats.get("fallback", 0)
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, res, None))
@@ -98,7 +148,7 @@ def main():
 
     world = int(os.environ.get("DDPB_RANKS", "2"))
     ctx = mp.get_context("spawn")
-    for mode in ("hook", "zchook"):
+    for mode in os.environ.get("DDPB_MODES", "pg,pg_nozc,hook,nccl").split(","):
         q = ctx.Queue()
         port = _port()
         ps = [ctx.Process(target=worker, args=(r, world, port, mode, q)) for r in range(world)]
@@ -110,7 +160,7 @@ def main():
         for rank, r, tb in res:
             if tb:
                 raise SystemExit(f"rank {rank} failed:\n{tb}")
-        print(json.dumps(sorted(res)[0][1]), flush=True)
+        print(json.dumps(sorted(res, key=lambda x: x[0])[0][1]), flush=True)
 
 
 if __name__ == "__main__":

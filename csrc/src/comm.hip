@@ -167,6 +167,9 @@ int get_program(flexar_comm* c, const AlgoSpec& s, uint64_t count, uint32_t esiz
     return FLEXAR_ERR_INVALID;
   }
   mark_barriers(dp->prog, c->rank);
+  dp->max_nsrc = 1;
+  for (const Op& o : dp->prog.ops)
+    if (o.kind == OP_XFER) dp->max_nsrc = std::max<uint32_t>(dp->max_nsrc, o.nsrc);
   logf(LOG_INFO, c->rank, "plan %s: count=%llu esize=%u ops=%zu channels=%u staging=%llu B", s.str().c_str(),
        (unsigned long long)count, esize, dp->prog.ops.size(), dp->prog.nchan,
        (unsigned long long)dp->prog.stg_bytes());
@@ -215,7 +218,7 @@ int zc_bind(flexar_comm* c, const Program& P, const void* in, uint64_t in_bytes,
     }
     const uint64_t d = (uint64_t)(q - g->base);
     for (int p = 0; p < c->nranks; ++p) x->peer_io[b][p] = p == c->rank ? (char*)q : g->peer[p] + d;
-    if (!g->aligned || (d & 15)) x->vec_ok = 0;
+    if (!vec_any_alignment() && (!g->aligned || (d & 15))) x->vec_ok = 0;
   }
   return 0;
 }
@@ -261,7 +264,7 @@ void fill_ctx(flexar_comm* c, DevProgram* dp, const void* in, void* out, DevCtx*
   x->stg_half_bytes = c->half_bytes;
   x->err = c->err_dev;
   x->timeout_ticks = c->timeout_ticks;
-  x->vec_ok = ((((uintptr_t)in) | ((uintptr_t)out)) & 15) == 0;
+  x->vec_ok = vec_ok_for(((uintptr_t)in) | ((uintptr_t)out));
   x->fi_kind = c->fi_kind;
   x->fi_slot = c->fi_slot;
   x->fi_ticks = c->fi_ticks;
@@ -344,6 +347,7 @@ int run_rs_ag(flexar_comm* c, Coll coll, const void* in, void* out, size_t count
     la.grid = choose_grid(c, n * es * c->nranks, dp->prog.nchan);
     la.stream = st;
     la.proto = proto_of(s);
+    la.kmax = kmax_of(dp);
     // all-gather moves bytes only: run the SUM instantiation (the op is never applied, K == 1)
     if ((rc = launch_dtype(dtype, coll == Coll::ALL_GATHER ? FLEXAR_SUM : op, la))) return rc;
     c->launches++;
@@ -401,6 +405,7 @@ int run_bcast(flexar_comm* c, const void* in, void* out, size_t count, int dtype
     la.grid = choose_grid(c, n * es, dp->prog.nchan);
     la.stream = st;
     la.proto = proto_of(s);
+    la.kmax = kmax_of(dp);
     if ((rc = launch_dtype(dtype, FLEXAR_SUM, la))) return rc;
     c->launches++;
   }
@@ -583,6 +588,7 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     la.grid = hit ? m.grid : choose_grid(c, count * es, dp->prog.nchan);
     la.stream = st;
     la.proto = proto_of(s);
+    la.kmax = kmax_of(dp);
     la.wire = dp->prog.wire;
     std::unique_ptr<DeviceTimer> tm(c->profile ? new DeviceTimer : nullptr);
     if (tm) tm->start(st);
@@ -621,6 +627,7 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     la.grid = grid;
     la.stream = st;
     la.proto = proto_of(s);
+    la.kmax = kmax_of(dp);
     la.wire = dp->prog.wire;
     rc = launch_dtype(dtype, op, la);
     if (rc) break;
@@ -726,6 +733,7 @@ int flexar_allreduce_fp8(flexar_comm_t c, const void* in, void* out, size_t coun
     la.grid = choose_grid(c, n * es, dp->prog.nchan);
     la.stream = st;
     la.proto = proto_of(s);
+    la.kmax = kmax_of(dp);
     la.wire = dp->prog.wire;
     if ((rc = launch_dtype(dtype, op, la))) return rc;
     c->launches++;

@@ -28,7 +28,7 @@ int reduce_chain(char* dst, char* dst2, const char* const* srcs, int nsrc, uint6
     la.dst2 = last ? dst2 : nullptr;
     la.n = count;
     la.scale = last ? fs : 1.0f;
-    la.vec = (al & 15) == 0 ? 1 : 0;
+    la.vec = vec_ok_for(al) ? 1 : 0;
     la.grid = grid;
     la.stream = st;
     la.proto = proto;

@@ -70,6 +70,7 @@ struct DevProgram {
   Program prog;
   Op* d_ops = nullptr;
   uint32_t* d_chan = nullptr;
+  uint32_t max_nsrc = kMaxSrc;  // widest XFER fan-in: <= 2 launches the KMAX = 2 executor (device_exec.hpp)
 };
 
 static const uint32_t kGroupMaxBlocks = 256;
@@ -148,6 +149,22 @@ inline uint64_t env_u64(const char* name, uint64_t dflt) {
   const char* e = getenv(name);
   if (!e || !*e) return dflt;
   return strtoull(e, nullptr, 0);
+}
+
+// Caller buffers at any byte offset take the 16-B vector path (device_exec.hpp ld16/st16: unaligned
+// dwordx4 accesses); FLEXAR_SCALAR_MISALIGNED=1 restores the round-3 policy (a base that is not 16-B
+// aligned runs the whole span through 4-byte scalar code) for A/B measurements.
+inline bool vec_any_alignment() {
+  static const bool v = env_u64("FLEXAR_SCALAR_MISALIGNED", 0) == 0;
+  return v;
+}
+inline bool vec_ok_for(uintptr_t addr_bits) { return vec_any_alignment() || (addr_bits & 15) == 0; }
+
+// Executor instantiation for a program: KMAX = 2 when no XFER reads more than two sources (rings, RHD,
+// binary trees, copies); FLEXAR_KMAX_SPECIALIZE=0 always runs the general kernel (A/B measurements).
+inline int kmax_of(const DevProgram* dp) {
+  static const bool on = env_u64("FLEXAR_KMAX_SPECIALIZE", 1) != 0;
+  return on && dp && dp->max_nsrc <= 2 ? 2 : (int)kMaxSrc;
 }
 
 }  // namespace flexar

@@ -95,7 +95,7 @@ int run_msg(flexar_comm* c, const AlgoSpec& s, Coll coll, const void* in, void* 
       x.stg_half_bytes = 0;
       x.err = c->err_dev;
       x.timeout_ticks = c->timeout_ticks;
-      x.vec_ok = ((((uintptr_t)in) | ((uintptr_t)out)) & 15) == 0;
+      x.vec_ok = vec_ok_for(((uintptr_t)in) | ((uintptr_t)out));
       x.stg_unit = es;
       uint64_t span = 0;
       for (const Op& o : stp.prog.ops) span = std::max<uint64_t>(span, o.len);

@@ -4,7 +4,7 @@
 // anything else), so a page of per-rank monotonic counters is an agreement that needs neither the
 // device protocol nor the caller's bootstrap (torch.distributed, MPI, a Store). It keeps working after
 // the peers' IPC mappings are closed, which is exactly what the collective teardown needs
-// (flexar_comm_destroy: quiesce -> agree -> unmap -> agree -> free; docs/DESIGN.md §20).
+// (flexar_comm_destroy: quiesce -> agree -> unmap -> agree -> free; docs/DESIGN.md §21).
 //
 // Reference counterpart: the reference never frees its scratch (allreduce_over_mpi/mpi_mod.hpp:931-950,
 // grow-only and never deleted while in use), so it has no teardown to agree on. Here workspaces are

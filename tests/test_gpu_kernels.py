@@ -516,3 +516,40 @@ def test_group_fp8_wire_large_slices(cuda, groups, dtype):
         mism = (~torch.isclose(outs[0].float(), want.float(), rtol=1e-5, atol=0)).float().mean().item()
         assert mism < 2e-3, mism
     grp.check()
+
+
+@pytest.mark.parametrize("dtype,offsets", [(torch.float32, ((1, 1), (1, 2), (3, 0), (2, 2))),
+                                           (torch.bfloat16, ((1, 1), (1, 3), (0, 5)))])
+def test_group_misaligned_views(cuda, groups, dtype, offsets):
+    """Tensor views at element offsets (+4 / +8 / +12 B fp32, +2 / +6 / +10 B bf16; input and output
+    misaligned alike or differently) take the 16-B vector path with unaligned accesses
+    and stay bit-exact against the fp32 torch sum (small integers: every sum is exact in the dtype)."""
+    n = 4
+    grp = groups[n]
+    specs = ["flat", "flat+push", "ring", "ring:3", "rhd", "tree:2,2+pull", "oneshot", "ll", "flat+wt", "dma"]
+    if dtype == torch.bfloat16:
+        specs += ["ring+f32", "rhd+f32"]
+    for size in (1000, 65539, (1 << 20) + 5):
+        for oi, oo in offsets:
+            bufs = [torch.zeros(size + 16, device=cuda, dtype=dtype) for _ in range(n)]
+            obufs = [torch.zeros(size + 16, device=cuda, dtype=dtype) for _ in range(n)]
+            base = torch.arange(size, device=cuda, dtype=torch.int32) % 61
+            ref = (base * n + n * (n - 1) // 2).to(torch.float32)
+            for spec in specs:
+                if spec == "ll" and size > 70000:
+                    continue
+                ins = [b[oi:oi + size] for b in bufs]
+                outs = [b[oo:oo + size] for b in obufs]
+                for r, x in enumerate(ins):
+                    x.copy_((base + r).to(dtype))
+                assert (ins[0].data_ptr() % 16 != 0) or (outs[0].data_ptr() % 16 != 0) or oi == oo == 0
+                for _ in range(2):  # both staging parities
+                    res = grp.all_reduce(ins, "sum", outs=outs, algo=spec)
+                    torch.cuda.synchronize()
+                    for r, o in enumerate(res):
+                        assert torch.equal(o.float(), ref), (spec, size, oi, oo, r,
+                                                             (o.float() - ref).abs().max().item())
+                # the bytes around the views are untouched
+                for b in obufs:
+                    assert not b[:oo].any() and not b[oo + size:].any(), (spec, size, oi, oo)
+    grp.check()

@@ -3,7 +3,7 @@ shared-memory page for several phases, in any arrival order; a rank that never a
 return FLEXAR_ERR_TIMEOUT naming it instead of hanging; the page's name is removed.
 
 The reference never frees its scratch (allreduce_over_mpi/mpi_mod.hpp:931-950), so it has no teardown to
-agree on; flexar_comm_destroy runs these barriers between drain, unmap and free (docs/DESIGN.md §20)."""
+agree on; flexar_comm_destroy runs these barriers between drain, unmap and free (docs/DESIGN.md §21)."""
 import multiprocessing as mp
 import os
 import time
