@@ -329,6 +329,14 @@ class Communicator:
         self._lib.flexar_comm_selftest_note(self._h, b, 1024)
         return b.value.decode(errors="replace")
 
+    def host_agree_max(self, value: int) -> int:
+        """Collective: the maximum of ``value`` (0 .. 2**64 - 1) over the ranks, through the communicator's
+        host shared-memory page - no device call, no bootstrap round trip. Raises
+        FlexarError when the communicator has no page (single rank, in-process group)."""
+        out = ctypes.c_uint64(0)
+        nv.check(self._lib.flexar_comm_host_agree(self._h, int(value), ctypes.byref(out)), "host_agree")
+        return int(out.value)
+
     def topology(self) -> dict:
         """Connect-time probe: per-peer PCI bus id, device, link class and hop count; self-test state."""
         import json

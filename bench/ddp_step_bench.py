@@ -8,7 +8,8 @@
             backend, whose zero-copy probe agrees (gloo MIN) on registering each new bucket during the first
             calls and sweeps dead registrations every 16 calls;
 - `pg_nozc`: the same with ``FLEXAR_PG_ZC=0`` (no probe, no sweeps: staging schedules only);
-- `hook`:   a gloo process group plus ``flexar_allreduce_hook`` (FlexarHookState; staging schedules);
+- `hook`:   a gloo process group plus ``flexar_allreduce_hook`` (FlexarHookState defaults: every bucket
+            registered, "flat+zc+push");
 - `nccl`:   RCCL (``init_process_group("nccl")``; the ranks share one GPU, so each gets its own
             NCCL_HOSTID and RCCL carries the bytes over loopback sockets - the step time is not an xGMI figure).
 
