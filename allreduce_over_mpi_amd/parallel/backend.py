@@ -94,8 +94,10 @@ class FlexarProcessGroup(dist.ProcessGroup):
         self.hierarchical = False
         self._grid = int(os.environ.get("FLEXAR_PG_GRID", "0") or 0)  # executor workgroups (0 = auto)
         # zero copy for persistent buffers (DDP gradient buckets), on by default (FLEXAR_PG_ZC=0 turns it
-        # off): during the first FLEXAR_PG_ZC_PROBES allreduces every rank agrees (one host MIN over gloo)
-        # whether its tensor is new and >= 1 MiB, and such tensors are registered collectively; later calls
+        # off): during the first FLEXAR_PG_ZC_PROBES allreduces every rank agrees (one max over the
+        # communicator's host shared-memory page, else a gloo MIN) whether its tensor is new and >= 1 MiB,
+        # and such tensors are registered collectively; FLEXAR_PG_ZC_IDLE_STOP (8) agreements in a row with
+        # nothing to register close the window early; later calls
         # on them then switch to "+zc+push" by themselves (comm.hip, FLEXAR_ZC_AUTO). A registration keeps
         # its tensor (so its memory cannot be reused under the peers' mappings); every FLEXAR_PG_ZC_SWEEP (16)
         # allreduces the ranks agree which registered tensors nothing but the registration refers to any more
@@ -105,6 +107,9 @@ class FlexarProcessGroup(dist.ProcessGroup):
         self._zc_on = os.environ.get("FLEXAR_PG_ZC", "1") == "1"
         self._host_agree = None  # host-page agreements available (None = not tried yet)
         self._zc_probes_left = int(os.environ.get("FLEXAR_PG_ZC_PROBES", "64") or 0)
+        # consecutive agreements without a registration that close the probe window early (the sweep re-opens it)
+        self._zc_idle_stop = max(1, int(os.environ.get("FLEXAR_PG_ZC_IDLE_STOP", "8") or 8))
+        self._zc_idle = 0
         self._zc_seen = set()  # (data_ptr, nbytes) registered by this process group
         self._zc_regs = []     # [(data_ptr, nbytes), registration id, tensor] in registration order
         self._zc_min = int(os.environ.get("FLEXAR_PG_ZC_MIN_BYTES", str(1 << 20)))
@@ -234,7 +239,14 @@ class FlexarProcessGroup(dist.ProcessGroup):
         want = (len(tensor_list) == 1 and key[1] >= self._zc_min and key[0] % 16 == 0 and key not in self._zc_seen
                 and len(self._zc_seen) < 64)
         if not self._agree_all([want], comm)[0]:
+            # a steady state (every rank's tensors already registered or not eligible) ends the window early:
+            # each agreement is a host barrier on the allreduce's issue path, so the skew between ranks
+            # would block the autograd thread on every call (profiles/r4_ddp)
+            self._zc_idle += 1
+            if self._zc_idle >= self._zc_idle_stop:
+                self._zc_probes_left = 0
             return
+        self._zc_idle = 0
         try:
             rid = comm.register(t)  # collective; the allocation is mapped by the peers
             self._zc_seen.add(key)
@@ -278,6 +290,7 @@ class FlexarProcessGroup(dist.ProcessGroup):
         if freed:
             self.stats["zc_deregistrations"] = self.stats.get("zc_deregistrations", 0) + freed
             self._zc_probes_left = max(self._zc_probes_left, 16)  # their replacements get registered
+            self._zc_idle = 0
 
     def zc_registered_bytes(self) -> int:
         """Bytes currently held by zero-copy registrations of this process group."""

@@ -119,8 +119,13 @@ def worker(rank, world, port, mode, q):
         host.update(calls=0, s=0.0)
         steps = int(os.environ.get("DDPB_STEPS", "10"))
         t0 = time.perf_counter()
+        per_step = []
         for _ in range(steps):
+            ts = time.perf_counter()
             loss = step()
+            if os.environ.get("DDPB_STEP_SYNC") == "1":  # per-step times (diagnostics; serialises steps)
+                torch.cuda.synchronize()
+            per_step.append(round((time.perf_counter() - ts) * 1e3, 2))
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         t = torch.tensor([dt, host["s"] / max(1, host["calls"])], device=dev if mode == "nccl" else "cpu")
@@ -131,6 +136,11 @@ def worker(rank, world, port, mode, q):
                "ms_per_step": round(dt / steps * 1e3, 2), "tokens_per_s": round(steps * batch * cfg.seq * world / dt, 1),
                "allreduce_calls_per_step": round(host["calls"] / steps, 2),
                "host_us_per_allreduce": round(host_call * 1e6, 1), "loss": round(float(loss.item()), 4)}
+        if os.environ.get("DDPB_STEP_SYNC") == "1":
+            res["step_ms"] = per_step
+        if state is not None:
+            res["registrations"] = state.registrations
+            res["deregistrations"] = state.deregistrations
         if mode in ("pg", "pg_nozc"):
             pg = dist.group.WORLD
             res["zc_registrations"] = pg.stats.get("zc_registrations", 0)

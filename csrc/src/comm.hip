@@ -167,9 +167,6 @@ int get_program(flexar_comm* c, const AlgoSpec& s, uint64_t count, uint32_t esiz
     return FLEXAR_ERR_INVALID;
   }
   mark_barriers(dp->prog, c->rank);
-  dp->max_nsrc = 1;
-  for (const Op& o : dp->prog.ops)
-    if (o.kind == OP_XFER) dp->max_nsrc = std::max<uint32_t>(dp->max_nsrc, o.nsrc);
   logf(LOG_INFO, c->rank, "plan %s: count=%llu esize=%u ops=%zu channels=%u staging=%llu B", s.str().c_str(),
        (unsigned long long)count, esize, dp->prog.ops.size(), dp->prog.nchan,
        (unsigned long long)dp->prog.stg_bytes());
@@ -347,7 +344,6 @@ int run_rs_ag(flexar_comm* c, Coll coll, const void* in, void* out, size_t count
     la.grid = choose_grid(c, n * es * c->nranks, dp->prog.nchan);
     la.stream = st;
     la.proto = proto_of(s);
-    la.kmax = kmax_of(dp);
     // all-gather moves bytes only: run the SUM instantiation (the op is never applied, K == 1)
     if ((rc = launch_dtype(dtype, coll == Coll::ALL_GATHER ? FLEXAR_SUM : op, la))) return rc;
     c->launches++;
@@ -405,7 +401,6 @@ int run_bcast(flexar_comm* c, const void* in, void* out, size_t count, int dtype
     la.grid = choose_grid(c, n * es, dp->prog.nchan);
     la.stream = st;
     la.proto = proto_of(s);
-    la.kmax = kmax_of(dp);
     if ((rc = launch_dtype(dtype, FLEXAR_SUM, la))) return rc;
     c->launches++;
   }
@@ -588,7 +583,6 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     la.grid = hit ? m.grid : choose_grid(c, count * es, dp->prog.nchan);
     la.stream = st;
     la.proto = proto_of(s);
-    la.kmax = kmax_of(dp);
     la.wire = dp->prog.wire;
     std::unique_ptr<DeviceTimer> tm(c->profile ? new DeviceTimer : nullptr);
     if (tm) tm->start(st);
@@ -627,7 +621,6 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     la.grid = grid;
     la.stream = st;
     la.proto = proto_of(s);
-    la.kmax = kmax_of(dp);
     la.wire = dp->prog.wire;
     rc = launch_dtype(dtype, op, la);
     if (rc) break;
@@ -733,7 +726,6 @@ int flexar_allreduce_fp8(flexar_comm_t c, const void* in, void* out, size_t coun
     la.grid = choose_grid(c, n * es, dp->prog.nchan);
     la.stream = st;
     la.proto = proto_of(s);
-    la.kmax = kmax_of(dp);
     la.wire = dp->prog.wire;
     if ((rc = launch_dtype(dtype, op, la))) return rc;
     c->launches++;

@@ -128,7 +128,7 @@ static int group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
   for (uint64_t off = 0; off < count; off += piece) {
     uint64_t n = std::min<uint64_t>(piece, count - off);
     std::vector<DevCtx> h(nranks);
-    int grid = 0, wire = 0, kmax = 1;
+    int grid = 0, wire = 0;
     bool zc = false;
     for (int r = 0; r < nranks; ++r) {
       DevProgram* dp = nullptr;
@@ -139,7 +139,6 @@ static int group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
       zc = zc || dp->prog.zc;
       if (amax_parts) h[r].amax_parts = amax_parts[r];
       wire = dp->prog.wire;
-      kmax = std::max(kmax, kmax_of(dp));
       int g = choose_grid(comms[r], n * es, dp->prog.nchan);
       grid = r == 0 ? g : grid;
       if (g != grid) { set_error("group ranks disagree on grid"); return FLEXAR_ERR_STATE; }
@@ -158,7 +157,6 @@ static int group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
     la.stream = st;
     la.proto = proto_of(specs[0]);
     la.wire = wire;
-    la.kmax = kmax;
     int rc = launch_dtype(dtype, op, la);
     if (!rc) (void)group_ctx_launched(st);
     if (rc) return rc;
@@ -198,7 +196,7 @@ int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const vo
   float fs = coll == 1 && op == FLEXAR_AVG ? 1.0f / (float)nranks : 1.0f;
   DevCtx* d_ctx = nullptr;
   std::vector<DevCtx> h(nranks);
-  int grid = 0, kmax = 1;
+  int grid = 0;
   int proto = PM_FENCE;
   bool zc = false;
   for (int r = 0; r < nranks; ++r) {
@@ -212,7 +210,6 @@ int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const vo
     if (dp->prog.stg_bytes() > comms[r]->exec_half) { set_error("group collective exceeds workspace"); return FLEXAR_ERR_NOMEM; }
     fill_ctx(comms[r], dp, ins[r], outs[r], &h[r]);
     zc = zc || dp->prog.zc;
-    kmax = std::max(kmax, kmax_of(dp));
     int g = choose_grid(comms[r], count * es * nranks, dp->prog.nchan);
     grid = r == 0 ? g : grid;
   }
@@ -225,7 +222,6 @@ int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const vo
   la.grid = grid;
   la.stream = st;
   la.proto = proto;
-  la.kmax = kmax;
   int rc = launch_dtype(dtype, op, la);
   if (!rc) (void)group_ctx_launched(st);
   if (rc) return rc;
@@ -247,7 +243,7 @@ int flexar_group_broadcast(flexar_comm_t* comms, int nranks, int root, const voi
   const uint32_t es = (uint32_t)dtype_size(dtype);
   DevCtx* d_ctx = nullptr;
   std::vector<DevCtx> h(nranks);
-  int grid = 0, proto = PM_FENCE, kmax = 1;
+  int grid = 0, proto = PM_FENCE;
   bool zc = false;
   for (int r = 0; r < nranks; ++r) {
     AlgoSpec s;
@@ -260,7 +256,6 @@ int flexar_group_broadcast(flexar_comm_t* comms, int nranks, int root, const voi
     const void* in = ins && ins[r] ? ins[r] : outs[r];
     fill_ctx(comms[r], dp, in, outs[r], &h[r]);
     zc = zc || dp->prog.zc;
-    kmax = std::max(kmax, kmax_of(dp));
     int g = choose_grid(comms[r], count * es, dp->prog.nchan);
     grid = r == 0 ? g : grid;
   }
@@ -273,7 +268,6 @@ int flexar_group_broadcast(flexar_comm_t* comms, int nranks, int root, const voi
   la.grid = grid;
   la.stream = st;
   la.proto = proto;
-  la.kmax = kmax;
   int rc = launch_dtype(dtype, FLEXAR_SUM, la);
   if (!rc) (void)group_ctx_launched(st);
   if (rc) return rc;

@@ -70,7 +70,6 @@ struct DevProgram {
   Program prog;
   Op* d_ops = nullptr;
   uint32_t* d_chan = nullptr;
-  uint32_t max_nsrc = kMaxSrc;  // widest XFER fan-in: <= 2 launches the KMAX = 2 executor (device_exec.hpp)
 };
 
 static const uint32_t kGroupMaxBlocks = 256;
@@ -159,13 +158,6 @@ inline bool vec_any_alignment() {
   return v;
 }
 inline bool vec_ok_for(uintptr_t addr_bits) { return vec_any_alignment() || (addr_bits & 15) == 0; }
-
-// Executor instantiation for a program: KMAX = 2 when no XFER reads more than two sources (rings, RHD,
-// binary trees, copies); FLEXAR_KMAX_SPECIALIZE=0 always runs the general kernel (A/B measurements).
-inline int kmax_of(const DevProgram* dp) {
-  static const bool on = env_u64("FLEXAR_KMAX_SPECIALIZE", 1) != 0;
-  return on && dp && dp->max_nsrc <= 2 ? 2 : (int)kMaxSrc;
-}
 
 }  // namespace flexar
 

@@ -310,33 +310,19 @@ __device__ FX_INLINE void xfer_k(const char* const (&s)[kMaxSrc], char* const (&
   }
 }
 
-// KMAX: the largest fan-in this kernel instantiation runs. One kernel holds every fan-in case of its
-// switch, and the widest case sets the VGPR budget of all of them: the fan-in-8 step keeps the executor
-// at 138-207 VGPRs (2-3 waves per SIMD, ONE 512-thread workgroup per CU). Programs whose XFERs read at
-// most two sources (rings, RHD, binary trees, copies) launch the KMAX = 2 instantiation instead, whose
-// smaller footprint lets two workgroups share a CU (twice the loads in flight per CU for these
-// latency-bound streams). The host picks it from the program (DevProgram::max_nsrc); a wider XFER in a
-// KMAX = 2 kernel is reported as a planner/executor mismatch, never computed.
-template <typename T, typename OP, int PM, int KMAX = 8>
+template <typename T, typename OP, int PM>
 __device__ FX_INLINE void xfer_dispatch(int K, const char* const (&s)[kMaxSrc], char* const (&d)[kMaxDst], int nd,
                                         uint64_t n, float scale, bool vec) {
   switch (K) {
     case 1: xfer_k<T, OP, 1, PM>(s, d, nd, n, scale, vec); break;
-    case 2: if constexpr (KMAX >= 2) xfer_k<T, OP, 2, PM>(s, d, nd, n, scale, vec); break;
-    case 3: if constexpr (KMAX >= 3) xfer_k<T, OP, 3, PM>(s, d, nd, n, scale, vec); break;
-    case 4: if constexpr (KMAX >= 4) xfer_k<T, OP, 4, PM>(s, d, nd, n, scale, vec); break;
-    case 5: if constexpr (KMAX >= 5) xfer_k<T, OP, 5, PM>(s, d, nd, n, scale, vec); break;
-    case 6: if constexpr (KMAX >= 6) xfer_k<T, OP, 6, PM>(s, d, nd, n, scale, vec); break;
-    case 7: if constexpr (KMAX >= 7) xfer_k<T, OP, 7, PM>(s, d, nd, n, scale, vec); break;
-    default: if constexpr (KMAX >= 8) xfer_k<T, OP, 8, PM>(s, d, nd, n, scale, vec); break;
+    case 2: xfer_k<T, OP, 2, PM>(s, d, nd, n, scale, vec); break;
+    case 3: xfer_k<T, OP, 3, PM>(s, d, nd, n, scale, vec); break;
+    case 4: xfer_k<T, OP, 4, PM>(s, d, nd, n, scale, vec); break;
+    case 5: xfer_k<T, OP, 5, PM>(s, d, nd, n, scale, vec); break;
+    case 6: xfer_k<T, OP, 6, PM>(s, d, nd, n, scale, vec); break;
+    case 7: xfer_k<T, OP, 7, PM>(s, d, nd, n, scale, vec); break;
+    default: xfer_k<T, OP, 8, PM>(s, d, nd, n, scale, vec); break;
   }
-}
-
-// An XFER wider than the instantiation's KMAX (host/kernel mismatch): flag it (same code as an
-// unsupported typed pattern, check_err names it) instead of skipping the transfer silently.
-__device__ FX_INLINE void report_unrunnable(uint32_t* err) {
-  if (threadIdx.x == 0)
-    __hip_atomic_store(err, (uint32_t)(0x40000000u | (0xfdu << 8)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __device__ FX_INLINE uint64_t ld_flag(uint64_t* f) {
@@ -352,14 +338,13 @@ __device__ FX_INLINE char* io_base(const DevCtx& c, const Loc& l) {
   return l.rank == c.rank ? c.local[l.buf] : c.peer_io[l.buf][l.rank];
 }
 
-template <typename T, typename OP, int PM, int KMAX = 8>
+template <typename T, typename OP, int PM>
 __device__ FX_INLINE void xfer_op(const DevCtx& c, const Op* o, uint32_t lb, uint32_t nb, uint32_t quantum,
                                   uint64_t par) {
   uint64_t lo, hi;
   slice_range(o->len, lb, nb, quantum, &lo, &hi);
   if (hi <= lo) return;
   const int ns = o->nsrc, nd = o->ndst;
-  if (ns > KMAX) return report_unrunnable(c.err);
   const char* s[kMaxSrc];
   char* d[kMaxDst];
   bool vec = true;
@@ -392,10 +377,10 @@ __device__ FX_INLINE void xfer_op(const DevCtx& c, const Op* o, uint32_t lb, uin
       for (int k = 0; k < kMaxSrc; ++k) s2[k] = k < ns ? s[k] + p * sizeof(T) : nullptr;
 #pragma unroll
       for (int k = 0; k < kMaxDst; ++k) d2[k] = k < nd ? d[k] + p * sizeof(T) : nullptr;
-      xfer_dispatch<T, OP, PM, KMAX>(ns, s2, d2, nd, (hi - lo - p) < step ? (hi - lo - p) : step, o->scale, vec);
+      xfer_dispatch<T, OP, PM>(ns, s2, d2, nd, (hi - lo - p) < step ? (hi - lo - p) : step, o->scale, vec);
     }
   } else {
-    xfer_dispatch<T, OP, PM, KMAX>(ns, s, d, nd, hi - lo, o->scale, vec);
+    xfer_dispatch<T, OP, PM>(ns, s, d, nd, hi - lo, o->scale, vec);
   }
 }
 
@@ -709,7 +694,7 @@ __device__ FX_INLINE bool xfer_mx_k(int sp, const char* const (&s)[kMaxSrc], cha
 
 // Typed op: operand addresses (STG offsets in units, element slice [lo, hi) in each operand's own
 // type), then the all-dtype / all-wire fast paths or the mixed one.
-template <typename T, typename W, int PM, int KMAX = 8>
+template <typename T, typename W, int PM>
 __device__ FX_INLINE void xfer_op_typed(const DevCtx& c, const Op* o, uint32_t lb, uint32_t nb, uint32_t quantum,
                                         uint64_t par, float pre, float post_inv) {
   uint64_t lo, hi;
@@ -717,7 +702,6 @@ __device__ FX_INLINE void xfer_op_typed(const DevCtx& c, const Op* o, uint32_t l
   if (hi <= lo) return;
   constexpr bool FP8 = sizeof(W) == 1;
   const int ns = o->nsrc, nd = o->ndst;
-  if (ns > KMAX) return report_unrunnable(c.err);
   const uint32_t sm = o->pad16[0], dm = o->pad16[1];
   const char* s[kMaxSrc];
   char* d[kMaxDst];
@@ -747,11 +731,11 @@ __device__ FX_INLINE void xfer_op_typed(const DevCtx& c, const Op* o, uint32_t l
   const uint64_t n = hi - lo;
   const uint32_t all_s = (1u << ns) - 1, all_d = (1u << nd) - 1;
   if (sm == all_s && dm == all_d) {  // wire type throughout (fp32 partial -> fp32 partial, fp8 copy)
-    xfer_dispatch<W, OpSum, PM, KMAX>(ns, s, d, nd, n, o->scale, vec);
+    xfer_dispatch<W, OpSum, PM>(ns, s, d, nd, n, o->scale, vec);
     return;
   }
   if (!FP8 && sm == 0 && dm == 0) {  // dtype throughout (raw inputs, all-gather copies)
-    xfer_dispatch<T, OpSum, PM, KMAX>(ns, s, d, nd, n, o->scale, vec);
+    xfer_dispatch<T, OpSum, PM>(ns, s, d, nd, n, o->scale, vec);
     return;
   }
   const int sp = sm == 0 ? SP_T : (sm == (all_s & ~1u) ? SP_TW : (sm == all_s ? SP_W : -1));
@@ -759,12 +743,12 @@ __device__ FX_INLINE void xfer_op_typed(const DevCtx& c, const Op* o, uint32_t l
   switch (ns) {
     case 1: ok = xfer_mx_k<T, W, 1, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
     case 2: ok = xfer_mx_k<T, W, 2, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-    case 3: if constexpr (KMAX >= 3) ok = xfer_mx_k<T, W, 3, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-    case 4: if constexpr (KMAX >= 4) ok = xfer_mx_k<T, W, 4, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-    case 5: if constexpr (KMAX >= 5) ok = xfer_mx_k<T, W, 5, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-    case 6: if constexpr (KMAX >= 6) ok = xfer_mx_k<T, W, 6, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-    case 7: if constexpr (KMAX >= 7) ok = xfer_mx_k<T, W, 7, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-    default: if constexpr (KMAX >= 8) ok = xfer_mx_k<T, W, 8, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    case 3: ok = xfer_mx_k<T, W, 3, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    case 4: ok = xfer_mx_k<T, W, 4, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    case 5: ok = xfer_mx_k<T, W, 5, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    case 6: ok = xfer_mx_k<T, W, 6, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    case 7: ok = xfer_mx_k<T, W, 7, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    default: ok = xfer_mx_k<T, W, 8, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
   }
   if (!ok && threadIdx.x == 0)  // unreachable for validated programs: fail loudly, never compute wrongly
     __hip_atomic_store(c.err, (uint32_t)(0x40000000u | (0xfdu << 8)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -812,7 +796,7 @@ __device__ FX_INLINE bool fp8_scale(const DevCtx& c, uint32_t b, uint64_t epoch,
   return __all(ok) != 0;
 }
 
-template <typename T, typename OP, int PM, typename W = void, int KMAX = 8>
+template <typename T, typename OP, int PM, typename W = void>
 __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uint32_t grid) {
   __shared__ int s_abort;
   __shared__ float s_pre;
@@ -856,8 +840,8 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
       bool bar = false;
       for (uint32_t k = 0; k < n; ++k) {
         const Op* q = c.ops + i + (n > 1 ? (k + lb) % n : 0);
-        if constexpr (TYPED) xfer_op_typed<T, WT_, PM, KMAX>(c, q, lb, nb, quantum, par, pre, post_inv);
-        else xfer_op<T, OP, PM, KMAX>(c, q, lb, nb, quantum, par);
+        if constexpr (TYPED) xfer_op_typed<T, WT_, PM>(c, q, lb, nb, quantum, par, pre, post_inv);
+        else xfer_op<T, OP, PM>(c, q, lb, nb, quantum, par);
         bar |= (q->flags & kXferBarrierAfter) != 0;
       }
       if (bar) __syncthreads();
@@ -1018,30 +1002,30 @@ __global__ void __launch_bounds__(kExecThreads) ll_group_kernel(const DevCtx* ct
   if constexpr (sizeof(T) <= 4) ll_body<T, OP>(ctxs[blockIdx.x / grid_per_rank], blockIdx.x % grid_per_rank, grid_per_rank);
 }
 
-// Production launch: one rank per process, context by value. KMAX: see xfer_dispatch.
-template <typename T, typename OP, int PM, int KMAX = 8>
+// Production launch: one rank per process, context by value.
+template <typename T, typename OP, int PM>
 __global__ void __launch_bounds__(kExecThreads) exec_kernel(DevCtx c) {
-  exec_body<T, OP, PM, void, KMAX>(c, blockIdx.x, gridDim.x);
+  exec_body<T, OP, PM>(c, blockIdx.x, gridDim.x);
 }
 
 // Typed programs (Program::wire: fp32 partials or an fp8 wire), SUM/AVG only.
-template <typename T, typename W, int PM, int KMAX = 8>
+template <typename T, typename W, int PM>
 __global__ void __launch_bounds__(kExecThreads) exec_mx_kernel(DevCtx c) {
-  exec_body<T, OpSum, PM, W, KMAX>(c, blockIdx.x, gridDim.x);
+  exec_body<T, OpSum, PM, W>(c, blockIdx.x, gridDim.x);
 }
-template <typename T, typename W, int PM, int KMAX = 8>
+template <typename T, typename W, int PM>
 __global__ void __launch_bounds__(kExecThreads) exec_mx_group_kernel(const DevCtx* ctxs, uint32_t grid_per_rank) {
   const uint32_t r = blockIdx.x / grid_per_rank;
-  exec_body<T, OpSum, PM, W, KMAX>(ctxs[r], blockIdx.x % grid_per_rank, grid_per_rank);
+  exec_body<T, OpSum, PM, W>(ctxs[r], blockIdx.x % grid_per_rank, grid_per_rank);
 }
 
 // In-process group launch: nranks ranks share one grid (rank = blockIdx / grid_per_rank) —
 // every rank's workgroups are co-resident by construction, so the full multi-rank protocol
 // runs on a single GPU in a single process (tests, calibration).
-template <typename T, typename OP, int PM, int KMAX = 8>
+template <typename T, typename OP, int PM>
 __global__ void __launch_bounds__(kExecThreads) exec_group_kernel(const DevCtx* ctxs, uint32_t grid_per_rank) {
   const uint32_t r = blockIdx.x / grid_per_rank;
-  exec_body<T, OP, PM, void, KMAX>(ctxs[r], blockIdx.x % grid_per_rank, grid_per_rank);
+  exec_body<T, OP, PM>(ctxs[r], blockIdx.x % grid_per_rank, grid_per_rank);
 }
 
 // Standalone reduction: dst[0] = scale * OP(src[0..K)), grid-sliced.

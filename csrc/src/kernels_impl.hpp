@@ -2,7 +2,6 @@
 #pragma once
 
 #include <string>
-#include <type_traits>
 
 #include "internal.hpp"
 #include "launch.hpp"
@@ -31,31 +30,6 @@ inline int query_kernel(K kern, const LaunchArgs& a) {
 // must not be reported as this launch's failure (the check after the launch reads only its own error).
 inline void clear_stale_error() { (void)hipGetLastError(); }
 
-template <typename T, typename OP, int KMAX>
-inline void launch_exec(const LaunchArgs& a) {
-  if (a.proto == PM_WT)
-    hipLaunchKernelGGL((exec_kernel<T, OP, PM_WT, KMAX>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
-  else if (a.proto == PM_FENCE_NTS)
-    hipLaunchKernelGGL((exec_kernel<T, OP, PM_FENCE_NTS, KMAX>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
-  else
-    hipLaunchKernelGGL((exec_kernel<T, OP, PM_FENCE, KMAX>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
-}
-template <typename T, typename OP, int KMAX>
-inline void launch_group(const LaunchArgs& a) {
-  if (a.proto == PM_WT)
-    hipLaunchKernelGGL((exec_group_kernel<T, OP, PM_WT, KMAX>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
-                       a.stream, a.d_ctxs, (uint32_t)a.grid);
-  else if (a.proto == PM_FENCE_NTS)
-    hipLaunchKernelGGL((exec_group_kernel<T, OP, PM_FENCE_NTS, KMAX>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
-                       a.stream, a.d_ctxs, (uint32_t)a.grid);
-  else
-    hipLaunchKernelGGL((exec_group_kernel<T, OP, PM_FENCE, KMAX>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
-                       a.stream, a.d_ctxs, (uint32_t)a.grid);
-}
-// The fan-in-2 instantiations exist for SUM (and AVG, its post-scaled form): the collective that
-// carries gradients and activations; other ops keep the one general kernel.
-template <typename OP> constexpr bool kHasK2 = std::is_same<OP, OpSum>::value;
-
 template <typename T, typename OP>
 inline int launch_one(const LaunchArgs& a) {
   if (a.kind != LAUNCH_QUERY) clear_stale_error();
@@ -66,32 +40,27 @@ inline int launch_one(const LaunchArgs& a) {
         return query_kernel(ll_kernel<T, OP>, a);
       }
       if (a.query == 2) return query_kernel(a.proto == PM_WT ? reduce_kernel<T, OP, PM_WT> : reduce_kernel<T, OP, PM_FENCE>, a);
-      if constexpr (kHasK2<OP>) {
-        if (a.kmax <= 2)
-          return query_kernel(a.proto == PM_WT ? exec_kernel<T, OP, PM_WT, 2>
-                                               : a.proto == PM_FENCE_NTS ? exec_kernel<T, OP, PM_FENCE_NTS, 2>
-                                                                         : exec_kernel<T, OP, PM_FENCE, 2>, a);
-      }
       return query_kernel(a.proto == PM_WT ? exec_kernel<T, OP, PM_WT>
                                            : a.proto == PM_FENCE_NTS ? exec_kernel<T, OP, PM_FENCE_NTS>
                                                                      : exec_kernel<T, OP, PM_FENCE>, a);
     case LAUNCH_EXEC:
-      if constexpr (kHasK2<OP>) {
-        if (a.kmax <= 2) {
-          launch_exec<T, OP, 2>(a);
-          break;
-        }
-      }
-      launch_exec<T, OP, 8>(a);
+      if (a.proto == PM_WT)
+        hipLaunchKernelGGL((exec_kernel<T, OP, PM_WT>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
+      else if (a.proto == PM_FENCE_NTS)
+        hipLaunchKernelGGL((exec_kernel<T, OP, PM_FENCE_NTS>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
+      else
+        hipLaunchKernelGGL((exec_kernel<T, OP, PM_FENCE>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
       break;
     case LAUNCH_GROUP:
-      if constexpr (kHasK2<OP>) {
-        if (a.kmax <= 2) {
-          launch_group<T, OP, 2>(a);
-          break;
-        }
-      }
-      launch_group<T, OP, 8>(a);
+      if (a.proto == PM_WT)
+        hipLaunchKernelGGL((exec_group_kernel<T, OP, PM_WT>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
+                           a.stream, a.d_ctxs, (uint32_t)a.grid);
+      else if (a.proto == PM_FENCE_NTS)
+        hipLaunchKernelGGL((exec_group_kernel<T, OP, PM_FENCE_NTS>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
+                           a.stream, a.d_ctxs, (uint32_t)a.grid);
+      else
+        hipLaunchKernelGGL((exec_group_kernel<T, OP, PM_FENCE>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
+                           a.stream, a.d_ctxs, (uint32_t)a.grid);
       break;
     case LAUNCH_REDUCE:
       if (a.proto == PM_WT)
@@ -155,26 +124,16 @@ template <typename T, typename W>
 inline int launch_typed(const LaunchArgs& a) {
   const bool wt = a.proto == PM_WT;
   if (a.kind != LAUNCH_QUERY) clear_stale_error();
-  const bool k2 = a.kmax <= 2;
   switch (a.kind) {
     case LAUNCH_QUERY:
-      if (k2) return query_kernel(wt ? exec_mx_kernel<T, W, PM_WT, 2> : exec_mx_kernel<T, W, PM_FENCE, 2>, a);
       return query_kernel(wt ? exec_mx_kernel<T, W, PM_WT> : exec_mx_kernel<T, W, PM_FENCE>, a);
     case LAUNCH_EXEC:
-      if (wt && k2) hipLaunchKernelGGL((exec_mx_kernel<T, W, PM_WT, 2>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
-      else if (wt) hipLaunchKernelGGL((exec_mx_kernel<T, W, PM_WT>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
-      else if (k2) hipLaunchKernelGGL((exec_mx_kernel<T, W, PM_FENCE, 2>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
+      if (wt) hipLaunchKernelGGL((exec_mx_kernel<T, W, PM_WT>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
       else hipLaunchKernelGGL((exec_mx_kernel<T, W, PM_FENCE>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
       break;
     case LAUNCH_GROUP:
-      if (wt && k2)
-        hipLaunchKernelGGL((exec_mx_group_kernel<T, W, PM_WT, 2>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
-                           a.stream, a.d_ctxs, (uint32_t)a.grid);
-      else if (wt)
+      if (wt)
         hipLaunchKernelGGL((exec_mx_group_kernel<T, W, PM_WT>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
-                           a.stream, a.d_ctxs, (uint32_t)a.grid);
-      else if (k2)
-        hipLaunchKernelGGL((exec_mx_group_kernel<T, W, PM_FENCE, 2>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
                            a.stream, a.d_ctxs, (uint32_t)a.grid);
       else
         hipLaunchKernelGGL((exec_mx_group_kernel<T, W, PM_FENCE>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,

@@ -32,7 +32,6 @@ struct LaunchArgs {
   int* occ_out = nullptr;
   int* regs_out = nullptr;
   int wire = 0;          // EXEC / GROUP / QUERY of a typed program (Program::wire): 1 fp32, 2 e4m3, 3 e5m2
-  int kmax = 8;          // EXEC / GROUP / QUERY: widest XFER fan-in of the program (<= 2: the KMAX = 2 kernels)
 };
 
 // Typed-program executors (exec_mx_kernel), SUM/AVG only: fp32 partials for 16/8-bit dtypes
