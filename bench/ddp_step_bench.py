@@ -78,7 +78,7 @@ def worker(rank, world, port, mode, q):
         ddp = DDP(model, device_ids=[0], bucket_cap_mb=float(os.environ.get("DDPB_BUCKET_MB", "25")))
         state = None
         if mode == "hook":
-            state = fb.FlexarHookState()
+            state = fb.FlexarHookState(algo=os.environ.get("DDPB_HOOK_ALGO") or None)
 
             def hook(st, bucket):
                 t0 = time.perf_counter()

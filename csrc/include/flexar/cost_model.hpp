@@ -112,25 +112,28 @@ inline ProgramCost program_cost(const Program& P, uint32_t rank, int links) {
 }
 
 // Partial sums of multi-hop schedules for 16/8-bit float SUM/AVG (FLEXAR_PARTIALS):
-//   fp32 (default): typed staging keeps every partial in fp32 - one rounding, like flat (<= 1 ulp of the
+//   fp32:           typed staging keeps every partial in fp32 - one rounding, like flat (<= 1 ulp of the
 //                   exact sum, tests/test_gpu_kernels.py::test_group_typed_fp32_partials) - at the price of
 //                   fp32 link bytes on every hop but the first (bf16 ring at N = 8: 20/8 S instead of 14/8 S);
 //   wire:           partials travel in the call's dtype and are rounded at every hop ("+rw", the reference's
-//                   ring semantics, mpi_mod.hpp:1129-1147): h roundings (ring N - 1, tree one per stage), error
-//                   <= h ulps of the partial sums' magnitude;
-//   auto:           the cost model prices both forms of the schedule and takes the per-hop one when it is at
+//                   ring semantics, mpi_mod.hpp:1129-1147, and RCCL's): h roundings (ring N - 1, tree one per
+//                   stage), error <= h ulps of the partial sums' magnitude;
+//   auto (default): the cost model prices both forms of the schedule and takes the per-hop one when it is at
 //                   least kAutoRwGain faster AND rounds at most kAutoRwMaxRoundings times (RHD at N = 8: 3;
 //                   a ring at N = 8 rounds 7 times and keeps fp32 partials): error <= 3 ulps.
+// Round 4 measured the fp32-partials executor at the untyped executor's HBM rate (5.15 vs 5.25 TB/s, RHD bf16,
+// 4 ranks on one GPU, profiles/r4_partials): its extra time is exactly its extra bytes (1.19x for RHD), so the
+// default is the policy that drops those bytes where they are worth more than two extra roundings.
 enum class Partials { FP32 = 0, WIRE = 1, AUTO = 2 };
 constexpr double kAutoRwGain = 0.10;
 constexpr int kAutoRwMaxRoundings = 3;
 
 inline Partials partials_from_env() {
   const char* e = getenv("FLEXAR_PARTIALS");
-  if (!e || !*e || !strcmp(e, "fp32")) return Partials::FP32;
+  if (!e || !*e || !strcmp(e, "auto")) return Partials::AUTO;
   if (!strcmp(e, "wire") || !strcmp(e, "rw")) return Partials::WIRE;
-  if (!strcmp(e, "auto")) return Partials::AUTO;
-  return Partials::FP32;
+  if (!strcmp(e, "fp32")) return Partials::FP32;
+  return Partials::AUTO;
 }
 
 // The call a schedule is priced for: element size, and whether it is a 16/8-bit float SUM/AVG (the

@@ -223,9 +223,13 @@ __device__ FX_INLINE uint4 combine16(const uint4 (&x)[K], float scale, bool sc) 
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] = OP::apply(acc[e], Elem<T>::load(v[e]));
   }
-  if (sc) {
+  // The post-scale multiplies unconditionally (x * 1 is exact): a runtime `if (sc)` here is if-converted
+  // by the compiler into a multiply AND a select per element (v_pk_mul + v_cndmask), the select being pure
+  // overhead in the common unscaled case. Integer types never scale (sc is false at compile time).
+  if constexpr (Elem<T>::is_float) {
+    const A f = sc ? (A)scale : (A)1;
 #pragma unroll
-    for (int e = 0; e < E; ++e) acc[e] = (A)(acc[e] * (A)scale);
+    for (int e = 0; e < E; ++e) acc[e] = (A)(acc[e] * f);
   }
 #pragma unroll
   for (int e = 0; e < E; ++e) v[e] = Elem<T>::store(acc[e]);
@@ -535,10 +539,8 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
 #pragma unroll
       for (int e = 0; e < G; ++e) acc[e] = k ? acc[e] + x[e] : x[e];
     }
-    if (scale != 1.0f) {
 #pragma unroll
-      for (int e = 0; e < G; ++e) acc[e] *= scale;
-    }
+    for (int e = 0; e < G; ++e) acc[e] *= scale;  // unconditional (x * 1 is exact): no per-element select
     if constexpr (FP8) {
       if (round_y) fp8_round_g<W, G>(acc);
     }

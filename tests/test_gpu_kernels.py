@@ -79,12 +79,51 @@ def _specs(n):
 
 @pytest.fixture(scope="module")
 def groups(cuda):
+    """Groups with FLEXAR_PARTIALS=fp32: the tests below assert single rounding of multi-hop schedules (the
+    default "auto" policy may round per hop; test_group_partials_auto_default covers it)."""
+    import os
+
     from allreduce_over_mpi_amd.parallel import LocalGroup
 
-    gs = {n: LocalGroup(n, workspace_bytes=64 << 20) for n in (2, 3, 4, 8)}
+    old = os.environ.get("FLEXAR_PARTIALS")
+    os.environ["FLEXAR_PARTIALS"] = "fp32"
+    try:
+        gs = {n: LocalGroup(n, workspace_bytes=64 << 20) for n in (2, 3, 4, 8)}
+    finally:
+        if old is None:
+            os.environ.pop("FLEXAR_PARTIALS")
+        else:
+            os.environ["FLEXAR_PARTIALS"] = old
     yield gs
     for g in gs.values():
         g.close()
+
+
+def test_group_partials_auto_default(cuda):
+    """The default partials policy ("auto", round 4): a large bf16 RHD at N = 8 runs the per-hop-rounded form
+    (three roundings, 1.19x fewer HBM bytes than fp32 partials), a ring keeps fp32 partials (seven roundings
+    would be too many); results stay within the roundings' ulps and identical on every rank."""
+    import os
+
+    from allreduce_over_mpi_amd.parallel import LocalGroup
+
+    assert "FLEXAR_PARTIALS" not in os.environ
+    n, count = 8, 8 << 20
+    grp = LocalGroup(n, workspace_bytes=256 << 20)
+    try:
+        g = torch.Generator(device=cuda).manual_seed(5)
+        xs = [torch.randn(count, device=cuda, generator=g).to(torch.bfloat16) for _ in range(n)]
+        exact = torch.stack([x.double() for x in xs]).sum(0).to(torch.bfloat16)
+        for spec, most in (("rhd", 3), ("ring", 1)):
+            outs = grp.all_reduce([x.clone() for x in xs], "sum", algo=spec)
+            torch.cuda.synchronize()
+            for o in outs:
+                assert torch.equal(o.view(torch.int16), outs[0].view(torch.int16)), spec
+            u = _ulps(outs[0], exact)
+            assert u <= most, (spec, u)
+        grp.check()
+    finally:
+        grp.close()
 
 
 @pytest.mark.parametrize("n", [2, 3, 4, 8])
