@@ -120,7 +120,8 @@ inline ProgramCost program_cost(const Program& P, uint32_t rank, int links) {
 //                   stage), error <= h ulps of the partial sums' magnitude;
 //   auto (default): the cost model prices both forms of the schedule and takes the per-hop one when it is at
 //                   least kAutoRwGain faster AND rounds at most kAutoRwMaxRoundings times (RHD at N = 8: 3;
-//                   a ring at N = 8 rounds 7 times and keeps fp32 partials): error <= 3 ulps.
+//                   a ring at N = 8 rounds 7 times and keeps fp32 partials): at most 3 roundings, each
+//                   within u = 2^-8 (bf16) of its partial sum.
 // Round 4 measured the fp32-partials executor at the untyped executor's HBM rate (5.15 vs 5.25 TB/s, RHD bf16,
 // 4 ranks on one GPU, profiles/r4_partials): its extra time is exactly its extra bytes (1.19x for RHD), so the
 // default is the policy that drops those bytes where they are worth more than two extra roundings.
