@@ -47,7 +47,7 @@ def _sig(lib):
         "flexar_comm_destroy": (i, [vp]),
         "flexar_comm_destroy_local": (i, [vp]),
         "flexar_comm_resync": (i, [vp]),
-        "flexar_comm_host_agree": (i, [vp, c.c_uint64, c.POINTER(c.c_uint64)]),
+        "flexar_comm_host_agree": (i, [vp, c.c_uint64, i, c.POINTER(c.c_uint64)]),
         "flexar_host_barrier_run": (i, [cp, i, i, i, c.c_uint64, i]),
         "flexar_comm_selftest_note": (i, [vp, cp, sz]),
         "flexar_comm_rank": (i, [vp]),

@@ -259,13 +259,14 @@ class FlexarProcessGroup(dist.ProcessGroup):
         """Collective: per flag, True when it is True on EVERY rank. Up to 64 flags go through the flexar
         communicator's host shared-memory page (one max over a bitmask of the flags that are False here:
         microseconds, where a blocking gloo allreduce costs a TCP round trip on every probe-window call,
-        VERDICT r3 weak 7); otherwise, or when the communicator has no page, one gloo MIN."""
+        VERDICT r3 weak 7); otherwise, or when the communicator has no page, one gloo MIN. (A bitwise OR of
+        the ranks' masks: a max of them would lose every flag below another rank's highest False one.)"""
         flags = [bool(f) for f in flags]
         if self._host_agree is None:  # once, over gloo: does EVERY rank's communicator have the page?
             have = bool(comm.topology().get("host_page")) if self._world > 1 else False
             self._host_agree = self._gloo_min([have])[0]
         if len(flags) <= 64 and self._host_agree:
-            anyfalse = comm.host_agree_max(sum(1 << i for i, f in enumerate(flags) if not f))
+            anyfalse = comm.host_agree_or(sum(1 << i for i, f in enumerate(flags) if not f))
             return [not (anyfalse >> i) & 1 for i in range(len(flags))]
         return self._gloo_min(flags)
 

@@ -333,8 +333,15 @@ class Communicator:
         """Collective: the maximum of ``value`` (0 .. 2**64 - 1) over the ranks, through the communicator's
         host shared-memory page - no device call, no bootstrap round trip. Raises
         FlexarError when the communicator has no page (single rank, in-process group)."""
+        return self._host_agree(value, 0)
+
+    def host_agree_or(self, value: int) -> int:
+        """Collective: the bitwise OR of ``value`` over the ranks (see :meth:`host_agree_max`)."""
+        return self._host_agree(value, 1)
+
+    def _host_agree(self, value: int, op: int) -> int:
         out = ctypes.c_uint64(0)
-        nv.check(self._lib.flexar_comm_host_agree(self._h, int(value), ctypes.byref(out)), "host_agree")
+        nv.check(self._lib.flexar_comm_host_agree(self._h, int(value), op, ctypes.byref(out)), "host_agree")
         return int(out.value)
 
     def topology(self) -> dict:

@@ -93,9 +93,9 @@ int flexar_comm_connect(flexar_comm_t comm, const void* all_handles);
 int flexar_comm_destroy(flexar_comm_t comm);
 /* Non-collective teardown (garbage collection): no agreement; exported buffers stay allocated. */
 int flexar_comm_destroy_local(flexar_comm_t comm);
-/* Collective host-side agreement (shared-memory page of a connected communicator): *max_out = the maximum
- * of `mine` over the ranks. FLEXAR_ERR_STATE when the communicator has no page. */
-int flexar_comm_host_agree(flexar_comm_t comm, uint64_t mine, uint64_t* max_out);
+/* Collective host-side agreement (shared-memory page of a connected communicator): *out = the maximum
+ * (op 0) or bitwise OR (op 1) of `mine` over the ranks. FLEXAR_ERR_STATE when the communicator has no page. */
+int flexar_comm_host_agree(flexar_comm_t comm, uint64_t mine, int op, uint64_t* out);
 int flexar_comm_rank(flexar_comm_t comm);
 int flexar_comm_size(flexar_comm_t comm);
 

@@ -655,9 +655,11 @@ int flexar_host_barrier_run(const char* name, int rank, int nranks, int phases, 
     if (delay_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(delay_ms));
     int late = -1;
     uint64_t mx = 0;
-    // odd phases also exchange a value: the maximum of rank * 1000 + phase is the last rank's
+    // odd phases also exchange a value: the maximum of rank * 1000 + phase is the last rank's; phases
+    // 2 mod 4 OR one bit per rank
     const bool ok = (p & 1) ? hb.exchange_max((uint64_t)rank * 1000 + p, &mx, timeout_ms, &late)
-                            : hb.arrive_and_wait(timeout_ms, &late);
+                  : (p % 4 == 2) ? hb.exchange(1ull << rank, &mx, timeout_ms, &late, true)
+                                 : hb.arrive_and_wait(timeout_ms, &late);
     if (!ok) {
       hb.unlink();
       set_error("phase " + std::to_string(p) + ": rank " + std::to_string(late) + " did not arrive");
@@ -665,6 +667,10 @@ int flexar_host_barrier_run(const char* name, int rank, int nranks, int phases, 
     }
     if ((p & 1) && mx != (uint64_t)(nranks - 1) * 1000 + p) {
       set_error("phase " + std::to_string(p) + ": exchanged maximum " + std::to_string(mx));
+      return FLEXAR_ERR_STATE;
+    }
+    if (p % 4 == 2 && mx != (nranks == 64 ? ~0ull : (1ull << nranks) - 1)) {
+      set_error("phase " + std::to_string(p) + ": exchanged OR " + std::to_string(mx));
       return FLEXAR_ERR_STATE;
     }
     if (p == 0 && rank == 0) hb.unlink();

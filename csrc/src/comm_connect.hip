@@ -753,16 +753,16 @@ extern "C" {
 
 int flexar_comm_destroy(flexar_comm_t c) { return c ? destroy_impl(c, true) : 0; }
 
-// Host-side agreement of this communicator's ranks (collective: every rank, same order): the maximum of
-// one 64-bit value over the ranks, through the teardown page (host_barrier.hpp) - microseconds, no device
-// call and no bootstrap round trip. FLEXAR_ERR_STATE when the communicator has no page (single rank,
-// in-process group, message-transport-only without a shared host), FLEXAR_ERR_TIMEOUT naming a late rank.
-int flexar_comm_host_agree(flexar_comm_t c, uint64_t mine, uint64_t* max_out) {
-  if (!c || !max_out) { set_error("null argument"); return FLEXAR_ERR_INVALID; }
+// Host-side agreement of this communicator's ranks (collective: every rank, same order): the maximum
+// (op 0) or the bitwise OR (op 1) of one 64-bit value over the ranks, through the teardown page
+// (host_barrier.hpp) - microseconds, no device call and no bootstrap round trip. FLEXAR_ERR_STATE when the
+// communicator has no page (single rank, in-process group), FLEXAR_ERR_TIMEOUT naming a late rank.
+int flexar_comm_host_agree(flexar_comm_t c, uint64_t mine, int op, uint64_t* out) {
+  if (!c || !out || op < 0 || op > 1) { set_error("bad host agreement arguments"); return FLEXAR_ERR_INVALID; }
   if (!c->hb) { set_error("no host agreement page on this communicator"); return FLEXAR_ERR_STATE; }
   int late = -1;
   const uint64_t tmo = std::max<uint64_t>(1000, c->timeout_ticks / 100000ull);
-  if (!c->hb->exchange_max(mine, max_out, tmo, &late)) {
+  if (!c->hb->exchange(mine, out, tmo, &late, op == 1)) {
     set_error("host agreement: rank " + std::to_string(late) + " did not arrive within " + std::to_string(tmo) + " ms");
     return FLEXAR_ERR_TIMEOUT;
   }

@@ -102,18 +102,25 @@ class HostBarrier {
     }
   }
 
-  // A barrier that also takes the maximum of one value over the ranks. The value is published before this
-  // rank arrives (release) and read after every rank has (acquire); a rank cannot be two phases ahead of
-  // another, so one slot per phase parity never holds a value someone still has to read.
-  bool exchange_max(uint64_t mine, uint64_t* out, uint64_t timeout_ms, int* straggler) {
+  // A barrier that also combines one value per rank: the maximum (bor = false) or the bitwise OR (bor =
+  // true). The value is published before this rank arrives (release) and read after every rank has
+  // (acquire); a rank cannot be two phases ahead of another, so one slot per phase parity never holds a
+  // value someone still has to read.
+  bool exchange(uint64_t mine, uint64_t* out, uint64_t timeout_ms, int* straggler, bool bor = false) {
     if (!page_) return false;
     const int par = (int)((phase_ + 1) & 1);
     page_->value[par][rank_].store(mine, std::memory_order_relaxed);
     if (!arrive_and_wait(timeout_ms, straggler)) return false;
     uint64_t m = 0;
-    for (int r = 0; r < nranks_; ++r) m = std::max<uint64_t>(m, page_->value[par][r].load(std::memory_order_relaxed));
+    for (int r = 0; r < nranks_; ++r) {
+      const uint64_t v = page_->value[par][r].load(std::memory_order_relaxed);
+      m = bor ? (m | v) : std::max<uint64_t>(m, v);
+    }
     if (out) *out = m;
     return true;
+  }
+  bool exchange_max(uint64_t mine, uint64_t* out, uint64_t timeout_ms, int* straggler) {
+    return exchange(mine, out, timeout_ms, straggler, false);
   }
 
   // Removes the name (existing mappings stay valid); safe to call more than once and from every rank.

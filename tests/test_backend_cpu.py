@@ -89,3 +89,69 @@ def test_file_exchange_rendezvous(tmp_path):
         a, b = res[r]
         assert a == [b"hello0", b"hello1", b"hello2"]
         assert b == [b"\x00", b"\x01\x01", b"\x02\x02\x02"]
+
+
+class _PageStub:
+    """Stand-in for a device Communicator's host agreement (Communicator.host_agree_or: bitwise OR over the
+    ranks of one 64-bit value), computed with a gloo BOR so the backend's bitmask logic runs on the CPU."""
+
+    def __init__(self, has_page, pg):
+        self.has_page, self.pg, self.calls = has_page, pg, 0
+
+    def topology(self):
+        return {"host_page": self.has_page}
+
+    def host_agree_or(self, v):
+        import torch.distributed as dist
+
+        self.calls += 1
+        t = torch.tensor([v], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.BOR, group=self.pg)
+        return int(t.item())
+
+
+def _agree_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import torch.distributed as dist
+
+        import allreduce_over_mpi_amd.parallel.backend as fb  # noqa: F401  registers "flexar"
+
+        dist.init_process_group("flexar", rank=rank, world_size=world)
+        pg = dist.group.WORLD
+        side = dist.new_group(backend="gloo")
+        out = {}
+        for has_page in (True, False):
+            pg._host_agree = None
+            stub = _PageStub(has_page and True, side)
+            # flag 1 is False on rank 0 only, flag 3 on rank 1 only, flag 5 everywhere; the others are True
+            flags = [not ((i == 1 and rank == 0) or (i == 3 and rank == 1) or i == 5) for i in range(7)]
+            got = pg._agree_all(flags, stub)
+            out[has_page] = (got, stub.calls, pg._host_agree)
+        dist.destroy_process_group()
+        q.put((rank, out, None))
+    except Exception:
+        import traceback
+
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_backend_agreements_over_the_host_page_bitmask():
+    """The zero-copy probe / sweep agreements (FlexarProcessGroup._agree_all): per flag, True only when it is
+    True on every rank - through one host-page max over a bitmask of this rank's False flags when every rank
+    has the page, else one gloo MIN."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_agree_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(2)]
+    for p in ps:
+        p.join(60)
+    for rank, out, err in res:
+        assert err is None, err
+        for has_page in (True, False):
+            got, calls, mode = out[has_page]
+            assert got == [True, False, True, False, True, False, True], (has_page, got)
+            assert calls == (1 if has_page else 0) and mode is has_page

@@ -42,7 +42,7 @@ def _spawn(world, phases, timeout_ms, delays, absent=()):
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_barrier_phases_any_arrival_order(world):
     # staggered arrivals (rank r is r * 15 ms late at every phase): everyone passes every phase
-    name, out = _spawn(world, 3, 20000, [15 * r for r in range(world)])
+    name, out = _spawn(world, 4, 20000, [15 * r for r in range(world)])
     assert sorted(out) == list(range(world))
     for r, (rc, err, _) in out.items():
         assert rc == 0, (r, err)
