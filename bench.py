@@ -143,9 +143,10 @@ def configure_env(world: int, rank: int, local: int, environ) -> tuple:
         local = 0
         # 8 processes x HIP's default 4 hardware queues oversubscribe the GPU's compute queues: the command
         # processor then time-slices the processes and every cross-rank hand-off waits for a queue switch
-        # (measured: 28.6 ms instead of 1.0 ms per 256 MiB call at N = 8). Set before HIP initialises.
-        if world > 4:
-            environ.setdefault("GPU_MAX_HW_QUEUES", "2")
+        # (measured: 28.6 ms instead of 1.0 ms per 256 MiB call at N = 8). Set before HIP initialises. A cap,
+        # not a default: the GPU box exports HIP's own default (4) explicitly (profiles/r4_rehearsal).
+        if world > 4 and int(environ.get("GPU_MAX_HW_QUEUES", "4") or 4) > 2:
+            environ["GPU_MAX_HW_QUEUES"] = "2"
         # every rank's workgroups must be co-resident on the one GPU (they spin on each other)
         environ.setdefault("FLEXAR_MAX_GRID", str(max(8, 256 // (2 * world))))
     return local, shared, shared_rccl

@@ -158,8 +158,10 @@ def main():
     import torch.multiprocessing as mp
 
     world = int(os.environ.get("DDPB_RANKS", "2"))
-    if world >= 4:  # every rank shares one GPU: keep the processes' hardware queues resident
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", "2")
+    # every rank shares one GPU: keep the processes' hardware queues resident; a cap, since the
+    # GPU box exports HIP's default of 4 explicitly
+    if world >= 4 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) > 2:
+        os.environ["GPU_MAX_HW_QUEUES"] = "2"
     ctx = mp.get_context("spawn")
     for mode in os.environ.get("DDPB_MODES", "pg,pg_nozc,hook,nccl").split(","):
         q = ctx.Queue()

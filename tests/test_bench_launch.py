@@ -38,7 +38,11 @@ def test_shared_gpu_rehearsal_env(world, queues, grid):
     env = {"FLEXAR_BENCH_SHARED_GPU": "1", "FLEXAR_BENCH_SHARED_RCCL": "1", "GPU_MAX_HW_QUEUES": "4"}
     bench.configure_env(world, 1, 1, env)
     assert env["NCCL_HOSTID"] == "flexar-bench-rank1" and env["NCCL_SOCKET_IFNAME"] == "lo"
-    assert env["GPU_MAX_HW_QUEUES"] == "4"  # an explicit setting is kept
+    # a cap, not a default: the GPU box exports HIP's default of 4 explicitly; 1 stays 1
+    assert env["GPU_MAX_HW_QUEUES"] == ("2" if world > 4 else "4")
+    env = {"FLEXAR_BENCH_SHARED_GPU": "1", "GPU_MAX_HW_QUEUES": "1"}
+    bench.configure_env(world, 1, 1, env)
+    assert env["GPU_MAX_HW_QUEUES"] == "1"
 
 
 def _stub(tmp_path, body):

@@ -103,8 +103,10 @@ def _worker(rank, world, port, shared, q, transport="rccl", no_ipc=False, parts=
         if shared:  # every rank on device 0: co-resident grids, one NCCL_HOSTID per rank (RCCL over loopback)
             os.environ.update(FLEXAR_MAX_GRID=str(max(8, 256 // (2 * world))), NCCL_HOSTID=f"flexar-md-rank{rank}",
                               NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
-            if world > 4:  # 8 processes x 4 hardware queues would be time-sliced by the command processor
-                os.environ.setdefault("GPU_MAX_HW_QUEUES", "2")
+            # 8 processes x 4 hardware queues would be time-sliced by the command processor; a cap, since the
+            # GPU box exports HIP's default of 4 explicitly
+            if world > 4 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) > 2:
+                os.environ["GPU_MAX_HW_QUEUES"] = "2"
         if no_ipc:
             os.environ["FLEXAR_FAULT_NO_IPC"] = "1"  # every peer mapping fails: the RCCL fallback carries all
         import torch.distributed as dist
