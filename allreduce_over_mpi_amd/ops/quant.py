@@ -55,3 +55,19 @@ def fp8_dequantize(q, amax, num: float = 448.0, out=None, dtype=None, stream=Non
     nv.check(nv.lib().flexar_dequantize_fp8(q.data_ptr(), x.data_ptr(), nv.dtype_code(x.dtype), q.numel(),
                                             amax.data_ptr(), float(num), _stream_handle(stream)), "dequantize_fp8")
     return x
+
+
+def fp8_wire_scale(nranks: int, amax: float, wire: str = "e4m3") -> float:
+    """The pre-scale s the fp8-wire executor derives on the device (device_exec.hpp fp8_scale): fp8_max /
+    (N * global amax * (1 + h)), h the wire type's largest relative rounding step, computed in fp32 and
+    rounded DOWN to a power of two (so x * s is exact and gfx950's scaled converts apply it). Every
+    contribution is quantised as fp8(x * s) and the result written as q / s."""
+    import numpy as np
+
+    f = np.float32
+    wmax, head = (f(448.0), f(1.0625)) if wire == "e4m3" else (f(57344.0), f(1.125))
+    g = f(amax)
+    s = wmax / (f(nranks) * g * head) if (g > 0 and g < f(3.0e38)) else f(1.0)
+    s = min(max(s, f(2.0 ** -120)), f(2.0 ** 120))
+    bits = np.array([s], dtype=np.float32).view(np.uint32)[0] & np.uint32(0x7F800000)
+    return float(np.array([bits], dtype=np.uint32).view(np.float32)[0])

@@ -434,6 +434,130 @@ __device__ FX_INLINE uint32_t fp8_word_encode(const float* x) {
   return (uint32_t)w;
 }
 
+// gfx950 scaled fp8 conversions (v_cvt_scalef32_pk_*): quantise a pair of f32 / bf16 / f16 values to fp8,
+// or dequantise an fp8 pair back, with a scale in ONE instruction. Measured on the device
+// (tools/probes/scaled_cvt_probe.hip, profiles/r4_scaled_cvt): q = rne(x / 2^floor(log2 scale)) and
+// x = q * 2^floor(log2 scale) - only the scale's exponent counts (OCP MX e8m0 semantics) - and an overflow
+// is NaN, as with the unscaled packed converts. The fp8 wire's pre-scale is a power of two (fp8_scale), so
+// these give bit for bit what decode -> x * s -> encode gave, with 1 instruction per 2 elements instead of
+// 3-5 (bf16: no f32 decode at all; the pair IS the instruction's packed operand).
+typedef short fx_s2 __attribute__((ext_vector_type(2)));
+typedef __bf16 fx_bf2 __attribute__((ext_vector_type(2)));
+typedef _Float16 fx_h2 __attribute__((ext_vector_type(2)));
+typedef float fx_f2 __attribute__((ext_vector_type(2)));
+template <typename T> struct HasScaledCvt { static constexpr bool value = false; };
+template <> struct HasScaledCvt<float> { static constexpr bool value = true; };
+template <> struct HasScaledCvt<bf16_t> { static constexpr bool value = true; };
+template <> struct HasScaledCvt<f16_t> { static constexpr bool value = true; };
+
+// G values of T (packed in raw) -> G fp8 values (packed in out): q = rne(x / inv), inv a power of two
+template <typename T, typename W, int G>
+__device__ FX_INLINE void sq_group(const uint4* raw, float inv, uint4* out) {
+  constexpr bool E4 = IsFp8<W>::e4m3;
+  uint32_t w[G / 4];
+  if constexpr (std::is_same<T, float>::value) {
+    float f[G];
+    __builtin_memcpy(f, raw, sizeof(f));
+#pragma unroll
+    for (int i = 0; i < G / 4; ++i) {
+      fx_s2 r = {0, 0};
+      if constexpr (E4) {
+        r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(r, f[4 * i], f[4 * i + 1], inv, false);
+        r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(r, f[4 * i + 2], f[4 * i + 3], inv, true);
+      } else {
+        r = __builtin_amdgcn_cvt_scalef32_pk_bf8_f32(r, f[4 * i], f[4 * i + 1], inv, false);
+        r = __builtin_amdgcn_cvt_scalef32_pk_bf8_f32(r, f[4 * i + 2], f[4 * i + 3], inv, true);
+      }
+      __builtin_memcpy(&w[i], &r, 4);
+    }
+  } else {
+    uint32_t p[G / 2];
+    __builtin_memcpy(p, raw, sizeof(p));
+#pragma unroll
+    for (int i = 0; i < G / 4; ++i) {
+      fx_s2 r = {0, 0};
+      if constexpr (std::is_same<T, bf16_t>::value) {
+        fx_bf2 a, b;
+        __builtin_memcpy(&a, &p[2 * i], 4);
+        __builtin_memcpy(&b, &p[2 * i + 1], 4);
+        if constexpr (E4) {
+          r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, a, inv, false);
+          r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, b, inv, true);
+        } else {
+          r = __builtin_amdgcn_cvt_scalef32_pk_bf8_bf16(r, a, inv, false);
+          r = __builtin_amdgcn_cvt_scalef32_pk_bf8_bf16(r, b, inv, true);
+        }
+      } else {
+        fx_h2 a, b;
+        __builtin_memcpy(&a, &p[2 * i], 4);
+        __builtin_memcpy(&b, &p[2 * i + 1], 4);
+        if constexpr (E4) {
+          r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(r, a, inv, false);
+          r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(r, b, inv, true);
+        } else {
+          r = __builtin_amdgcn_cvt_scalef32_pk_bf8_f16(r, a, inv, false);
+          r = __builtin_amdgcn_cvt_scalef32_pk_bf8_f16(r, b, inv, true);
+        }
+      }
+      __builtin_memcpy(&w[i], &r, 4);
+    }
+  }
+  __builtin_memcpy(out, w, sizeof(w));
+}
+
+// G fp8 values (packed in raw) -> G values of T (packed in out): x = q * scale, scale a power of two
+template <typename T, typename W, int G>
+__device__ FX_INLINE void dq_group(const uint4* raw, float scale, uint4* out) {
+  constexpr bool E4 = IsFp8<W>::e4m3;
+  uint32_t w[G / 4];
+  __builtin_memcpy(w, raw, sizeof(w));
+  if constexpr (std::is_same<T, float>::value) {
+    float f[G];
+#pragma unroll
+    for (int i = 0; i < G / 4; ++i) {
+      fx_f2 lo, hi;
+      if constexpr (E4) {
+        lo = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(w[i], scale, false);
+        hi = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(w[i], scale, true);
+      } else {
+        lo = __builtin_amdgcn_cvt_scalef32_pk_f32_bf8(w[i], scale, false);
+        hi = __builtin_amdgcn_cvt_scalef32_pk_f32_bf8(w[i], scale, true);
+      }
+      f[4 * i] = lo.x; f[4 * i + 1] = lo.y; f[4 * i + 2] = hi.x; f[4 * i + 3] = hi.y;
+    }
+    __builtin_memcpy(out, f, sizeof(f));
+  } else {
+    uint32_t p[G / 2];
+#pragma unroll
+    for (int i = 0; i < G / 4; ++i) {
+      if constexpr (std::is_same<T, bf16_t>::value) {
+        fx_bf2 lo, hi;
+        if constexpr (E4) {
+          lo = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[i], scale, false);
+          hi = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[i], scale, true);
+        } else {
+          lo = __builtin_amdgcn_cvt_scalef32_pk_bf16_bf8(w[i], scale, false);
+          hi = __builtin_amdgcn_cvt_scalef32_pk_bf16_bf8(w[i], scale, true);
+        }
+        __builtin_memcpy(&p[2 * i], &lo, 4);
+        __builtin_memcpy(&p[2 * i + 1], &hi, 4);
+      } else {
+        fx_h2 lo, hi;
+        if constexpr (E4) {
+          lo = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(w[i], scale, false);
+          hi = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(w[i], scale, true);
+        } else {
+          lo = __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(w[i], scale, false);
+          hi = __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(w[i], scale, true);
+        }
+        __builtin_memcpy(&p[2 * i], &lo, 4);
+        __builtin_memcpy(&p[2 * i + 1], &hi, 4);
+      }
+    }
+    __builtin_memcpy(out, p, sizeof(p));
+  }
+}
+
 template <typename S, int G>
 __device__ FX_INLINE void decode_g(const uint4* raw, float (&x)[G]) {
   if constexpr (IsFp8<S>::value && G % 4 == 0) {
@@ -522,12 +646,24 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
   // rounding, done by the store's encode; any dtype destination needs the rounded value itself
   const bool direct = FP8 && K == 1 && SP == SP_T && dm == (1u << nd) - 1 && scale == 1.0f;
   const bool round_y = FP8 && dm && !direct;
+  // gfx950 scaled converts (sq_group / dq_group): the quantising push (dtype -> fp8 everywhere) and the
+  // dequantising all-gather (fp8 -> dtype everywhere) become one conversion per element pair, with no f32
+  // round trip; `post_inv` = 1 / pre is the power of two both directions take
+  constexpr bool SCV = FP8 && HasScaledCvt<T>::value;
+  const bool fast_push = SCV && K == 1 && SP == SP_T && direct;
+  const bool fast_ag = SCV && K == 1 && SP == SP_W && dm == 0 && scale == 1.0f;
   auto compute_group = [&](const uint4 (&raw)[K][VM], float (&acc)[G]) {
+    if (fast_push || fast_ag) return;  // encode_dst converts straight from `raw`
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       float x[G];
       if (isw(k)) {
         decode_g<W, G>(raw[k], x);
+      } else if constexpr (SCV) {
+        // every own contribution is the value the peers receive: fp8(x * pre), in one scaled convert
+        uint4 q[VW > 0 ? VW : 1];
+        sq_group<T, W, G>(raw[k], post_inv, q);
+        decode_g<W, G>(q, x);
       } else {
         decode_g<T, G>(raw[k], x);
         if constexpr (FP8) {
@@ -546,7 +682,11 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
     }
   };
   // destination dd's G values, packed in its element type
-  auto encode_dst = [&](int dd, const float (&acc)[G], uint4 (&y)[VM]) {
+  auto encode_dst = [&](int dd, const uint4 (&raw)[K][VM], const float (&acc)[G], uint4 (&y)[VM]) {
+    if constexpr (SCV && K == 1) {
+      if (fast_push) return sq_group<T, W, G>(raw[0], post_inv, y);
+      if (fast_ag) return dq_group<T, W, G>(raw[0], post_inv, y);
+    }
     if ((dm >> dd) & 1) {
       encode_g<W, G, !FP8>(acc, y);  // fp8 wire values are in range: packed encode, no clamp
     } else {
@@ -563,7 +703,7 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
     for (int dd = 0; dd < kMaxDst; ++dd) {
       if (dd >= nd) continue;
       uint4 y[VM];
-      encode_dst(dd, acc, y);
+      encode_dst(dd, raw, acc, y);
       if ((dm >> dd) & 1) {
 #pragma unroll
         for (int j = 0; j < VW; ++j) st(dd, g * G * sizeof(W) + 16 * j, y[j]);
@@ -621,7 +761,7 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
         for (int dd = 0; dd < kMaxDst; ++dd) {
           if (dd >= nd) continue;
           uint4 y[VM];
-          encode_dst(dd, acc, y);
+          encode_dst(dd, raw[u], acc, y);
           const bool wide = (dm >> dd) & 1;
 #pragma unroll
           for (int j = 0; j < VM; ++j) {
@@ -794,7 +934,12 @@ __device__ FX_INLINE bool fp8_scale(const DevCtx& c, uint32_t b, uint64_t epoch,
   // (and every rounding of it) stays within fp8_max and the packed converters need no saturation
   const float wmax = (float)Elem<W>::load(Elem<W>::store(1e30f));  // saturating encode: the type's max
   const float head = IsFp8<W>::e4m3 ? 1.0625f : 1.125f;
-  *s_out = (g > 0.0f && g < 3.0e38f) ? wmax / ((float)c.nranks * g * head) : 1.0f;
+  float sc = (g > 0.0f && g < 3.0e38f) ? wmax / ((float)c.nranks * g * head) : 1.0f;
+  // a power of two (round down: the sum still cannot saturate): x * s and x / (1 / s) are then exact, which
+  // is what lets the scaled converts (e8m0 semantics, sq_group / dq_group) replace decode -> scale -> encode
+  // bit for bit; fp8 keeps its relative precision, at most one binade of range goes unused
+  sc = fminf(fmaxf(sc, 0x1p-120f), 0x1p+120f);
+  *s_out = __uint_as_float(__float_as_uint(sc) & 0x7f800000u);
   return __all(ok) != 0;
 }
 

@@ -251,7 +251,9 @@ def test_group_fp8_wire_fused_scale(cuda, groups, n, dtype, op):
     g = torch.Generator(device=cuda).manual_seed(31 + n)
     xs = [(torch.randn(1000003, device=cuda, generator=g) * (r + 1)).to(dtype) for r in range(n)]
     amax = max(float(x.float().abs().max()) for x in xs)
-    s = 448.0 / (n * amax * 1.0625)  # e4m3 headroom (device_exec.hpp fp8_scale): the sum never saturates
+    from allreduce_over_mpi_amd.ops.quant import fp8_wire_scale
+
+    s = fp8_wire_scale(n, amax)  # the device's pre-scale (device_exec.hpp fp8_scale): the sum never saturates
     want = _emulate_fp8_flat(xs, s, op)
     ref = torch.stack([x.double() for x in xs]).sum(0) / (n if op == "avg" else 1)
     for _ in range(3):  # parities; the amax granules are epoch-tagged
@@ -550,7 +552,9 @@ def test_group_fp8_wire_large_slices(cuda, groups, dtype):
     g = torch.Generator(device=cuda).manual_seed(77)
     xs = [(torch.randn(8 * 1024 * 1024 + 333, device=cuda, generator=g) * (r + 1)).to(dtype) for r in range(n)]
     amax = max(float(x.float().abs().max()) for x in xs)
-    s = 448.0 / (n * amax * 1.0625)
+    from allreduce_over_mpi_amd.ops.quant import fp8_wire_scale
+
+    s = fp8_wire_scale(n, amax)
     want = _emulate_fp8_flat(xs, s, "avg")
     for _ in range(2):
         outs = grp.all_reduce_fp8([x.clone() for x in xs], op="avg")

@@ -159,7 +159,9 @@ def _worker(rank, world, port, shared, q, transport="rccl", no_ipc=False, parts=
             for dtype, op in ((torch.float32, "avg"), (torch.bfloat16, "avg"), (torch.float32, "sum")):
                 xs = [x * (r + 1) for r, x in enumerate(inputs(big, 5, dtype))]
                 amax = max(float(x.float().abs().max()) for x in xs)
-                s = 448.0 / (world * amax * 1.0625)  # e4m3 headroom (device_exec.hpp fp8_scale)
+                from allreduce_over_mpi_amd.ops.quant import fp8_wire_scale
+
+                s = fp8_wire_scale(world, amax)  # the device's pre-scale (device_exec.hpp fp8_scale)
                 want = _emulate_fp8_flat(xs, s, op)
                 ref = torch.stack([x.double() for x in xs]).sum(0) / (world if op == "avg" else 1)
                 for _ in range(3):
