@@ -4,6 +4,7 @@ every rank uses device 0 (IPC between processes on one device exercises the
 same handle exchange, mapping and system-scope flag protocol as xGMI peers).
 """
 import os
+import time
 import socket
 
 import pytest
@@ -757,6 +758,7 @@ def _rebuild_worker(rank, world, port, cycles, q):
                 if not torch.equal(y[:m], want):
                     bad.append((cyc, spec))
             comm.check()
+            time.sleep(((rank * 7 + cyc * 3) % 5) * 0.006)  # ranks reach the collective teardown at different times
             comm.close()  # collective in the library: no caller barrier before the next communicator
         dist.destroy_process_group()
         q.put((rank, bad, None))
@@ -768,19 +770,21 @@ def _rebuild_worker(rank, world, port, cycles, q):
 
 @pytest.mark.skipif(not os.environ.get("FLEXAR_SOAK"), reason="soak run: FLEXAR_SOAK (scripts/gpu_soak.sh)")
 @pytest.mark.timeout(600)
-def test_ipc_communicator_rebuild_cycles(cuda):
-    """20 communicator rebuilds over the same registered buffers (close -> fresh communicator -> register the
-    same allocations -> zero-copy and staging allreduces), every result exact."""
+@pytest.mark.parametrize("world,cycles", [(2, 20), (4, 10)])
+def test_ipc_communicator_rebuild_cycles(cuda, world, cycles):
+    """Communicator rebuilds over the same registered buffers (close -> fresh communicator -> register the
+    same allocations -> zero-copy and staging allreduces), ranks closing at staggered times with no caller
+    barrier (the teardown agrees by itself), every result exact."""
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rebuild_worker, args=(r, 2, port, 20, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rebuild_worker, args=(r, world, port, cycles, q)) for r in range(world)]
     for p in procs:
         p.start()
     try:
-        res = [q.get(timeout=500) for _ in range(2)]
+        res = [q.get(timeout=500) for _ in range(world)]
     finally:
         for p in procs:
             p.join(timeout=60)
