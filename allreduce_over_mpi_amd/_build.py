@@ -128,7 +128,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
     objs = [o for o in objs if o]
     nproc = max(1, min(max(1, len(jobs)), int(os.environ.get("MAX_JOBS", "8"))))
     # the slowest translation units first: the typed executors dominate the build
-    jobs.sort(key=lambda j: 0 if "k_mx_" in j[-3] else 1)
+    jobs.sort(key=lambda j: 0 if "k_mx" in j[-3] else 1)
     with cf.ThreadPoolExecutor(nproc) as ex:
         for out in ex.map(_run, jobs):
             if verbose and out.strip():

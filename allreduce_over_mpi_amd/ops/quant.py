@@ -71,3 +71,72 @@ def fp8_wire_scale(nranks: int, amax: float, wire: str = "e4m3") -> float:
     s = min(max(s, f(2.0 ** -120)), f(2.0 ** 120))
     bits = np.array([s], dtype=np.float32).view(np.uint32)[0] & np.uint32(0x7F800000)
     return float(np.array([bits], dtype=np.uint32).view(np.float32)[0])
+
+
+# ---- OCP MX block-scaled fp8 wire ("+mxe4m3" / "+mxe5m2", docs/DESIGN.md §9.2) --------------------------
+MX_BLOCK = 32
+_MX_EMAX = {"e4m3": 8, "e5m2": 15}
+
+
+def mx_scale_bytes(x, wire: str = "e4m3"):
+    """e8m0 scale byte of every 32-element block of the fp32 tensor ``x`` (1-D, any length; the last block may
+    be partial) - types.hpp mx_scale_byte: 2^X with X the smallest exponent such that max|x| <= fp8_max * 2^X,
+    as X + 127 clamped to [1, 254]. The maximum is taken over sign-cleared f32 bits (NaN / inf count as largest)."""
+    import torch
+
+    n = x.numel()
+    pad = (-n) % MX_BLOCK
+    bits = x.float().contiguous().view(torch.int32).to(torch.int64) & 0x7FFFFFFF
+    if pad:
+        bits = torch.cat([bits, torch.zeros(pad, dtype=torch.int64)])
+    am = bits.view(-1, MX_BLOCK).amax(1)
+    e = (am >> 23) - _MX_EMAX[wire] + ((am & 0x7FFFFF) > 0x600000).to(torch.int64)
+    return e.clamp(1, 254)
+
+
+def mx_quantize(x, wire: str = "e4m3"):
+    """(q, scale bytes): the fp8 values q = rne(x / 2^X) of every block of the fp32 tensor ``x`` and the blocks'
+    e8m0 bytes - what the MX executor puts on the wire."""
+    import torch
+
+    sb = mx_scale_bytes(x, wire)
+    sc = torch.pow(2.0, (sb - 127).double()).float().repeat_interleave(MX_BLOCK)[: x.numel()]
+    fp8 = torch.float8_e4m3fn if wire == "e4m3" else torch.float8_e5m2
+    return (x.float() / sc).to(fp8), sb
+
+
+def mx_round(x, wire: str = "e4m3"):
+    """x rounded through the MX wire: q * 2^X per block, fp32."""
+    import torch
+
+    q, sb = mx_quantize(x, wire)
+    sc = torch.pow(2.0, (sb - 127).double()).float().repeat_interleave(MX_BLOCK)[: x.numel()]
+    return q.float() * sc
+
+
+def mx_allreduce_reference(inputs, wire: str = "e4m3", op: str = "sum"):
+    """What the flat MX-wire allreduce computes (device_exec.hpp xfer_mxb, host_exec.hpp host_xfer_mxb), on CPU
+    tensors of one float dtype: the count splits into N chunks of whole 256-element granules; the owner c of
+    chunk c sums its own contribution and those of ranks c+1, c+2, ... (mod N) in fp32 - each rounded through
+    MX with its sender's block scales - applies AVG's 1/N, rounds the sum through MX (the result's own block
+    scales) and every rank gets that value in the input dtype."""
+    import torch
+
+    n = len(inputs)
+    dt = inputs[0].dtype
+    count = inputs[0].numel()
+    split = (-(-count // n) + 255) // 256 * 256
+    out = torch.empty(count, dtype=torch.float32)
+    for c in range(n):
+        lo, hi = min(count, c * split), min(count, (c + 1) * split)
+        if hi <= lo:
+            continue
+        acc = None
+        for k in range(n):
+            src = (c + k) % n
+            v = mx_round(inputs[src].reshape(-1)[lo:hi].float(), wire)
+            acc = v if acc is None else acc + v
+        if op == "avg":
+            acc = acc * torch.tensor(1.0 / n, dtype=torch.float32)
+        out[lo:hi] = mx_round(acc, wire)
+    return out.to(dt)

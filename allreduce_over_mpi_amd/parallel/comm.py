@@ -628,9 +628,13 @@ class Communicator:
         config #5): one amax pass (``fp8_amax``, 256 per-workgroup partials, device-resident), then ONE
         executor launch that derives the pre-scale s = fp8_max / (N * global amax) from every rank's amax,
         quantises each contribution with it inside the first transfer, sums in fp32 and writes the result
-        / s in the tensor's dtype inside the last. All ranks get identical results. In place unless ``out``."""
+        / s in the tensor's dtype inside the last. All ranks get identical results. In place unless ``out``.
+        ``wire="mx_e4m3"`` / ``"mx_e5m2"``: the OCP MX form - one e8m0 scale per 32-element block, computed in
+        the same single launch, so no amax pass (docs/DESIGN.md §9.2)."""
         from ..ops.quant import fp8_amax
 
+        if wire in ("mx_e4m3", "mx_e5m2"):  # OCP MX block scales: computed inside the executor, no amax pass
+            return self.all_reduce(tensor, op, out=out, algo=(algo or "flat+pull") + "+mx" + wire[3:], stream=stream)
         _require_cuda(tensor)
         dst = tensor if out is None else out
         if out is not None:
@@ -809,6 +813,8 @@ class LocalGroup:
         """fp8-wire allreduce of every rank of the group in one launch (see Communicator.all_reduce_fp8)."""
         from ..ops.quant import fp8_amax
 
+        if wire in ("mx_e4m3", "mx_e5m2"):
+            return self.all_reduce(tensors, op, outs=outs, algo="flat+pull+mx" + wire[3:], stream=stream)
         outs = list(tensors) if outs is None else list(outs)
         parts = [fp8_amax(t, stream=stream) for t in tensors]
         ins = (ctypes.c_void_p * self.nranks)(*[t.data_ptr() for t in tensors])

@@ -128,7 +128,9 @@ int flexar_allreduce_ex(flexar_comm_t comm, const void* sendbuf, void* recvbuf, 
  * links. amax_parts: FLEXAR_AMAX_PARTIALS device floats from flexar_amax(sendbuf) on the same stream; the
  * pre-scale fp8_max / (N * global amax) and the post-scale are fused into the flat schedule's transfers
  * (every contribution and every result is rounded to fp8 once; all ranks get identical results).
- * op: SUM or AVG. algo: NULL = "flat+pull"; "+wt" selects the write-through protocol. */
+ * op: SUM or AVG. algo: NULL = "flat+pull"; "+wt" selects the write-through protocol.
+ * The OCP MX form needs no amax pass: flexar_allreduce_ex with algo "flat+mxe4m3" / "flat+mxe5m2" (one
+ * e8m0 scale per 32-element block, computed inside the executor; docs/DESIGN.md §9.2). */
 int flexar_allreduce_fp8(flexar_comm_t comm, const void* sendbuf, void* recvbuf, size_t count, int dtype, int op,
                          void* hip_stream, int wire_dtype, const float* amax_parts, const char* algo);
 /* Reduce-scatter: sendbuf holds nranks blocks of `count` elements, recvbuf receives this rank's
@@ -271,7 +273,8 @@ void* flexar_device_alloc(size_t bytes);
 void flexar_device_free(void* p);
 
 /* Kernel facts for a (dtype, op) instantiation: kind 0 = executor (proto 0 fence, 1 +nts, 2 +wt),
- * 1 = LL, 2 = standalone reduce, 3/4/5 = typed executor with fp32 partials / e4m3 wire / e5m2 wire.
+ * 1 = LL, 2 = standalone reduce, 3/4/5 = typed executor with fp32 partials / e4m3 wire / e5m2 wire,
+ * 6/7 = typed executor with an OCP MX block-scaled e4m3 / e5m2 wire.
  * Writes workgroups resident per CU (512 threads) and VGPRs. */
 int flexar_kernel_info(int dtype, int op, int kind, int proto, int* blocks_per_cu, int* vgprs);
 
@@ -334,8 +337,9 @@ int flexar_simulate_coll(int coll, const char* spec, int nranks, size_t count, i
                          const void* const* inputs, void* const* outputs, int grid, int ncalls, float scale);
 int flexar_simulate(const char* spec, int nranks, size_t count, int dtype, int op, const void* const* inputs,
                     void* const* outputs, int grid, int ncalls, int in_place, float scale);
-/* Typed-staging programs (spec suffix "+f32", "+e4m3", "+e5m2"; float dtype, SUM/AVG) with the fp8
- * pre-scale `pre` given explicitly (the device derives it from the global amax). */
+/* Typed-staging programs (spec suffix "+f32", "+e4m3", "+e5m2", "+mxe4m3", "+mxe5m2"; float dtype, SUM/AVG)
+ * with the fp8 pre-scale `pre` given explicitly (the device derives it from the global amax; the MX wire
+ * modes have per-block scales and ignore it). */
 int flexar_simulate_typed(const char* spec, int nranks, size_t count, int dtype, int op, const void* const* inputs,
                           void* const* outputs, int grid, int ncalls, float scale, float pre);
 /* Message-transport plans (msg_plan.hpp: the schedule as local executor segments + grouped send/recv,

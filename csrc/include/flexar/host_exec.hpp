@@ -15,6 +15,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <thread>
@@ -110,6 +111,83 @@ inline void host_xfer_typed(int wire, const Op& o, char* const* src, char* const
   }
 }
 
+// MX wire (Program::wire 4 = e4m3, 5 = e5m2): one typed XFER in OCP MX form over a slice that starts on a
+// block boundary, block by block - the device's xfer_mxb, bit for bit (docs/DESIGN.md §9.2):
+//   quantising push (K = 1, dtype source): y = x * scale; the block's scale 2^X from max |y|
+//     (mx_scale_byte); q = rne(y / 2^X); wire destinations get q and the scale byte, dtype ones q * 2^X;
+//   dequantising all-gather (K = 1, wire source): y = q * 2^X * scale into dtype destinations;
+//   reduction (K >= 2, own dtype value first): the own value rounded through MX with its own block scale,
+//     each peer's q * 2^X, summed in source order, times scale; with a wire destination the sum is
+//     quantised again (its own block scale) and every destination gets that value.
+inline uint32_t mx_mag_bits(float v) { return f2u(v) & 0x7fffffffu; }
+inline uint8_t mx_q(bool e4, float v) { return e4 ? f32_to_e4m3(v) : f32_to_e5m2(v); }
+inline float mx_dq(bool e4, uint8_t q) { return e4 ? e4m3_to_f32(q) : e5m2_to_f32(q); }
+
+template <typename T>
+inline void host_xfer_mxb(int wire, const Op& o, char* const* src, const uint8_t* const* ssc, char* const* dst,
+                          uint8_t* const* dsc, uint64_t n) {
+  const bool e4 = wire == 4;
+  const uint16_t sm = o.pad16[0], dm = o.pad16[1];
+  const int K = o.nsrc;
+  auto ld = [&](int k, uint64_t i) { return (float)Elem<T>::load(reinterpret_cast<const T*>(src[k])[i]); };
+  for (uint64_t b0 = 0; b0 < n; b0 += kMxBlock) {
+    const uint64_t m = n - b0 < kMxBlock ? n - b0 : kMxBlock, blk = b0 / kMxBlock;
+    float y[kMxBlock];
+    uint8_t q[kMxBlock];
+    uint32_t xr = 0;
+    if (K == 1 && !(sm & 1u)) {
+      uint32_t am = 0;
+      for (uint64_t i = 0; i < m; ++i) {
+        y[i] = ld(0, b0 + i) * o.scale;
+        am = std::max(am, mx_mag_bits(y[i]));
+      }
+      xr = mx_scale_byte(am, e4);
+    } else if (K == 1) {
+      const float sc = mx_scale_value(ssc[0][blk]);
+      for (uint64_t i = 0; i < m; ++i) y[i] = mx_dq(e4, (uint8_t)src[0][b0 + i]) * sc * o.scale;
+    } else {
+      for (int k = 0; k < K; ++k) {
+        float v[kMxBlock];
+        if (sm & (1u << k)) {
+          const float sc = mx_scale_value(ssc[k][blk]);
+          for (uint64_t i = 0; i < m; ++i) v[i] = mx_dq(e4, (uint8_t)src[k][b0 + i]) * sc;
+        } else {
+          uint32_t am = 0;
+          for (uint64_t i = 0; i < m; ++i) {
+            v[i] = ld(k, b0 + i);
+            am = std::max(am, mx_mag_bits(v[i]));
+          }
+          const float sc = mx_scale_value(mx_scale_byte(am, e4));
+          for (uint64_t i = 0; i < m; ++i) v[i] = mx_dq(e4, mx_q(e4, v[i] / sc)) * sc;
+        }
+        for (uint64_t i = 0; i < m; ++i) y[i] = k ? y[i] + v[i] : v[i];
+      }
+      uint32_t am = 0;
+      for (uint64_t i = 0; i < m; ++i) {
+        y[i] *= o.scale;
+        am = std::max(am, mx_mag_bits(y[i]));
+      }
+      if (dm) xr = mx_scale_byte(am, e4);
+    }
+    if (xr) {
+      const float sc = mx_scale_value(xr);
+      for (uint64_t i = 0; i < m; ++i) {
+        q[i] = mx_q(e4, y[i] / sc);
+        y[i] = mx_dq(e4, q[i]) * sc;
+      }
+    }
+    for (int d = 0; d < o.ndst; ++d) {
+      if (dm & (1u << d)) {
+        memcpy(dst[d] + b0, q, m);
+        dsc[d][blk] = (uint8_t)xr;
+      } else {
+        for (uint64_t i = 0; i < m; ++i)
+          reinterpret_cast<T*>(dst[d])[b0 + i] = Elem<T>::store((typename Elem<T>::acc)y[i]);
+      }
+    }
+  }
+}
+
 template <typename T, typename OP>
 struct HostExec {
   // Returns 0, or FLEXAR_ERR_TIMEOUT if a WAIT exceeded the timeout.
@@ -119,7 +197,7 @@ struct HostExec {
     const uint32_t nb = (grid - ch + nchan - 1) / nchan;
     const uint32_t unit = P.stg_unit();
     // slice boundaries keep every operand 16-B aligned: 16 bytes of the narrowest operand type
-    const uint32_t quantum = unit >= 16 ? 1 : (uint32_t)(16 / (P.wire ? unit : sizeof(T)));
+    const uint32_t quantum = P.wire >= 4 ? kMxBlock : unit >= 16 ? 1 : (uint32_t)(16 / (P.wire ? unit : sizeof(T)));
     const uint64_t par = (epoch & 1) ? c.stg_half_bytes : 0;
     auto addr = [&](const Loc& l) -> char* {
       if (l.buf == BUF_STG) return c.peer_stg[l.rank] + par + l.off * unit;
@@ -141,6 +219,18 @@ struct HostExec {
             char* dp[kMaxDst];
             for (int q = 0; q < o.nsrc; ++q) sp[q] = addr(o.src[q]) + lo * esz(o.src[q]);
             for (int q = 0; q < o.ndst; ++q) dp[q] = addr(o.dst[q]) + lo * esz(o.dst[q]);
+            if (P.wire >= 4) {  // block scales: the shadow byte of each wire operand's first block
+              auto sc = [&](const Loc& l) -> uint8_t* {
+                return (l.pad & 1) ? (uint8_t*)c.peer_stg[l.rank] + par + P.mx_shadow * unit + (l.off * unit + lo) / kMxBlock
+                                   : nullptr;
+              };
+              const uint8_t* ss[kMaxSrc];
+              uint8_t* ds[kMaxDst];
+              for (int q = 0; q < o.nsrc; ++q) ss[q] = sc(o.src[q]);
+              for (int q = 0; q < o.ndst; ++q) ds[q] = sc(o.dst[q]);
+              host_xfer_mxb<T>(P.wire, o, sp, ss, dp, ds, hi - lo);
+              continue;
+            }
             host_xfer_typed<T>(P.wire, o, sp, dp, hi - lo, c.pre, c.post_inv);
             continue;
           }

@@ -48,6 +48,9 @@ struct Program {
   int wire = 0;
   uint32_t wsize = 0;
   uint32_t unit = 0;
+  // MX wire (wire 4 / 5): the e8m0 scale of the 32-element block of a wire operand at staging byte o lives
+  // at byte mx_shadow + o / 32 of the same rank's staging half (offset units; 0 = no shadow)
+  uint64_t mx_shadow = 0;
   // zero-copy program (AlgoSpec::zc): IN / OUT operands of other ranks address their registered buffers;
   // zc_bufs = which of them the program addresses on a peer (bit BUF_IN, bit BUF_OUT)
   bool zc = false;
@@ -155,6 +158,10 @@ class Planner {
     } else {
       if (err) *err = "planner needs a concrete algorithm (not auto)";
       return false;
+    }
+    if (wire >= 4 && N > 1) {  // MX scale shadow: one byte per 32 staging bytes, after the payload
+      P->mx_shadow = round_up(stg);
+      stg = P->mx_shadow + round_up((stg + kMxBlock - 1) / kMxBlock);
     }
     P->stg_elems = stg;
     P->nchan = (uint32_t)P->chan_start.size() - 1;
@@ -294,7 +301,7 @@ class Planner {
   // operands stay in elements of the call's dtype.
   bool set_wire(const AlgoSpec& spec, std::string* err) {
     wire = spec.wire;
-    if (wire < 0 || wire > 3) { if (err) *err = "bad wire type"; return false; }
+    if (wire < 0 || wire > 5) { if (err) *err = "bad wire type"; return false; }
     if (wire == 1 && esize >= 4) wire = 0;  // fp32 (or wider) partials already: nothing to widen
     wsize = wire == 1 ? 4u : (wire >= 2 ? 1u : esize);
     if (wire >= 2 && esize < 2) { if (err) *err = "fp8 wire compression needs a 16/32-bit float input"; return false; }
@@ -1053,6 +1060,8 @@ inline bool typed_pattern_ok(const Program& P, const Op& o) {
   const uint32_t all_s = (1u << o.nsrc) - 1, all_d = (1u << o.ndst) - 1;
   const bool fp8 = P.wire >= 2;
   const int K = o.nsrc;
+  // MX wire: a wire-to-wire copy would have to carry the block scales too (the flat schedule has none)
+  if (P.wire >= 4 && sm == all_s && dm) return false;
   if (sm == all_s && dm == all_d) return true;  // wire type throughout
   if (!fp8 && sm == 0 && dm == 0) return true;  // dtype throughout
   if (sm == 0) return fp8 ? K == 1 : K >= 2;
@@ -1112,7 +1121,9 @@ inline std::string dump_program(const Program& P, uint32_t rank) {
   std::ostringstream ss;
   ss << "rank " << rank << " program '" << P.desc << "': " << P.ops.size() << " ops, " << P.nchan
      << " channel(s), staging " << P.stg_elems << " elems/parity, " << P.nslots << " flag slots";
-  if (P.wire) ss << ", wire type " << (P.wire == 1 ? "fp32" : P.wire == 2 ? "e4m3" : "e5m2") << " ('~'), unit " << P.unit << " B";
+  static const char* wn[] = {"", "fp32", "e4m3", "e5m2", "mx e4m3", "mx e5m2"};
+  if (P.wire) ss << ", wire type " << wn[P.wire] << " ('~'), unit " << P.unit << " B";
+  if (P.mx_shadow) ss << ", block scales at " << P.mx_shadow;
   ss << "\n";
   for (uint32_t c = 0; c < P.nchan; ++c) {
     ss << "channel " << c << ":\n";

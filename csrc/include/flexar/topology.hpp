@@ -43,7 +43,8 @@ struct AlgoSpec {
   // Typed staging (planner.hpp "typed operands"): WIRE_ACC keeps the partial sums of multi-hop schedules
   // (ring, multi-stage trees) in fp32 staging so a 16/8-bit allreduce rounds once, like flat; WIRE_E4M3 /
   // WIRE_E5M2 carry a wider dtype over the links as fp8 with a per-call pre-scale from the global amax
-  // (flat schedule only: one quantisation per contribution, one per result). round_wire ("+rw") opts a
+  // (flat schedule only: one quantisation per contribution, one per result); WIRE_MXE4M3 / WIRE_MXE5M2
+  // the same schedule in OCP MX form, a scale per 32-element block and no amax pass. round_wire ("+rw") opts a
   // multi-hop 16/8-bit schedule out of the fp32 staging default.
   int wire = 0;
   bool round_wire = false;
@@ -85,6 +86,8 @@ struct AlgoSpec {
     if (wire == 1) ss << "+f32";
     if (wire == 2) ss << "+e4m3";
     if (wire == 3) ss << "+e5m2";
+    if (wire == 4) ss << "+mxe4m3";
+    if (wire == 5) ss << "+mxe5m2";
     if (round_wire) ss << "+rw";
     if (msg) ss << "+rccl";
     if (zc) ss << "+zc";
@@ -215,6 +218,8 @@ inline bool parse_algo(const std::string& raw, int nranks, AlgoSpec* spec, std::
     else if (mod == "f32") spec->wire = 1;
     else if (mod == "e4m3" || mod == "fp8") spec->wire = 2;
     else if (mod == "e5m2") spec->wire = 3;
+    else if (mod == "mxe4m3" || mod == "mxfp8") spec->wire = 4;
+    else if (mod == "mxe5m2") spec->wire = 5;
     else if (mod == "rw") spec->round_wire = true;
     else if (mod == "rccl" || mod == "msg") spec->msg = true;
     else if (mod == "zc") spec->zc = true;

@@ -28,6 +28,11 @@ struct bf16_t { uint16_t bits; };
 struct f16_t { uint16_t bits; };
 struct fp8e4m3_t { uint8_t bits; };
 struct fp8e5m2_t { uint8_t bits; };
+// OCP MX block-scaled fp8 on the links (AlgoSpec::wire 4 / 5, "+mxe4m3" / "+mxe5m2"): the element bits
+// are those of fp8e4m3_t / fp8e5m2_t, and every kMxBlock consecutive elements share one e8m0 scale byte
+// (device_exec.hpp xfer_mxb, host_exec.hpp host_xfer_mxb). Distinct types select the block-scaled executor.
+struct mxe4m3_t { uint8_t bits; };
+struct mxe5m2_t { uint8_t bits; };
 
 FX_HD FX_INLINE uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
 FX_HD FX_INLINE float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
@@ -210,6 +215,32 @@ template <> struct Elem<fp8e5m2_t> {
   FX_HD static FX_INLINE acc load(fp8e5m2_t v) { return e5m2_to_f32(v.bits); }
   FX_HD static FX_INLINE fp8e5m2_t store(acc v) { return fp8e5m2_t{f32_to_e5m2(v)}; }
 };
+template <> struct Elem<mxe4m3_t> {
+  using acc = float;
+  static constexpr bool is_float = true;
+  FX_HD static FX_INLINE acc load(mxe4m3_t v) { return e4m3_to_f32(v.bits); }
+  FX_HD static FX_INLINE mxe4m3_t store(acc v) { return mxe4m3_t{f32_to_e4m3(v)}; }
+};
+template <> struct Elem<mxe5m2_t> {
+  using acc = float;
+  static constexpr bool is_float = true;
+  FX_HD static FX_INLINE acc load(mxe5m2_t v) { return e5m2_to_f32(v.bits); }
+  FX_HD static FX_INLINE mxe5m2_t store(acc v) { return mxe5m2_t{f32_to_e5m2(v)}; }
+};
+
+// ---- OCP MX block scales (e8m0) -------------------------------------------
+// A block's scale is 2^X with X the smallest exponent such that amax <= fp8_max * 2^X, fp8_max = 1.75 *
+// 2^emax (e4m3: 448, emax 8; e5m2: 57344, emax 15): every element / 2^X is then within the fp8 range, so
+// the quantisation never saturates (the gfx950 scaled converts turn an overflow into NaN) and the largest
+// element keeps fp8's full relative precision. `amax_bits` = the f32 bits of the block's largest
+// magnitude, taken as an unsigned maximum over sign-cleared bits (NaN and inf count as the largest);
+// returned: the biased e8m0 byte X + 127, clamped to [1, 254] (a normal f32 scale).
+constexpr uint32_t kMxBlock = 32;
+FX_HD FX_INLINE uint32_t mx_scale_byte(uint32_t amax_bits, bool e4m3) {
+  const int e = (int)(amax_bits >> 23) - (e4m3 ? 8 : 15) + ((amax_bits & 0x7fffffu) > 0x600000u ? 1 : 0);
+  return (uint32_t)(e < 1 ? 1 : (e > 254 ? 254 : e));
+}
+FX_HD FX_INLINE float mx_scale_value(uint32_t byte) { return u2f(byte << 23); }
 
 // ---- reduction functors (operate on the accumulator type) ---------------------
 // Integer SUM/PROD wrap (computed in the unsigned domain: no signed-overflow UB).

@@ -82,8 +82,19 @@ int resolve_spec(flexar_comm* c, const char* algo, double bytes, AlgoSpec* out, 
 // Typed staging for an allreduce schedule (AlgoSpec::wire): multi-hop schedules of 16/8-bit float dtypes
 // keep fp32 partials or round per hop by the communicator's partials policy (cost_model.hpp
 // apply_partials, FLEXAR_PARTIALS; "+f32" / "+rw" in the spec win); fp8 wire modes need
-// flexar_allreduce_fp8 (the amax partials). Other ops / schedules run untyped.
+// flexar_allreduce_fp8 (the amax partials); the MX wire ("+mxe4m3" / "+mxe5m2") runs from any allreduce
+// entry. Other ops / schedules run untyped.
 int typed_spec(flexar_comm* c, AlgoSpec* s, int dtype, int op, bool have_amax, double bytes) {
+  if (s->wire >= 2 && c->nranks == 1) {  // one rank: the executor's copy, nothing crosses a link
+    s->wire = 0;
+    return 0;
+  }
+  if (s->wire >= 2 && (!(dtype == FLEXAR_FLOAT32 || dtype == FLEXAR_BFLOAT16 || dtype == FLEXAR_FLOAT16) ||
+                       (op != FLEXAR_SUM && op != FLEXAR_AVG))) {
+    set_error("fp8 wire compression (" + s->str() + ") takes fp32 / bf16 / fp16 buffers with SUM / AVG");
+    return FLEXAR_ERR_UNSUPPORTED;
+  }
+  if (s->wire >= 4) return 0;  // MX wire: block scales computed inside the executor, no amax pass
   if (s->wire >= 2) {
     if (!have_amax) {
       set_error("fp8 wire compression (" + s->str() + ") needs the amax partials: use flexar_allreduce_fp8");
@@ -247,6 +258,7 @@ void fill_ctx(flexar_comm* c, DevProgram* dp, const void* in, void* out, DevCtx*
   }
   x->ll_off = c->exec_half + kAmaxRegion;
   x->amax_off = c->exec_half;
+  x->mx_shadow = dp ? dp->prog.mx_shadow * dp->prog.stg_unit() : 0;
   x->stg_unit = dp ? dp->prog.stg_unit() : 0;
   x->nranks = c->nranks;
   x->rank = c->rank;
@@ -809,11 +821,12 @@ void* flexar_device_alloc(size_t bytes) {
 void flexar_device_free(void* p) { (void)hipFree(p); }
 
 int flexar_kernel_info(int dtype, int op, int kind, int proto, int* blocks_per_cu, int* vgprs) {
-  if (kind < 0 || kind > 5 || proto < 0 || proto > 2) { set_error("bad kernel_info arguments"); return FLEXAR_ERR_INVALID; }
+  if (kind < 0 || kind > 7 || proto < 0 || proto > 2) { set_error("bad kernel_info arguments"); return FLEXAR_ERR_INVALID; }
   LaunchArgs la;
   la.kind = LAUNCH_QUERY;
   la.query = kind > 2 ? 0 : kind;
-  la.wire = kind > 2 ? kind - 2 : 0;  // typed executors: 3 = fp32 partials, 4 = e4m3 wire, 5 = e5m2 wire
+  // typed executors: 3 = fp32 partials, 4 / 5 = e4m3 / e5m2 wire, 6 / 7 = MX e4m3 / e5m2 wire
+  la.wire = kind > 2 ? kind - 2 : 0;
   la.proto = proto;
   la.occ_out = blocks_per_cu;
   la.regs_out = vgprs;

@@ -57,6 +57,7 @@ struct DevCtx {
   uint32_t stg_unit;
   const float* amax_parts;  // FLEXAR_AMAX_PARTIALS per-workgroup max |x| of this rank's input
   uint64_t amax_off;        // byte offset of the amax granule slots in each staging parity half
+  uint64_t mx_shadow;       // MX wire: byte offset of the block-scale shadow in each staging parity half
 };
 constexpr uint32_t kAmaxParts = 256;    // == FLEXAR_AMAX_PARTIALS
 constexpr uint64_t kAmaxRegion = 256;   // bytes reserved per parity half for the amax granules
@@ -445,14 +446,21 @@ typedef short fx_s2 __attribute__((ext_vector_type(2)));
 typedef __bf16 fx_bf2 __attribute__((ext_vector_type(2)));
 typedef _Float16 fx_h2 __attribute__((ext_vector_type(2)));
 typedef float fx_f2 __attribute__((ext_vector_type(2)));
+template <> struct IsFp8<mxe4m3_t> { static constexpr bool value = true; static constexpr bool e4m3 = true; };
+template <> struct IsFp8<mxe5m2_t> { static constexpr bool value = true; static constexpr bool e4m3 = false; };
+template <typename S> struct IsMx { static constexpr bool value = false; };
+template <> struct IsMx<mxe4m3_t> { static constexpr bool value = true; };
+template <> struct IsMx<mxe5m2_t> { static constexpr bool value = true; };
 template <typename T> struct HasScaledCvt { static constexpr bool value = false; };
 template <> struct HasScaledCvt<float> { static constexpr bool value = true; };
 template <> struct HasScaledCvt<bf16_t> { static constexpr bool value = true; };
 template <> struct HasScaledCvt<f16_t> { static constexpr bool value = true; };
 
-// G values of T (packed in raw) -> G fp8 values (packed in out): q = rne(x / inv), inv a power of two
-template <typename T, typename W, int G>
-__device__ FX_INLINE void sq_group(const uint4* raw, float inv, uint4* out) {
+// G values of T (packed in raw) -> G fp8 values (packed in out): q = rne(x / inv), inv a power of two;
+// inv[r] applies to the run of RL elements r (RL = G: one scale for the group; MX blocks: one per run)
+template <typename T, typename W, int G, int RL = G>
+__device__ FX_INLINE void sq_group(const uint4* raw, const float* inv, uint4* out) {
+  static_assert(RL % 4 == 0 && G % RL == 0, "runs of whole 4-element words");
   constexpr bool E4 = IsFp8<W>::e4m3;
   uint32_t w[G / 4];
   if constexpr (std::is_same<T, float>::value) {
@@ -462,11 +470,11 @@ __device__ FX_INLINE void sq_group(const uint4* raw, float inv, uint4* out) {
     for (int i = 0; i < G / 4; ++i) {
       fx_s2 r = {0, 0};
       if constexpr (E4) {
-        r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(r, f[4 * i], f[4 * i + 1], inv, false);
-        r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(r, f[4 * i + 2], f[4 * i + 3], inv, true);
+        r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(r, f[4 * i], f[4 * i + 1], inv[4 * i / RL], false);
+        r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(r, f[4 * i + 2], f[4 * i + 3], inv[4 * i / RL], true);
       } else {
-        r = __builtin_amdgcn_cvt_scalef32_pk_bf8_f32(r, f[4 * i], f[4 * i + 1], inv, false);
-        r = __builtin_amdgcn_cvt_scalef32_pk_bf8_f32(r, f[4 * i + 2], f[4 * i + 3], inv, true);
+        r = __builtin_amdgcn_cvt_scalef32_pk_bf8_f32(r, f[4 * i], f[4 * i + 1], inv[4 * i / RL], false);
+        r = __builtin_amdgcn_cvt_scalef32_pk_bf8_f32(r, f[4 * i + 2], f[4 * i + 3], inv[4 * i / RL], true);
       }
       __builtin_memcpy(&w[i], &r, 4);
     }
@@ -481,22 +489,22 @@ __device__ FX_INLINE void sq_group(const uint4* raw, float inv, uint4* out) {
         __builtin_memcpy(&a, &p[2 * i], 4);
         __builtin_memcpy(&b, &p[2 * i + 1], 4);
         if constexpr (E4) {
-          r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, a, inv, false);
-          r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, b, inv, true);
+          r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, a, inv[4 * i / RL], false);
+          r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, b, inv[4 * i / RL], true);
         } else {
-          r = __builtin_amdgcn_cvt_scalef32_pk_bf8_bf16(r, a, inv, false);
-          r = __builtin_amdgcn_cvt_scalef32_pk_bf8_bf16(r, b, inv, true);
+          r = __builtin_amdgcn_cvt_scalef32_pk_bf8_bf16(r, a, inv[4 * i / RL], false);
+          r = __builtin_amdgcn_cvt_scalef32_pk_bf8_bf16(r, b, inv[4 * i / RL], true);
         }
       } else {
         fx_h2 a, b;
         __builtin_memcpy(&a, &p[2 * i], 4);
         __builtin_memcpy(&b, &p[2 * i + 1], 4);
         if constexpr (E4) {
-          r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(r, a, inv, false);
-          r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(r, b, inv, true);
+          r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(r, a, inv[4 * i / RL], false);
+          r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(r, b, inv[4 * i / RL], true);
         } else {
-          r = __builtin_amdgcn_cvt_scalef32_pk_bf8_f16(r, a, inv, false);
-          r = __builtin_amdgcn_cvt_scalef32_pk_bf8_f16(r, b, inv, true);
+          r = __builtin_amdgcn_cvt_scalef32_pk_bf8_f16(r, a, inv[4 * i / RL], false);
+          r = __builtin_amdgcn_cvt_scalef32_pk_bf8_f16(r, b, inv[4 * i / RL], true);
         }
       }
       __builtin_memcpy(&w[i], &r, 4);
@@ -506,8 +514,9 @@ __device__ FX_INLINE void sq_group(const uint4* raw, float inv, uint4* out) {
 }
 
 // G fp8 values (packed in raw) -> G values of T (packed in out): x = q * scale, scale a power of two
-template <typename T, typename W, int G>
-__device__ FX_INLINE void dq_group(const uint4* raw, float scale, uint4* out) {
+// (scale[r] for the run of RL elements r)
+template <typename T, typename W, int G, int RL = G>
+__device__ FX_INLINE void dq_group(const uint4* raw, const float* scale, uint4* out) {
   constexpr bool E4 = IsFp8<W>::e4m3;
   uint32_t w[G / 4];
   __builtin_memcpy(w, raw, sizeof(w));
@@ -517,11 +526,11 @@ __device__ FX_INLINE void dq_group(const uint4* raw, float scale, uint4* out) {
     for (int i = 0; i < G / 4; ++i) {
       fx_f2 lo, hi;
       if constexpr (E4) {
-        lo = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(w[i], scale, false);
-        hi = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(w[i], scale, true);
+        lo = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(w[i], scale[4 * i / RL], false);
+        hi = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(w[i], scale[4 * i / RL], true);
       } else {
-        lo = __builtin_amdgcn_cvt_scalef32_pk_f32_bf8(w[i], scale, false);
-        hi = __builtin_amdgcn_cvt_scalef32_pk_f32_bf8(w[i], scale, true);
+        lo = __builtin_amdgcn_cvt_scalef32_pk_f32_bf8(w[i], scale[4 * i / RL], false);
+        hi = __builtin_amdgcn_cvt_scalef32_pk_f32_bf8(w[i], scale[4 * i / RL], true);
       }
       f[4 * i] = lo.x; f[4 * i + 1] = lo.y; f[4 * i + 2] = hi.x; f[4 * i + 3] = hi.y;
     }
@@ -533,22 +542,22 @@ __device__ FX_INLINE void dq_group(const uint4* raw, float scale, uint4* out) {
       if constexpr (std::is_same<T, bf16_t>::value) {
         fx_bf2 lo, hi;
         if constexpr (E4) {
-          lo = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[i], scale, false);
-          hi = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[i], scale, true);
+          lo = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[i], scale[4 * i / RL], false);
+          hi = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[i], scale[4 * i / RL], true);
         } else {
-          lo = __builtin_amdgcn_cvt_scalef32_pk_bf16_bf8(w[i], scale, false);
-          hi = __builtin_amdgcn_cvt_scalef32_pk_bf16_bf8(w[i], scale, true);
+          lo = __builtin_amdgcn_cvt_scalef32_pk_bf16_bf8(w[i], scale[4 * i / RL], false);
+          hi = __builtin_amdgcn_cvt_scalef32_pk_bf16_bf8(w[i], scale[4 * i / RL], true);
         }
         __builtin_memcpy(&p[2 * i], &lo, 4);
         __builtin_memcpy(&p[2 * i + 1], &hi, 4);
       } else {
         fx_h2 lo, hi;
         if constexpr (E4) {
-          lo = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(w[i], scale, false);
-          hi = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(w[i], scale, true);
+          lo = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(w[i], scale[4 * i / RL], false);
+          hi = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(w[i], scale[4 * i / RL], true);
         } else {
-          lo = __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(w[i], scale, false);
-          hi = __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(w[i], scale, true);
+          lo = __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(w[i], scale[4 * i / RL], false);
+          hi = __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(w[i], scale[4 * i / RL], true);
         }
         __builtin_memcpy(&p[2 * i], &lo, 4);
         __builtin_memcpy(&p[2 * i + 1], &hi, 4);
@@ -662,7 +671,7 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
       } else if constexpr (SCV) {
         // every own contribution is the value the peers receive: fp8(x * pre), in one scaled convert
         uint4 q[VW > 0 ? VW : 1];
-        sq_group<T, W, G>(raw[k], post_inv, q);
+        sq_group<T, W, G>(raw[k], &post_inv, q);
         decode_g<W, G>(q, x);
       } else {
         decode_g<T, G>(raw[k], x);
@@ -684,8 +693,8 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
   // destination dd's G values, packed in its element type
   auto encode_dst = [&](int dd, const uint4 (&raw)[K][VM], const float (&acc)[G], uint4 (&y)[VM]) {
     if constexpr (SCV && K == 1) {
-      if (fast_push) return sq_group<T, W, G>(raw[0], post_inv, y);
-      if (fast_ag) return dq_group<T, W, G>(raw[0], post_inv, y);
+      if (fast_push) return sq_group<T, W, G>(raw[0], &post_inv, y);
+      if (fast_ag) return dq_group<T, W, G>(raw[0], &post_inv, y);
     }
     if ((dm >> dd) & 1) {
       encode_g<W, G, !FP8>(acc, y);  // fp8 wire values are in range: packed encode, no clamp
@@ -811,6 +820,347 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
   }
 }
 
+// ---- MX wire: OCP MX block-scaled fp8 (AlgoSpec::wire 4 / 5) ------------------------------------------
+// The flat schedule of the fp8 wire with a scale per 32-element block instead of one per call: no amax
+// pass and no amax agreement before the launch, and each block's scale follows its own magnitude (a
+// block of small gradients next to large ones keeps fp8's relative precision instead of flushing to zero).
+// The block scales of a staging operand live in the same rank's staging half at mx_shadow + byte / 32
+// (planner.hpp Program::mx_shadow). Semantics, element for element what host_exec.hpp host_xfer_mxb
+// computes (docs/DESIGN.md §9.2):
+//   quantising push (K = 1, SP_T): 2^X from the block's max |x * scale|, q = rne(x * scale / 2^X) (one
+//     scaled convert per element pair), q and the e8m0 byte to every wire destination;
+//   dequantising all-gather (K = 1, SP_W): q * 2^X * scale into dtype destinations;
+//   reduction (K >= 2, SP_TW): the own value rounded through MX with its own block scale, each peer's
+//     q * 2^X, summed in fp32 in source order, times scale, re-quantised with the sum's block scale for the
+//     wire destinations, and that value (q * 2^X) into the dtype ones.
+// A block's 32 elements sit in consecutive lanes of one wave (8 lanes x 4 for fp32 inputs, 4 x 8 for
+// 16-bit ones, 2 x 16 in the contiguous layout), so its maximum is a few cross-lane swaps.
+
+// per run of RL elements of a packed group of 16 values of T: the f32 bits of the largest magnitude (an
+// unsigned maximum of the sign-cleared bits, as mx_scale_byte expects)
+typedef unsigned short fx_u16x2 __attribute__((ext_vector_type(2)));
+template <typename T, int RL>
+__device__ FX_INLINE void mx_run_amax(const uint4* raw, uint32_t (&m)[16 / RL]) {
+  constexpr int R = 16 / RL;
+  if constexpr (std::is_same<T, float>::value) {
+    uint32_t w[16];
+    __builtin_memcpy(w, raw, sizeof(w));
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      uint32_t a = 0;
+#pragma unroll
+      for (int e = r * RL; e < (r + 1) * RL; ++e) a = max(a, w[e] & 0x7fffffffu);
+      m[r] = a;
+    }
+  } else {
+    uint32_t w[8];
+    __builtin_memcpy(w, raw, sizeof(w));
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      fx_u16x2 a = {0, 0};
+#pragma unroll
+      for (int i = r * RL / 2; i < (r + 1) * RL / 2; ++i)
+        a = __builtin_elementwise_max(a, __builtin_bit_cast(fx_u16x2, w[i] & 0x7fff7fffu));  // v_pk_max_u16
+      const uint16_t h = a.x > a.y ? a.x : a.y;
+      if constexpr (std::is_same<T, bf16_t>::value) m[r] = (uint32_t)h << 16;
+      else m[r] = __float_as_uint((float)__builtin_bit_cast(_Float16, h));
+    }
+  }
+}
+template <int RL>
+__device__ FX_INLINE void mx_run_amax_f(const float (&x)[16], uint32_t (&m)[16 / RL]) {
+#pragma unroll
+  for (int r = 0; r < 16 / RL; ++r) {
+    uint32_t a = 0;
+#pragma unroll
+    for (int e = r * RL; e < (r + 1) * RL; ++e) a = max(a, __float_as_uint(x[e]) & 0x7fffffffu);
+    m[r] = a;
+  }
+}
+// maximum over the LPB consecutive lanes that hold one block (LPB a power of two dividing 64)
+template <int LPB>
+__device__ FX_INLINE uint32_t mx_block_max(uint32_t m) {
+#pragma unroll
+  for (int o = 1; o < LPB; o <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+  return m;
+}
+
+// One lane's group of 16 elements in runs of RL (sb[k][r] = the scale byte of wire source k's block for
+// run r, loaded with the payload): the fp8 result `yq` with its block scale bytes `xb` (wire
+// destinations) and / or the dtype result `yt` (dtype destinations).
+template <typename T, typename W, int K, int SP, int RL>
+__device__ FX_INLINE void mx_group(const uint4 (&raw)[K][(int)sizeof(T)], const uint32_t (&sb)[K][16 / RL], float scale,
+                                   int nd, uint32_t dm, uint4& yq, uint32_t (&xb)[16 / RL], uint4 (&yt)[(int)sizeof(T)]) {
+  constexpr int R = 16 / RL, LPB = (int)kMxBlock / RL;
+  constexpr bool E4 = IsFp8<W>::e4m3;
+  const uint32_t all_d = (1u << nd) - 1;
+  float sc[R];
+  if constexpr (SP == SP_T) {
+    uint32_t m[R];
+    if (scale == 1.0f) {
+      mx_run_amax<T, RL>(raw[0], m);
+#pragma unroll
+      for (int r = 0; r < R; ++r) xb[r] = mx_scale_byte(mx_block_max<LPB>(m[r]), E4), sc[r] = mx_scale_value(xb[r]);
+      sq_group<T, W, 16, RL>(raw[0], sc, &yq);
+    } else {
+      float y[16];
+      decode_g<T, 16>(raw[0], y);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) y[e] *= scale;
+      mx_run_amax_f<RL>(y, m);
+#pragma unroll
+      for (int r = 0; r < R; ++r) xb[r] = mx_scale_byte(mx_block_max<LPB>(m[r]), E4), sc[r] = mx_scale_value(xb[r]);
+      uint4 t[4];
+      __builtin_memcpy(t, y, sizeof(y));
+      sq_group<float, W, 16, RL>(t, sc, &yq);
+    }
+    if (dm != all_d) dq_group<T, W, 16, RL>(&yq, sc, yt);
+  } else if constexpr (SP == SP_W) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) sc[r] = mx_scale_value(sb[0][r]);
+    if (scale == 1.0f) {
+      dq_group<T, W, 16, RL>(&raw[0][0], sc, yt);
+    } else {
+      uint4 t[4];
+      dq_group<float, W, 16, RL>(&raw[0][0], sc, t);
+      float y[16];
+      __builtin_memcpy(y, t, sizeof(y));
+#pragma unroll
+      for (int e = 0; e < 16; ++e) y[e] *= scale;
+      encode_g<T, 16>(y, yt);
+    }
+  } else {
+    float acc[16];
+    {  // the own contribution, rounded through MX with its own block scale (what a peer would receive)
+      uint32_t m[R];
+      mx_run_amax<T, RL>(raw[0], m);
+      float s0[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) s0[r] = mx_scale_value(mx_scale_byte(mx_block_max<LPB>(m[r]), E4));
+      uint4 q, t[4];
+      sq_group<T, W, 16, RL>(raw[0], s0, &q);
+      dq_group<float, W, 16, RL>(&q, s0, t);
+      __builtin_memcpy(acc, t, sizeof(acc));
+    }
+#pragma unroll
+    for (int k = 1; k < K; ++k) {
+      float sk[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) sk[r] = mx_scale_value(sb[k][r]);
+      uint4 t[4];
+      dq_group<float, W, 16, RL>(&raw[k][0], sk, t);
+      float x[16];
+      __builtin_memcpy(x, t, sizeof(x));
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] += x[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] *= scale;
+    if (dm) {
+      uint32_t m[R];
+      mx_run_amax_f<RL>(acc, m);
+#pragma unroll
+      for (int r = 0; r < R; ++r) xb[r] = mx_scale_byte(mx_block_max<LPB>(m[r]), E4), sc[r] = mx_scale_value(xb[r]);
+      uint4 t[4];
+      __builtin_memcpy(t, acc, sizeof(acc));
+      sq_group<float, W, 16, RL>(t, sc, &yq);
+      if (dm != all_d) dq_group<T, W, 16, RL>(&yq, sc, yt);
+    } else {
+      encode_g<T, 16>(acc, yt);
+    }
+  }
+}
+
+// One element of an MX operation by itself (the tail of a slice: fewer than 32 elements, or the whole
+// slice when a caller buffer takes no vector access): each thread recomputes its block's scale from the
+// block's elements, so it needs no other lane.
+template <typename T, typename W, int K, int SP, int PM>
+__device__ FX_INLINE void mx_elem(const char* const (&s)[kMaxSrc], const uint8_t* const (&ss)[kMaxSrc],
+                                  char* const (&d)[kMaxDst], uint8_t* const (&sd)[kMaxDst], int nd, uint32_t dm,
+                                  uint64_t n, float scale, uint64_t i) {
+  constexpr bool E4 = IsFp8<W>::e4m3;
+  const uint64_t b = i / kMxBlock, b0 = b * kMxBlock, b1 = b0 + kMxBlock < n ? b0 + kMxBlock : n;
+  auto own = [&](int k, uint64_t j) { return (float)Elem<T>::load(ld_elem<PM, T>(s[k], j)); };
+  auto wire = [&](int k, uint64_t j) {
+    return (float)Elem<W>::load(W{ld_elem<PM, uint8_t>(s[k], j)}) *
+           mx_scale_value(ld_elem<PM, uint8_t>(reinterpret_cast<const char*>(ss[k]), b));
+  };
+  float y;
+  uint32_t xr = 0;
+  if constexpr (SP == SP_T) {
+    uint32_t am = 0;
+    for (uint64_t j = b0; j < b1; ++j) am = max(am, __float_as_uint(own(0, j) * scale) & 0x7fffffffu);
+    xr = mx_scale_byte(am, E4);
+    y = own(0, i) * scale;
+  } else if constexpr (SP == SP_W) {
+    y = wire(0, i) * scale;
+  } else {
+    uint32_t am0 = 0;
+    for (uint64_t j = b0; j < b1; ++j) am0 = max(am0, __float_as_uint(own(0, j)) & 0x7fffffffu);
+    const float s0 = mx_scale_value(mx_scale_byte(am0, E4));
+    auto sum = [&](uint64_t j) {
+      float a = (float)Elem<W>::load(Elem<W>::store(own(0, j) / s0)) * s0;
+#pragma unroll
+      for (int k = 1; k < K; ++k) a += wire(k, j);
+      return a * scale;
+    };
+    y = sum(i);
+    if (dm) {
+      uint32_t am = 0;
+      for (uint64_t j = b0; j < b1; ++j) am = max(am, __float_as_uint(sum(j)) & 0x7fffffffu);
+      xr = mx_scale_byte(am, E4);
+    }
+  }
+  uint8_t q = 0;
+  if (xr) {
+    const float sc = mx_scale_value(xr);
+    q = Elem<W>::store(y / sc).bits;
+    y = (float)Elem<W>::load(W{q}) * sc;
+  }
+#pragma unroll
+  for (int dd = 0; dd < kMaxDst; ++dd) {
+    if (dd >= nd) continue;
+    if ((dm >> dd) & 1) {
+      st_elem<PM, uint8_t>(d[dd], i, q);
+      if (i == b0) st_elem<PM, uint8_t>(reinterpret_cast<char*>(sd[dd]), b, (uint8_t)xr);
+    } else {
+      st_elem<PM, T>(d[dd], i, Elem<T>::store((typename Elem<T>::acc)y));
+    }
+  }
+}
+
+// The MX executor over one slice (starting on a block boundary): full super-groups in the lane-interleaved
+// layout of xfer_mx (every memory instruction contiguous across the workgroup; the scale bytes through
+// buffer descriptors built once, at one per-lane offset shared by every operand), then whole blocks in the
+// contiguous layout (16 elements per lane, a block per lane pair), then the last partial block element-wise.
+template <typename T, typename W, int K, int SP, int PM>
+__device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_t* const (&ss)[kMaxSrc],
+                                   char* const (&d)[kMaxDst], uint8_t* const (&sd)[kMaxDst], int nd, uint32_t dm,
+                                   uint64_t n, float scale, bool vec) {
+  constexpr int G = 16;
+  constexpr int VT = (int)sizeof(T);  // 16-B vectors per group of T (W: one)
+  constexpr int V = SP == SP_T ? VT : (SP == SP_TW ? VT + (K - 1) : K);
+  constexpr int UU = V <= 2 ? 4 : (V <= 4 ? 2 : 1);
+  constexpr bool WT = PM == PM_WT;
+  constexpr bool NTS = PM == PM_FENCE_NTS;
+  auto isw = [](int k) constexpr -> bool { return SP == SP_W || (SP == SP_TW && k > 0); };
+  const uint64_t nt = blockDim.x;
+  const uint64_t nblk = (n + kMxBlock - 1) / kMxBlock;
+  uint64_t v = threadIdx.x;  // next contiguous group of this lane
+  if constexpr (!WT) {
+    constexpr int VM = VT, SE = G / VM, RL = SE;  // lane l's run j: elements (j * nt + l) * SE .. + SE
+    constexpr int LPB = (int)kMxBlock / SE;
+    const uint64_t span = nt * (uint64_t)G;
+    const uint64_t nsg = vec ? n / span : 0;
+    constexpr int SBT = SE * (int)sizeof(T), SBW = SE;
+    const uint32_t lt = threadIdx.x * SBT, lw = threadIdx.x * SBW;
+    const uint32_t lb = threadIdx.x / LPB;  // the lane's block within a run's row of nt * SE elements
+    const bool lead = (threadIdx.x % LPB) == 0;
+    __amdgpu_buffer_rsrc_t rss[K], rsd[kMaxDst];
+#pragma unroll
+    for (int k = 0; k < K; ++k) rss[k] = rsrc_of(isw(k) ? (const char*)ss[k] : nullptr, isw(k) ? nblk : 0);
+#pragma unroll
+    for (int dd = 0; dd < kMaxDst; ++dd) rsd[dd] = rsrc_of((const char*)sd[dd], sd[dd] ? nblk : 0);
+    uint64_t sg = 0;
+    for (; sg + UU <= nsg; sg += UU) {
+      __amdgpu_buffer_rsrc_t bs[K], bd[kMaxDst];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const uint64_t es = isw(k) ? 1 : sizeof(T);
+        bs[k] = rsrc_of(s[k] + sg * span * es, (uint64_t)UU * span * es);
+      }
+#pragma unroll
+      for (int dd = 0; dd < kMaxDst; ++dd) {
+        if (dd >= nd) continue;
+        const uint64_t es = (dm >> dd) & 1 ? 1 : sizeof(T);
+        bd[dd] = rsrc_of(d[dd] + sg * span * es, (uint64_t)UU * span * es);
+      }
+      // block of (u, j) = sboff(u, j) (uniform) + lb (per lane)
+      auto sboff = [&](int u, int j) -> uint32_t { return (uint32_t)(((sg + u) * span + j * nt * SE) / kMxBlock); };
+      uint4 raw[UU][K][VM];
+      uint32_t sb[UU][K][VM];
+#pragma unroll
+      for (int u = 0; u < UU; ++u)
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+          for (int j = 0; j < VM; ++j) {
+            const uint32_t e0 = (uint32_t)(u * span + j * nt * SE);  // uniform
+            if (isw(k)) {
+              ld_sub<SBW>(raw[u][k], j, bs[k], lw, e0);
+              sb[u][k][j] = __builtin_amdgcn_raw_buffer_load_b8(rss[k], lb, sboff(u, j), kAuxLd);
+            } else {
+              ld_sub<SBT>(raw[u][k], j, bs[k], lt, e0 * (uint32_t)sizeof(T));
+              sb[u][k][j] = 0;
+            }
+          }
+#pragma unroll
+      for (int u = 0; u < UU; ++u) {
+        uint4 yq, yt[VM];
+        uint32_t xb[VM];
+        mx_group<T, W, K, SP, RL>(raw[u], sb[u], scale, nd, dm, yq, xb, yt);
+#pragma unroll
+        for (int dd = 0; dd < kMaxDst; ++dd) {
+          if (dd >= nd) continue;
+          const bool wide = (dm >> dd) & 1;
+#pragma unroll
+          for (int j = 0; j < VM; ++j) {
+            const uint32_t e0 = (uint32_t)(u * span + j * nt * SE);
+            if (wide) {
+              const uint4 q1[1] = {yq};
+              st_sub<SBW, NTS>(bd[dd], lw, e0, q1, j);
+              if (lead) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)xb[j], rsd[dd], lb, sboff(u, j), NTS ? 2 : 0);
+            } else {
+              st_sub<SBT, NTS>(bd[dd], lt, e0 * (uint32_t)sizeof(T), yt, j);
+            }
+          }
+        }
+      }
+    }
+    v = sg * nt + threadIdx.x;
+  }
+  // whole blocks, contiguous layout: group g = elements 16 g .. 16 g + 15, block g / 2 (lanes g, g ^ 1)
+  const uint64_t ng = vec ? (n / kMxBlock) * 2 : 0;
+  auto ld = [&](int k, uint64_t byte) -> uint4 {
+    if constexpr (WT) return ld16_sys(rsrc_of(s[k], isw(k) ? n : n * sizeof(T)), (uint32_t)byte);
+    else return ld16(s[k] + byte);
+  };
+  auto st = [&](int dd, uint64_t byte, uint4 y) {
+    if constexpr (WT) st16_sys(rsrc_of(d[dd], (dm >> dd) & 1 ? n : n * sizeof(T)), (uint32_t)byte, y);
+    else st16<NTS>(d[dd] + byte, y);
+  };
+  for (; v < ng; v += nt) {
+    uint4 raw[K][VT];
+    uint32_t sb[K][1];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (isw(k)) {
+        raw[k][0] = ld(k, v * G);
+        sb[k][0] = ld_elem<PM, uint8_t>(reinterpret_cast<const char*>(ss[k]), v / 2);
+      } else {
+        sb[k][0] = 0;
+#pragma unroll
+        for (int j = 0; j < VT; ++j) raw[k][j] = ld(k, v * G * sizeof(T) + 16 * j);
+      }
+    }
+    uint4 yq, yt[VT];
+    uint32_t xb[1];
+    mx_group<T, W, K, SP, G>(raw, sb, scale, nd, dm, yq, xb, yt);
+#pragma unroll
+    for (int dd = 0; dd < kMaxDst; ++dd) {
+      if (dd >= nd) continue;
+      if ((dm >> dd) & 1) {
+        st(dd, v * G, yq);
+        if ((v & 1) == 0) st_elem<PM, uint8_t>(reinterpret_cast<char*>(sd[dd]), v / 2, (uint8_t)xb[0]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < VT; ++j) st(dd, v * G * sizeof(T) + 16 * j, yt[j]);
+      }
+    }
+  }
+  for (uint64_t i = ng * G + threadIdx.x; i < n; i += nt) mx_elem<T, W, K, SP, PM>(s, ss, d, sd, nd, dm, n, scale, i);
+}
+
 // The (K, pattern) combinations the planner emits (validate_typed_patterns): fp8 wire = quantising push
 // (K 1, SP_T), reduction (K >= 2, SP_TW), dequantising all-gather (K 1, SP_W); fp32 partials = tree
 // stage 0 (SP_T), ring step (K 2, SP_TW), final stage / temp chains (SP_W). Anything else is reported
@@ -832,6 +1182,22 @@ __device__ FX_INLINE bool xfer_mx_k(int sp, const char* const (&s)[kMaxSrc], cha
     return true;
   }
   return false;
+}
+
+// MX wire patterns (validate: typed_pattern_ok): quantising push (K 1, SP_T), reduction (K >= 2, SP_TW),
+// dequantising all-gather (K 1, SP_W, dtype destinations only).
+template <typename T, typename W, int K, int PM>
+__device__ FX_INLINE bool xfer_mxb_k(int sp, const char* const (&s)[kMaxSrc], const uint8_t* const (&ss)[kMaxSrc],
+                                     char* const (&d)[kMaxDst], uint8_t* const (&sd)[kMaxDst], int nd, uint32_t dm,
+                                     uint64_t n, float scale, bool vec) {
+  if constexpr (K == 1) {
+    if (sp == SP_T) { xfer_mxb<T, W, 1, SP_T, PM>(s, ss, d, sd, nd, dm, n, scale, vec); return true; }
+    if (sp == SP_W && dm == 0) { xfer_mxb<T, W, 1, SP_W, PM>(s, ss, d, sd, nd, dm, n, scale, vec); return true; }
+    return false;
+  } else {
+    if (sp == SP_TW) { xfer_mxb<T, W, K, SP_TW, PM>(s, ss, d, sd, nd, dm, n, scale, vec); return true; }
+    return false;
+  }
 }
 
 // Typed op: operand addresses (STG offsets in units, element slice [lo, hi) in each operand's own
@@ -872,25 +1238,57 @@ __device__ FX_INLINE void xfer_op_typed(const DevCtx& c, const Op* o, uint32_t l
   }
   const uint64_t n = hi - lo;
   const uint32_t all_s = (1u << ns) - 1, all_d = (1u << nd) - 1;
-  if (sm == all_s && dm == all_d) {  // wire type throughout (fp32 partial -> fp32 partial, fp8 copy)
-    xfer_dispatch<W, OpSum, PM>(ns, s, d, nd, n, o->scale, vec);
-    return;
-  }
-  if (!FP8 && sm == 0 && dm == 0) {  // dtype throughout (raw inputs, all-gather copies)
-    xfer_dispatch<T, OpSum, PM>(ns, s, d, nd, n, o->scale, vec);
-    return;
-  }
   const int sp = sm == 0 ? SP_T : (sm == (all_s & ~1u) ? SP_TW : (sm == all_s ? SP_W : -1));
   bool ok = false;
-  switch (ns) {
-    case 1: ok = xfer_mx_k<T, W, 1, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-    case 2: ok = xfer_mx_k<T, W, 2, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-    case 3: ok = xfer_mx_k<T, W, 3, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-    case 4: ok = xfer_mx_k<T, W, 4, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-    case 5: ok = xfer_mx_k<T, W, 5, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-    case 6: ok = xfer_mx_k<T, W, 6, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-    case 7: ok = xfer_mx_k<T, W, 7, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-    default: ok = xfer_mx_k<T, W, 8, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+  if constexpr (IsMx<W>::value) {
+    // block scales: the shadow byte of each wire operand's first block (the slice starts on a block)
+    const uint8_t* ss[kMaxSrc];
+    uint8_t* sd[kMaxDst];
+#pragma unroll
+    for (int k = 0; k < kMaxSrc; ++k) {
+      const Loc l = o->src[k];
+      ss[k] = (k < ns && ((sm >> k) & 1))
+                  ? (const uint8_t*)c.peer_stg[l.rank] + par + c.mx_shadow + (l.off * c.stg_unit + lo) / kMxBlock
+                  : nullptr;
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxDst; ++k) {
+      const Loc l = o->dst[k];
+      sd[k] = (k < nd && ((dm >> k) & 1))
+                  ? (uint8_t*)c.peer_stg[l.rank] + par + c.mx_shadow + (l.off * c.stg_unit + lo) / kMxBlock
+                  : nullptr;
+    }
+    switch (ns) {
+      case 1: ok = xfer_mxb_k<T, W, 1, PM>(sp, s, ss, d, sd, nd, dm, n, o->scale, vec); break;
+      case 2: ok = xfer_mxb_k<T, W, 2, PM>(sp, s, ss, d, sd, nd, dm, n, o->scale, vec); break;
+      case 3: ok = xfer_mxb_k<T, W, 3, PM>(sp, s, ss, d, sd, nd, dm, n, o->scale, vec); break;
+      case 4: ok = xfer_mxb_k<T, W, 4, PM>(sp, s, ss, d, sd, nd, dm, n, o->scale, vec); break;
+      case 5: ok = xfer_mxb_k<T, W, 5, PM>(sp, s, ss, d, sd, nd, dm, n, o->scale, vec); break;
+      case 6: ok = xfer_mxb_k<T, W, 6, PM>(sp, s, ss, d, sd, nd, dm, n, o->scale, vec); break;
+      case 7: ok = xfer_mxb_k<T, W, 7, PM>(sp, s, ss, d, sd, nd, dm, n, o->scale, vec); break;
+      default: ok = xfer_mxb_k<T, W, 8, PM>(sp, s, ss, d, sd, nd, dm, n, o->scale, vec); break;
+    }
+    (void)pre;
+    (void)post_inv;
+  } else {
+    if (sm == all_s && dm == all_d) {  // wire type throughout (fp32 partial -> fp32 partial, fp8 copy)
+      xfer_dispatch<W, OpSum, PM>(ns, s, d, nd, n, o->scale, vec);
+      return;
+    }
+    if (!FP8 && sm == 0 && dm == 0) {  // dtype throughout (raw inputs, all-gather copies)
+      xfer_dispatch<T, OpSum, PM>(ns, s, d, nd, n, o->scale, vec);
+      return;
+    }
+    switch (ns) {
+      case 1: ok = xfer_mx_k<T, W, 1, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+      case 2: ok = xfer_mx_k<T, W, 2, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+      case 3: ok = xfer_mx_k<T, W, 3, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+      case 4: ok = xfer_mx_k<T, W, 4, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+      case 5: ok = xfer_mx_k<T, W, 5, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+      case 6: ok = xfer_mx_k<T, W, 6, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+      case 7: ok = xfer_mx_k<T, W, 7, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+      default: ok = xfer_mx_k<T, W, 8, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+    }
   }
   if (!ok && threadIdx.x == 0)  // unreachable for validated programs: fail loudly, never compute wrongly
     __hip_atomic_store(c.err, (uint32_t)(0x40000000u | (0xfdu << 8)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -954,12 +1352,12 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
   constexpr bool TYPED = !std::is_void<W>::value;
   using WT_ = typename std::conditional<TYPED, W, T>::type;
   constexpr uint32_t U = sizeof(T) < sizeof(WT_) ? sizeof(T) : sizeof(WT_);
-  const uint32_t quantum = TYPED ? 16 / U : (sizeof(T) >= 16 ? 1u : (uint32_t)(16 / sizeof(T)));
+  const uint32_t quantum = IsMx<WT_>::value ? kMxBlock : TYPED ? 16 / U : (sizeof(T) >= 16 ? 1u : (uint32_t)(16 / sizeof(T)));
   const uint64_t epoch = c.epochs[b] + 1;
   const uint64_t par = (epoch & 1) ? c.stg_half_bytes : 0;
   if (tid == 0) s_abort = 0;
   float pre = 1.0f;
-  if constexpr (TYPED && sizeof(WT_) == 1) {
+  if constexpr (TYPED && sizeof(WT_) == 1 && !IsMx<WT_>::value) {
     if (tid < 64) {
       float sc;
       const bool ok = fp8_scale<WT_>(c, b, epoch, par, &sc);

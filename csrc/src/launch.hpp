@@ -31,7 +31,8 @@ struct LaunchArgs {
   int query = 0;         // QUERY: which kernel
   int* occ_out = nullptr;
   int* regs_out = nullptr;
-  int wire = 0;          // EXEC / GROUP / QUERY of a typed program (Program::wire): 1 fp32, 2 e4m3, 3 e5m2
+  int wire = 0;          // EXEC / GROUP / QUERY of a typed program (Program::wire): 1 fp32, 2 e4m3, 3 e5m2,
+                         // 4 / 5 MX e4m3 / e5m2
 };
 
 // Typed-program executors (exec_mx_kernel), SUM/AVG only: fp32 partials for 16/8-bit dtypes
@@ -44,7 +45,18 @@ int launch_mx_acc_e5m2(const LaunchArgs& a);
 int launch_mx_wire_f32(const LaunchArgs& a);          // fp32 over e4m3 / e5m2 (a.wire)
 int launch_mx_wire_bf16(const LaunchArgs& a);
 int launch_mx_wire_f16(const LaunchArgs& a);
+int launch_mxb_wire_f32(const LaunchArgs& a);         // OCP MX block-scaled fp8 wire (a.wire 4 / 5)
+int launch_mxb_wire_bf16(const LaunchArgs& a);
+int launch_mxb_wire_f16(const LaunchArgs& a);
 inline int launch_mx(int dtype, const LaunchArgs& a) {
+  if (a.wire >= 4) {
+    switch (dtype) {
+      case FLEXAR_FLOAT32: return launch_mxb_wire_f32(a);
+      case FLEXAR_BFLOAT16: return launch_mxb_wire_bf16(a);
+      case FLEXAR_FLOAT16: return launch_mxb_wire_f16(a);
+      default: return FLEXAR_ERR_UNSUPPORTED;
+    }
+  }
   if (a.wire == 1) {
     switch (dtype) {
       case FLEXAR_BFLOAT16: return launch_mx_acc_bf16(a);

@@ -12,7 +12,8 @@ parities, so a stale staging line cannot go unnoticed):
   2,4 and 4,2 at N = 8 - 2,2 at N = 4 - with push and pull all-gather, RHD), multi-channel rings, fp32 and
   bf16, SUM and the fused AVG, uneven tail sizes, in place;
 * typed bf16 partials ("+f32", one rounding) and per-hop rounding ("+rw") of the multi-hop schedules;
-* all_reduce_fp8 (fused pre/post-scale, e4m3 wire) against a torch emulation of the same arithmetic;
+* all_reduce_fp8 (fused pre/post-scale, e4m3 wire) against a torch emulation of the same arithmetic, and the
+  OCP MX wire ("flat+mxe4m3", block scales, no amax pass) bit for bit against ops.quant.mx_allreduce_reference;
 * reduce-scatter / all-gather / all-to-all / broadcast (staging and zero copy);
 * zero-copy allreduce over registered buffers;
 * executor grid requests of 256, 512 and 1024 workgroups when ranks do not share a device (clamped to
@@ -170,6 +171,17 @@ def _worker(rank, world, port, shared, q, transport="rccl", no_ipc=False, parts=
                 mism = (~torch.isclose(y.float().cpu(), want.float(), rtol=1e-5, atol=0)).float().mean().item()
                 results[("fp8_emulation_mismatch", str(dtype), op)] = mism
                 results[("fp8_rel", str(dtype), op)] = rel(y, ref)
+            # OCP MX wire (block scales, no amax pass): bit for bit the reference arithmetic
+            from allreduce_over_mpi_amd.ops.quant import mx_allreduce_reference
+
+            for dtype, spec in ((torch.float32, "flat+mxe4m3"), (torch.bfloat16, "flat+mxe4m3"),
+                                (torch.bfloat16, "flat+wt+mxe5m2")):
+                xs = [x * (r + 1) for r, x in enumerate(inputs(big, 9, dtype))]
+                want = mx_allreduce_reference(xs, spec.rsplit("+mx", 1)[1], "avg")
+                for _ in range(3):
+                    y = comm.all_reduce(xs[rank].to(dev), op="avg", algo=spec)
+                    torch.cuda.synchronize()
+                results[("mx_mismatch", str(dtype), spec)] = int((y.cpu().view(torch.uint8) != want.view(torch.uint8)).sum())
         if "all" in parts or "colls" in parts:
             m = 4099
             for spec in (None, "ring", "flat+wt"):
@@ -338,6 +350,9 @@ def _check(out, world, shared):
                 continue
             if key[0] == "fp8_rel":
                 assert err < 0.1, (rank, key, err)
+                continue
+            if key[0] == "mx_mismatch":
+                assert err == 0, (rank, key, err)
                 continue
             if key[0] == "ddp":
                 assert err < 2e-4, (rank, key, err)

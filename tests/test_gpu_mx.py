@@ -1,0 +1,74 @@
+"""The OCP MX block-scaled fp8 wire on the GPU ("+mxe4m3" / "+mxe5m2", docs/DESIGN.md §9.2): one launch of
+every rank of an in-process group, bit for bit against ops.quant.mx_allreduce_reference (the CPU tests pin
+that reference to the host executor), over the lane-interleaved super-groups, the contiguous blocks and the
+element-wise tail, the fence and write-through protocols, both parities. The multi-process form is in
+test_gpu_multidevice.py (exec kernel, one process per rank).
+
+Reference counterpart: none (the reference moves fp32 only); BASELINE config #5 without its amax pass.
+"""
+import pytest
+import torch
+
+from allreduce_over_mpi_amd.ops.quant import mx_allreduce_reference
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def groups(cuda):
+    from allreduce_over_mpi_amd.parallel import LocalGroup
+
+    gs = {n: LocalGroup(n, workspace_bytes=96 << 20) for n in (2, 4, 8)}
+    yield gs
+    for g in gs.values():
+        g.close()
+
+
+def _xs(n, count, dtype, seed, spread=2.0):
+    g = torch.Generator().manual_seed(seed)
+    lim = 6e4 if dtype == torch.float16 else 1e30
+    return [(torch.randn(count, generator=g) * torch.exp(torch.randn(count, generator=g) * spread)).clamp(-lim, lim)
+            .to(dtype) for _ in range(n)]
+
+
+def _check(grp, xs, spec, op, cuda, reps=2):
+    wire = spec.rsplit("+mx", 1)[1]
+    want = mx_allreduce_reference(xs, wire, op)
+    for _ in range(reps):  # both staging parities
+        outs = grp.all_reduce([x.to(cuda) for x in xs], op, algo=spec)
+        torch.cuda.synchronize()
+        for r, o in enumerate(outs):
+            bad = (o.cpu().view(torch.uint8) != want.view(torch.uint8)).nonzero().flatten()
+            assert bad.numel() == 0, (spec, op, str(xs[0].dtype), r, bad[:8].tolist(), o.numel())
+    grp.check()
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+def test_group_mx_wire_bitwise(cuda, groups, n, dtype):
+    # 1000003: interleaved super-groups + contiguous blocks + a 19-element tail per chunk boundary
+    for count in (1000003, 4099, 33):
+        _check(groups[n], _xs(n, count, dtype, seed=n * 7 + count), "flat+pull+mxe4m3", "avg", cuda)
+    _check(groups[n], _xs(n, 65537, dtype, seed=n), "flat+pull+mxe5m2", "sum", cuda)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_group_mx_wire_write_through_and_large(cuda, groups, dtype):
+    n = 4
+    _check(groups[n], _xs(n, 300001, dtype, seed=5), "flat+pull+wt+mxe4m3", "avg", cuda)
+    _check(groups[n], _xs(n, 8 * 1024 * 1024 + 333, dtype, seed=6), "flat+pull+mxe4m3", "avg", cuda, reps=1)
+
+
+def test_group_mx_wire_keeps_small_blocks(cuda, groups):
+    """Blocks 2^-20 .. 2^20 apart: per-block scales keep each block's relative precision, where the
+    per-call global scale of "+e4m3" flushes the small blocks (test_mx_wire.py has the CPU form)."""
+    n, count = 4, 1 << 20
+    g = torch.Generator().manual_seed(9)
+    mag = torch.pow(2.0, torch.randint(-20, 21, (count // 32,), generator=g).float()).repeat_interleave(32)
+    xs = [torch.randn(count, generator=g) * mag for _ in range(n)]
+    exact = torch.stack([x.double() for x in xs]).sum(0)
+    mx = groups[n].all_reduce([x.to(cuda) for x in xs], "sum", algo="flat+pull+mxe4m3")[0].cpu().double()
+    glob = groups[n].all_reduce_fp8([x.to(cuda) for x in xs], op="sum")[0].cpu().double()
+    med = lambda y: float(((y - exact).abs() / exact.abs().clamp_min(1e-30)).median())
+    assert med(mx) < 0.05, med(mx)
+    assert med(glob) > 10 * med(mx), (med(glob), med(mx))
