@@ -4,7 +4,8 @@ ITERS calls of SPEC on MIB MiB per rank, hipEvent-timed; the bytes are the progr
 the ranks, csrc/include/flexar/cost_model.hpp program_cost, which matches rocprofv3 FETCH/WRITE counters:
 profiles/r3_pmc_model). Run under `rocprofv3 --kernel-trace --stats` for per-kernel times.
 
-    python3 bench/typed_exec_probe.py SPEC DTYPE       # SPEC "fp8" = all_reduce_fp8 (flat, e4m3 wire, AVG)
+    python3 bench/typed_exec_probe.py SPEC DTYPE       # SPEC "fp8" = all_reduce_fp8 (flat, e4m3 wire, AVG);
+                                                       # "flat+pull+mxe4m3" = the OCP MX wire (AVG)
 """
 import json
 import os
@@ -36,8 +37,9 @@ def main():
         run = lambda: grp.all_reduce_fp8(xs, op="avg", outs=ys)  # noqa: E731
         model_spec = "flat+pull+e4m3"
         del parts
-    else:
-        run = lambda: grp.all_reduce(xs, outs=ys, algo=spec)  # noqa: E731
+    else:  # "+mxe4m3" / "+mxe5m2": the OCP MX wire, no amax pass (AVG like the fp8 case)
+        op = "avg" if "+mx" in spec else "sum"
+        run = lambda: grp.all_reduce(xs, op, outs=ys, algo=spec)  # noqa: E731
         model_spec = spec
     for _ in range(3):
         run()

@@ -51,6 +51,7 @@ struct Program {
   // MX wire (wire 4 / 5): the e8m0 scale of the 32-element block of a wire operand at staging byte o lives
   // at byte mx_shadow + o / 32 of the same rank's staging half (offset units; 0 = no shadow)
   uint64_t mx_shadow = 0;
+  uint32_t max_nsrc = 0;  // the widest XFER fan-in (typed launches pick a kernel instantiation by it)
   // zero-copy program (AlgoSpec::zc): IN / OUT operands of other ranks address their registered buffers;
   // zc_bufs = which of them the program addresses on a peer (bit BUF_IN, bit BUF_OUT)
   bool zc = false;
@@ -351,6 +352,8 @@ class Planner {
 
   // Final typing pass: fp8 wire = every staging operand carries the wire type; per-XFER masks.
   void finish_types(Program& P) const {
+    for (const Op& o : P.ops)
+      if (o.kind == OP_XFER) P.max_nsrc = std::max<uint32_t>(P.max_nsrc, o.nsrc);
     if (!wire) return;
     for (Op& o : P.ops) {
       if (o.kind != OP_XFER) continue;

@@ -596,6 +596,7 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     la.stream = st;
     la.proto = proto_of(s);
     la.wire = dp->prog.wire;
+    la.max_fanin = (int)dp->prog.max_nsrc;
     std::unique_ptr<DeviceTimer> tm(c->profile ? new DeviceTimer : nullptr);
     if (tm) tm->start(st);
     c->calls++;
@@ -634,6 +635,7 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     la.stream = st;
     la.proto = proto_of(s);
     la.wire = dp->prog.wire;
+    la.max_fanin = (int)dp->prog.max_nsrc;
     rc = launch_dtype(dtype, op, la);
     if (rc) break;
     c->launches++;
@@ -739,6 +741,7 @@ int flexar_allreduce_fp8(flexar_comm_t c, const void* in, void* out, size_t coun
     la.stream = st;
     la.proto = proto_of(s);
     la.wire = dp->prog.wire;
+    la.max_fanin = (int)dp->prog.max_nsrc;
     if ((rc = launch_dtype(dtype, op, la))) return rc;
     c->launches++;
   }

@@ -128,7 +128,7 @@ static int group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
   for (uint64_t off = 0; off < count; off += piece) {
     uint64_t n = std::min<uint64_t>(piece, count - off);
     std::vector<DevCtx> h(nranks);
-    int grid = 0, wire = 0;
+    int grid = 0, wire = 0, fanin = 0;
     bool zc = false;
     for (int r = 0; r < nranks; ++r) {
       DevProgram* dp = nullptr;
@@ -139,6 +139,7 @@ static int group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
       zc = zc || dp->prog.zc;
       if (amax_parts) h[r].amax_parts = amax_parts[r];
       wire = dp->prog.wire;
+      fanin = std::max(fanin, (int)dp->prog.max_nsrc);
       int g = choose_grid(comms[r], n * es, dp->prog.nchan);
       grid = r == 0 ? g : grid;
       if (g != grid) { set_error("group ranks disagree on grid"); return FLEXAR_ERR_STATE; }
@@ -157,6 +158,7 @@ static int group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
     la.stream = st;
     la.proto = proto_of(specs[0]);
     la.wire = wire;
+    la.max_fanin = fanin;
     int rc = launch_dtype(dtype, op, la);
     if (!rc) (void)group_ctx_launched(st);
     if (rc) return rc;

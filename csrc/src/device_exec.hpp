@@ -885,6 +885,56 @@ __device__ FX_INLINE uint32_t mx_block_max(uint32_t m) {
   return m;
 }
 
+// The reduction's three steps (SP_TW), also run in operand batches by xfer_mxb for fan-ins above 4:
+// acc = the own value rounded through MX with its own block scale (what a peer would receive) ...
+template <typename T, typename W, int RL>
+__device__ FX_INLINE void mx_own(const uint4 (&raw)[(int)sizeof(T)], float (&acc)[16]) {
+  constexpr int R = 16 / RL, LPB = (int)kMxBlock / RL;
+  uint32_t m[R];
+  mx_run_amax<T, RL>(raw, m);
+  float s0[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) s0[r] = mx_scale_value(mx_scale_byte(mx_block_max<LPB>(m[r]), IsFp8<W>::e4m3));
+  uint4 q, t[4];
+  sq_group<T, W, 16, RL>(raw, s0, &q);
+  dq_group<float, W, 16, RL>(&q, s0, t);
+  __builtin_memcpy(acc, t, sizeof(acc));
+}
+// ... plus each peer's q * 2^X ...
+template <typename W, int RL>
+__device__ FX_INLINE void mx_wire_add(const uint4& raw, const uint32_t (&sb)[16 / RL], float (&acc)[16]) {
+  float sk[16 / RL];
+#pragma unroll
+  for (int r = 0; r < 16 / RL; ++r) sk[r] = mx_scale_value(sb[r]);
+  uint4 t[4];
+  dq_group<float, W, 16, RL>(&raw, sk, t);
+  float x[16];
+  __builtin_memcpy(x, t, sizeof(x));
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] += x[e];
+}
+// ... then times scale and, with a wire destination, re-quantised with the sum's own block scales.
+template <typename T, typename W, int RL>
+__device__ FX_INLINE void mx_finish(float (&acc)[16], float scale, int nd, uint32_t dm, uint4& yq,
+                                    uint32_t (&xb)[16 / RL], uint4 (&yt)[(int)sizeof(T)]) {
+  constexpr int R = 16 / RL, LPB = (int)kMxBlock / RL;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] *= scale;
+  if (dm) {
+    uint32_t m[R];
+    float sc[R];
+    mx_run_amax_f<RL>(acc, m);
+#pragma unroll
+    for (int r = 0; r < R; ++r) xb[r] = mx_scale_byte(mx_block_max<LPB>(m[r]), IsFp8<W>::e4m3), sc[r] = mx_scale_value(xb[r]);
+    uint4 t[4];
+    __builtin_memcpy(t, acc, sizeof(acc));
+    sq_group<float, W, 16, RL>(t, sc, &yq);
+    if (dm != (1u << nd) - 1) dq_group<T, W, 16, RL>(&yq, sc, yt);
+  } else {
+    encode_g<T, 16>(acc, yt);
+  }
+}
+
 // One lane's group of 16 elements in runs of RL (sb[k][r] = the scale byte of wire source k's block for
 // run r, loaded with the payload): the fp8 result `yq` with its block scale bytes `xb` (wire
 // destinations) and / or the dtype result `yt` (dtype destinations).
@@ -931,43 +981,10 @@ __device__ FX_INLINE void mx_group(const uint4 (&raw)[K][(int)sizeof(T)], const 
     }
   } else {
     float acc[16];
-    {  // the own contribution, rounded through MX with its own block scale (what a peer would receive)
-      uint32_t m[R];
-      mx_run_amax<T, RL>(raw[0], m);
-      float s0[R];
+    mx_own<T, W, RL>(raw[0], acc);
 #pragma unroll
-      for (int r = 0; r < R; ++r) s0[r] = mx_scale_value(mx_scale_byte(mx_block_max<LPB>(m[r]), E4));
-      uint4 q, t[4];
-      sq_group<T, W, 16, RL>(raw[0], s0, &q);
-      dq_group<float, W, 16, RL>(&q, s0, t);
-      __builtin_memcpy(acc, t, sizeof(acc));
-    }
-#pragma unroll
-    for (int k = 1; k < K; ++k) {
-      float sk[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) sk[r] = mx_scale_value(sb[k][r]);
-      uint4 t[4];
-      dq_group<float, W, 16, RL>(&raw[k][0], sk, t);
-      float x[16];
-      __builtin_memcpy(x, t, sizeof(x));
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[e] += x[e];
-    }
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] *= scale;
-    if (dm) {
-      uint32_t m[R];
-      mx_run_amax_f<RL>(acc, m);
-#pragma unroll
-      for (int r = 0; r < R; ++r) xb[r] = mx_scale_byte(mx_block_max<LPB>(m[r]), E4), sc[r] = mx_scale_value(xb[r]);
-      uint4 t[4];
-      __builtin_memcpy(t, acc, sizeof(acc));
-      sq_group<float, W, 16, RL>(t, sc, &yq);
-      if (dm != all_d) dq_group<T, W, 16, RL>(&yq, sc, yt);
-    } else {
-      encode_g<T, 16>(acc, yt);
-    }
+    for (int k = 1; k < K; ++k) mx_wire_add<W, RL>(raw[k][0], sb[k], acc);
+    mx_finish<T, W, RL>(acc, scale, nd, dm, yq, xb, yt);
   }
 }
 
@@ -1202,7 +1219,10 @@ __device__ FX_INLINE bool xfer_mxb_k(int sp, const char* const (&s)[kMaxSrc], co
 
 // Typed op: operand addresses (STG offsets in units, element slice [lo, hi) in each operand's own
 // type), then the all-dtype / all-wire fast paths or the mixed one.
-template <typename T, typename W, int PM>
+// KMAX: the widest fan-in this instantiation runs (fp8 wire kernels come in KMAX 4 and 8: the K 5..8 cases
+// raise the whole kernel's register allocation - 256 VGPRs and scratch spills - which cost the 4-rank MX
+// executor 25 % (profiles/r4_mx/README.md); programs with fan-in <= 4 launch the narrow instantiation).
+template <typename T, typename W, int PM, int KMAX = kMaxSrc>
 __device__ FX_INLINE void xfer_op_typed(const DevCtx& c, const Op* o, uint32_t lb, uint32_t nb, uint32_t quantum,
                                         uint64_t par, float pre, float post_inv) {
   uint64_t lo, hi;
@@ -1263,10 +1283,10 @@ __device__ FX_INLINE void xfer_op_typed(const DevCtx& c, const Op* o, uint32_t l
       case 2: ok = xfer_mxb_k<T, W, 2, PM>(sp, s, ss, d, sd, nd, dm, n, o->scale, vec); break;
       case 3: ok = xfer_mxb_k<T, W, 3, PM>(sp, s, ss, d, sd, nd, dm, n, o->scale, vec); break;
       case 4: ok = xfer_mxb_k<T, W, 4, PM>(sp, s, ss, d, sd, nd, dm, n, o->scale, vec); break;
-      case 5: ok = xfer_mxb_k<T, W, 5, PM>(sp, s, ss, d, sd, nd, dm, n, o->scale, vec); break;
-      case 6: ok = xfer_mxb_k<T, W, 6, PM>(sp, s, ss, d, sd, nd, dm, n, o->scale, vec); break;
-      case 7: ok = xfer_mxb_k<T, W, 7, PM>(sp, s, ss, d, sd, nd, dm, n, o->scale, vec); break;
-      default: ok = xfer_mxb_k<T, W, 8, PM>(sp, s, ss, d, sd, nd, dm, n, o->scale, vec); break;
+      case 5: if constexpr (KMAX >= 5) ok = xfer_mxb_k<T, W, 5, PM>(sp, s, ss, d, sd, nd, dm, n, o->scale, vec); break;
+      case 6: if constexpr (KMAX >= 6) ok = xfer_mxb_k<T, W, 6, PM>(sp, s, ss, d, sd, nd, dm, n, o->scale, vec); break;
+      case 7: if constexpr (KMAX >= 7) ok = xfer_mxb_k<T, W, 7, PM>(sp, s, ss, d, sd, nd, dm, n, o->scale, vec); break;
+      default: if constexpr (KMAX >= 8) ok = xfer_mxb_k<T, W, 8, PM>(sp, s, ss, d, sd, nd, dm, n, o->scale, vec); break;
     }
     (void)pre;
     (void)post_inv;
@@ -1284,10 +1304,10 @@ __device__ FX_INLINE void xfer_op_typed(const DevCtx& c, const Op* o, uint32_t l
       case 2: ok = xfer_mx_k<T, W, 2, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
       case 3: ok = xfer_mx_k<T, W, 3, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
       case 4: ok = xfer_mx_k<T, W, 4, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-      case 5: ok = xfer_mx_k<T, W, 5, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-      case 6: ok = xfer_mx_k<T, W, 6, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-      case 7: ok = xfer_mx_k<T, W, 7, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
-      default: ok = xfer_mx_k<T, W, 8, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+      case 5: if constexpr (KMAX >= 5) ok = xfer_mx_k<T, W, 5, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+      case 6: if constexpr (KMAX >= 6) ok = xfer_mx_k<T, W, 6, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+      case 7: if constexpr (KMAX >= 7) ok = xfer_mx_k<T, W, 7, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
+      default: if constexpr (KMAX >= 8) ok = xfer_mx_k<T, W, 8, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
     }
   }
   if (!ok && threadIdx.x == 0)  // unreachable for validated programs: fail loudly, never compute wrongly
@@ -1341,7 +1361,7 @@ __device__ FX_INLINE bool fp8_scale(const DevCtx& c, uint32_t b, uint64_t epoch,
   return __all(ok) != 0;
 }
 
-template <typename T, typename OP, int PM, typename W = void>
+template <typename T, typename OP, int PM, typename W = void, int KMAX = kMaxSrc>
 __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uint32_t grid) {
   __shared__ int s_abort;
   __shared__ float s_pre;
@@ -1385,7 +1405,7 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
       bool bar = false;
       for (uint32_t k = 0; k < n; ++k) {
         const Op* q = c.ops + i + (n > 1 ? (k + lb) % n : 0);
-        if constexpr (TYPED) xfer_op_typed<T, WT_, PM>(c, q, lb, nb, quantum, par, pre, post_inv);
+        if constexpr (TYPED) xfer_op_typed<T, WT_, PM, KMAX>(c, q, lb, nb, quantum, par, pre, post_inv);
         else xfer_op<T, OP, PM>(c, q, lb, nb, quantum, par);
         bar |= (q->flags & kXferBarrierAfter) != 0;
       }
@@ -1554,14 +1574,14 @@ __global__ void __launch_bounds__(kExecThreads) exec_kernel(DevCtx c) {
 }
 
 // Typed programs (Program::wire: fp32 partials or an fp8 wire), SUM/AVG only.
-template <typename T, typename W, int PM>
+template <typename T, typename W, int PM, int KMAX = kMaxSrc>
 __global__ void __launch_bounds__(kExecThreads) exec_mx_kernel(DevCtx c) {
-  exec_body<T, OpSum, PM, W>(c, blockIdx.x, gridDim.x);
+  exec_body<T, OpSum, PM, W, KMAX>(c, blockIdx.x, gridDim.x);
 }
-template <typename T, typename W, int PM>
+template <typename T, typename W, int PM, int KMAX = kMaxSrc>
 __global__ void __launch_bounds__(kExecThreads) exec_mx_group_kernel(const DevCtx* ctxs, uint32_t grid_per_rank) {
   const uint32_t r = blockIdx.x / grid_per_rank;
-  exec_body<T, OpSum, PM, W>(ctxs[r], blockIdx.x % grid_per_rank, grid_per_rank);
+  exec_body<T, OpSum, PM, W, KMAX>(ctxs[r], blockIdx.x % grid_per_rank, grid_per_rank);
 }
 
 // In-process group launch: nranks ranks share one grid (rank = blockIdx / grid_per_rank) —

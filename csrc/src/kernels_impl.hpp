@@ -119,24 +119,24 @@ inline int launch_int(int op, const LaunchArgs& a) {
 
 namespace flexar {
 
-// Typed-program executor launch (exec_mx_kernel<T, W, PM>); "+nts" runs the fence protocol.
-template <typename T, typename W>
-inline int launch_typed(const LaunchArgs& a) {
+// Typed-program executor launch (exec_mx_kernel<T, W, PM, KMAX>); "+nts" runs the fence protocol.
+template <typename T, typename W, int KMAX>
+inline int launch_typed_k(const LaunchArgs& a) {
   const bool wt = a.proto == PM_WT;
   if (a.kind != LAUNCH_QUERY) clear_stale_error();
   switch (a.kind) {
     case LAUNCH_QUERY:
-      return query_kernel(wt ? exec_mx_kernel<T, W, PM_WT> : exec_mx_kernel<T, W, PM_FENCE>, a);
+      return query_kernel(wt ? exec_mx_kernel<T, W, PM_WT, KMAX> : exec_mx_kernel<T, W, PM_FENCE, KMAX>, a);
     case LAUNCH_EXEC:
-      if (wt) hipLaunchKernelGGL((exec_mx_kernel<T, W, PM_WT>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
-      else hipLaunchKernelGGL((exec_mx_kernel<T, W, PM_FENCE>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
+      if (wt) hipLaunchKernelGGL((exec_mx_kernel<T, W, PM_WT, KMAX>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
+      else hipLaunchKernelGGL((exec_mx_kernel<T, W, PM_FENCE, KMAX>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
       break;
     case LAUNCH_GROUP:
       if (wt)
-        hipLaunchKernelGGL((exec_mx_group_kernel<T, W, PM_WT>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
+        hipLaunchKernelGGL((exec_mx_group_kernel<T, W, PM_WT, KMAX>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
                            a.stream, a.d_ctxs, (uint32_t)a.grid);
       else
-        hipLaunchKernelGGL((exec_mx_group_kernel<T, W, PM_FENCE>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
+        hipLaunchKernelGGL((exec_mx_group_kernel<T, W, PM_FENCE, KMAX>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
                            a.stream, a.d_ctxs, (uint32_t)a.grid);
       break;
     default:
@@ -148,6 +148,15 @@ inline int launch_typed(const LaunchArgs& a) {
     return FLEXAR_ERR_HIP;
   }
   return 0;
+}
+// fp8 wire kernels (global and MX scales) come in two fan-in classes (xfer_op_typed KMAX): programs whose
+// XFERs read at most 4 operands (flat schedules of <= 4 ranks) launch the narrow one
+template <typename T, typename W>
+inline int launch_typed(const LaunchArgs& a) {
+  if constexpr (sizeof(W) == 1) {
+    if (a.max_fanin > 0 && a.max_fanin <= 4) return launch_typed_k<T, W, 4>(a);
+  }
+  return launch_typed_k<T, W, kMaxSrc>(a);
 }
 
 }  // namespace flexar
