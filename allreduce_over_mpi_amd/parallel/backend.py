@@ -635,8 +635,18 @@ def flexar_fp8_compress_hook(state, bucket):
     side.wait_stream(cur)
     with torch.cuda.stream(side):
         buf.record_stream(side)
-        state.comm.all_reduce_fp8(buf, op="avg", algo=state.algo if state.algo and "wt" in state.algo else None)
+        state.comm.all_reduce_fp8(buf, op="avg", algo=state.algo if state.algo and "wt" in state.algo else None,
+                                  wire=getattr(state, "fp8_wire", "e4m3"))
         fut = torch.futures.Future(devices=[buf.device])
         fut.set_result(buf)
     state.calls += 1
     return fut
+
+
+def flexar_mxfp8_compress_hook(state, bucket):
+    """DDP comm hook: the OCP MX form of ``flexar_fp8_compress_hook`` - one executor launch per bucket and no
+    amax kernel: each 32-element block of the gradients carries its own e8m0 scale, computed inside the
+    launch (docs/DESIGN.md §9.2), so a bucket mixing layers of very different gradient magnitude keeps
+    fp8's relative precision in every block instead of scaling all of it by the bucket's largest value."""
+    state.fp8_wire = "mx_e4m3"
+    return flexar_fp8_compress_hook(state, bucket)

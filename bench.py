@@ -832,6 +832,27 @@ def run_config5(comm, world, dev, dist, timed_fn, max_vec, host_ref, args, rank)
                flexar_busbw_GBps=round(busbw_gbps(4 * n, t, world), 2) if t else None,
                max_rel_err=round(errs[0], 5),
                correct=errs[0] <= 0.13)  # e4m3: 3 mantissa bits, one rounding per contribution and result
+    # the OCP MX form of the same wire: a scale per 32-element block inside the one launch, no amax pass
+    failed, err = 0.0, None
+    try:
+        comm.all_reduce_fp8(x, op="avg", out=y, wire="mx_e4m3")
+        torch.cuda.synchronize()
+        err = float((y - ref).abs().max().item()) / (float(ref.abs().max().item()) + 1e-12)
+    except nv.FlexarError as e:
+        failed, err = 1.0, str(e)
+    failed, = max_vec([failed])
+    if failed:
+        out["mx"] = {"error": err if isinstance(err, str) else "failed on a peer"}
+        _recover(comm)
+    else:
+        tm = timed_fn(lambda: comm.all_reduce_fp8(x, op="avg", out=y, wire="mx_e4m3"), 10, 2)
+        if tm is None:
+            _recover(comm)
+        errm = max_vec([err])
+        out["mx"] = {"what": "wire mx_e4m3 (OCP MX, 32-element blocks, one launch)",
+                     "flexar_us": round(tm * 1e6, 1) if tm else None,
+                     "flexar_busbw_GBps": round(busbw_gbps(4 * n, tm, world), 2) if tm else None,
+                     "max_rel_err": round(errm[0], 5), "correct": errm[0] <= 0.13}
     if not host_ref and not args.no_rccl:
         z = x.clone()
         tr = timed_fn(lambda: dist.all_reduce(z, op=dist.ReduceOp.AVG), 10, 2)

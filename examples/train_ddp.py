@@ -8,6 +8,7 @@
 --comm backend : process group "flexar" (dist.all_reduce -> flexar executor, rest -> RCCL)
 --comm hook    : process group "nccl" + DDP comm hook routing gradient buckets through flexar
 --comm fp8hook : the same hook with fp8 e4m3 gradients on the wire (flexar_fp8_compress_hook)
+--comm mxhook  : OCP MX fp8 gradients, a scale per 32-element block, one launch (flexar_mxfp8_compress_hook)
 --comm zchook  : the hook with zero-copy buckets (registered on first sight, "flat+zc+push": no staging)
 Data: synthetic token batches; weights: random init (no network / checkpoints needed).
 """
@@ -24,7 +25,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--comm", default="backend", choices=["backend", "hook", "fp8hook", "zchook", "nccl"])
+    ap.add_argument("--comm", default="backend", choices=["backend", "hook", "fp8hook", "mxhook", "zchook", "nccl"])
     ap.add_argument("--model", default="gpt-small")
     ap.add_argument("--batch", type=int, default=8, help="sequences per rank")
     ap.add_argument("--steps", type=int, default=20)
@@ -66,8 +67,9 @@ def main():
     else:
         bucket_mb = float(args.bucket_mb)
     ddp = DDP(model, device_ids=[local], bucket_cap_mb=bucket_mb)
-    if args.comm in ("hook", "fp8hook", "zchook"):
-        hook = fb.flexar_fp8_compress_hook if args.comm == "fp8hook" else fb.flexar_allreduce_hook
+    if args.comm in ("hook", "fp8hook", "mxhook", "zchook"):
+        hook = {"fp8hook": fb.flexar_fp8_compress_hook,
+                "mxhook": fb.flexar_mxfp8_compress_hook}.get(args.comm, fb.flexar_allreduce_hook)
         ddp.register_comm_hook(fb.FlexarHookState(zero_copy=args.comm == "zchook"), hook)
     opt = torch.optim.AdamW(ddp.parameters(), lr=3e-4)
     gen = torch.Generator().manual_seed(1000 + rank)

@@ -72,10 +72,11 @@ def _train(rank, world, port, q, mode, model_kind="mlp", fallback="gloo"):
         model.load_state_dict(ref.state_dict())
         ddp = DDP(model, device_ids=[0], bucket_cap_mb=1)
         state = None
-        if mode in ("hook", "fp8hook", "zchook"):
+        if mode in ("hook", "fp8hook", "mxhook", "zchook"):
             # zchook: every gradient bucket registered on first sight, reduced by "flat+zc" (no staging)
             state = fb.FlexarHookState(zero_copy=mode == "zchook")
-            ddp.register_comm_hook(state, fb.flexar_fp8_compress_hook if mode == "fp8hook" else fb.flexar_allreduce_hook)
+            ddp.register_comm_hook(state, {"fp8hook": fb.flexar_fp8_compress_hook,
+                                           "mxhook": fb.flexar_mxfp8_compress_hook}.get(mode, fb.flexar_allreduce_hook))
         opt = torch.optim.SGD(ddp.parameters(), lr=0.05)
         ropt = torch.optim.SGD(ref.parameters(), lr=0.05)
         g = torch.Generator().manual_seed(42)
@@ -150,14 +151,14 @@ def _spawn(target, world, *args, timeout=300):
 
 @pytest.mark.parametrize("mode,model_kind,fallback", [
     ("backend", "mlp", "gloo"), ("hook", "mlp", "gloo"), ("backend", "gpt", "gloo"), ("hook", "gpt", "gloo"),
-    ("fp8hook", "mlp", "gloo"), ("zchook", "mlp", "gloo"), ("zchook", "gpt", "gloo"), ("backend", "gpt", "nccl")])
+    ("fp8hook", "mlp", "gloo"), ("mxhook", "mlp", "gloo"), ("zchook", "mlp", "gloo"), ("zchook", "gpt", "gloo"), ("backend", "gpt", "nccl")])
 def test_ddp_over_flexar(cuda, mode, model_kind, fallback):
     res = _spawn(_train, 2, mode, model_kind, fallback)
     for rank, err, used, tb, _ in res:
         assert tb is None, tb
         assert used and used > 0, "flexar path was not used"
         # fp8 on the wire: e4m3's 2^-4 relative step of each bucket's largest gradient, over 4 SGD steps
-        tol = 1e-2 if mode == "fp8hook" else (1e-5 if model_kind == "mlp" else 2e-4)
+        tol = 1e-2 if mode in ("fp8hook", "mxhook") else (1e-5 if model_kind == "mlp" else 2e-4)
         assert err < tol, (mode, model_kind, rank, err)
 
 
