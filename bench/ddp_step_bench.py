@@ -10,6 +10,8 @@
 - `pg_nozc`: the same with ``FLEXAR_PG_ZC=0`` (no probe, no sweeps: staging schedules only);
 - `hook`:   a gloo process group plus ``flexar_allreduce_hook`` (FlexarHookState defaults: every bucket
             registered, "flat+zc+push");
+- `fp8hook` / `mxhook`: the same with fp8 gradients on the wire (``flexar_fp8_compress_hook``: amax kernel +
+            one launch; ``flexar_mxfp8_compress_hook``: OCP MX block scales, one launch);
 - `nccl`:   RCCL (``init_process_group("nccl")``; the ranks share one GPU, so each gets its own
             NCCL_HOSTID and RCCL carries the bytes over loopback sockets - the step time is not an xGMI figure).
 
@@ -88,6 +90,18 @@ def worker(rank, world, port, mode, q):
                 return fut
 
             ddp.register_comm_hook(state, hook)
+        elif mode in ("fp8hook", "mxhook"):  # compressed gradients: global-scale fp8 / OCP MX fp8 on the wire
+            state = fb.FlexarHookState(algo=os.environ.get("DDPB_HOOK_ALGO") or None)
+            base = fb.flexar_fp8_compress_hook if mode == "fp8hook" else fb.flexar_mxfp8_compress_hook
+
+            def chook(st, bucket):
+                t0 = time.perf_counter()
+                fut = base(st, bucket)
+                host["calls"] += 1
+                host["s"] += time.perf_counter() - t0
+                return fut
+
+            ddp.register_comm_hook(state, chook)
         elif mode == "nccl":
             def nccl_hook(_, bucket):
                 t0 = time.perf_counter()
