@@ -737,23 +737,27 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
     constexpr int SBT = SE * (int)sizeof(T), SBW = SE * (int)sizeof(W);
     const uint32_t lt = threadIdx.x * SBT, lw = threadIdx.x * SBW;  // the lane's offset, per element size
     uint64_t sg = 0;
-    for (; sg + UU <= nsg; sg += UU) {
-      // descriptors over this iteration's UU super-groups (<= UU * 16 KiB * 4 B: 32-bit offsets)
+    // one iteration over UI super-groups; full super-groups beyond the last multiple of UU take the same
+    // lane-interleaved layout one at a time (a slice of a few super-groups - DDP buckets, small pieces -
+    // would otherwise fall to the contiguous layout's lane-strided instructions)
+    auto iter = [&](auto ucnt) {
+      constexpr int UI = decltype(ucnt)::value;
+      // descriptors over this iteration's UI super-groups (<= UI * 16 KiB * 4 B: 32-bit offsets)
       __amdgpu_buffer_rsrc_t bs[K], bd[kMaxDst];
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const uint64_t es = isw(k) ? sizeof(W) : sizeof(T);
-        bs[k] = rsrc_of(s[k] + sg * span * es, (uint64_t)UU * span * es);
+        bs[k] = rsrc_of(s[k] + sg * span * es, (uint64_t)UI * span * es);
       }
 #pragma unroll
       for (int dd = 0; dd < kMaxDst; ++dd) {
         if (dd >= nd) continue;
         const uint64_t es = (dm >> dd) & 1 ? sizeof(W) : sizeof(T);
-        bd[dd] = rsrc_of(d[dd] + sg * span * es, (uint64_t)UU * span * es);
+        bd[dd] = rsrc_of(d[dd] + sg * span * es, (uint64_t)UI * span * es);
       }
-      uint4 raw[UU][K][VM];
+      uint4 raw[UI][K][VM];
 #pragma unroll
-      for (int u = 0; u < UU; ++u)
+      for (int u = 0; u < UI; ++u)
 #pragma unroll
         for (int k = 0; k < K; ++k)
 #pragma unroll
@@ -763,7 +767,7 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
             else ld_sub<SBT>(raw[u][k], j, bs[k], lt, e0 * (uint32_t)sizeof(T));
           }
 #pragma unroll
-      for (int u = 0; u < UU; ++u) {
+      for (int u = 0; u < UI; ++u) {
         float acc[G];
         compute_group(raw[u], acc);
 #pragma unroll
@@ -780,7 +784,10 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
           }
         }
       }
-    }
+    };
+    for (; sg + UU <= nsg; sg += UU) iter(std::integral_constant<int, UU>{});
+    if constexpr (UU > 1)
+      for (; sg < nsg; ++sg) iter(std::integral_constant<int, 1>{});
     v = sg * nt + threadIdx.x;  // the contiguous-group loops below take the rest (< UU super-groups)
   }
   for (; v + (UU - 1) * nt < ng; v += UU * nt) {
@@ -1079,25 +1086,29 @@ __device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_
 #pragma unroll
     for (int dd = 0; dd < kMaxDst; ++dd) rsd[dd] = rsrc_of((const char*)sd[dd], sd[dd] ? nblk : 0);
     uint64_t sg = 0;
-    for (; sg + UU <= nsg; sg += UU) {
+    // one iteration over UI super-groups; full super-groups beyond the last multiple of UU take the same
+    // lane-interleaved layout one at a time (a slice of a few super-groups - DDP buckets, small pieces -
+    // would otherwise fall to the contiguous layout's lane-strided instructions)
+    auto iter = [&](auto ucnt) {
+      constexpr int UI = decltype(ucnt)::value;
       __amdgpu_buffer_rsrc_t bs[K], bd[kMaxDst];
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const uint64_t es = isw(k) ? 1 : sizeof(T);
-        bs[k] = rsrc_of(s[k] + sg * span * es, (uint64_t)UU * span * es);
+        bs[k] = rsrc_of(s[k] + sg * span * es, (uint64_t)UI * span * es);
       }
 #pragma unroll
       for (int dd = 0; dd < kMaxDst; ++dd) {
         if (dd >= nd) continue;
         const uint64_t es = (dm >> dd) & 1 ? 1 : sizeof(T);
-        bd[dd] = rsrc_of(d[dd] + sg * span * es, (uint64_t)UU * span * es);
+        bd[dd] = rsrc_of(d[dd] + sg * span * es, (uint64_t)UI * span * es);
       }
       // block of (u, j) = sboff(u, j) (uniform) + lb (per lane)
       auto sboff = [&](int u, int j) -> uint32_t { return (uint32_t)(((sg + u) * span + j * nt * SE) / kMxBlock); };
-      uint4 raw[UU][K][VM];
-      uint32_t sb[UU][K][VM];
+      uint4 raw[UI][K][VM];
+      uint32_t sb[UI][K][VM];
 #pragma unroll
-      for (int u = 0; u < UU; ++u)
+      for (int u = 0; u < UI; ++u)
 #pragma unroll
         for (int k = 0; k < K; ++k)
 #pragma unroll
@@ -1112,7 +1123,7 @@ __device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_
             }
           }
 #pragma unroll
-      for (int u = 0; u < UU; ++u) {
+      for (int u = 0; u < UI; ++u) {
         uint4 yq, yt[VM];
         uint32_t xb[VM];
         mx_group<T, W, K, SP, RL>(raw[u], sb[u], scale, nd, dm, yq, xb, yt);
@@ -1133,7 +1144,10 @@ __device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_
           }
         }
       }
-    }
+    };
+    for (; sg + UU <= nsg; sg += UU) iter(std::integral_constant<int, UU>{});
+    if constexpr (UU > 1)
+      for (; sg < nsg; ++sg) iter(std::integral_constant<int, 1>{});
     v = sg * nt + threadIdx.x;
   }
   // whole blocks, contiguous layout: group g = elements 16 g .. 16 g + 15, block g / 2 (lanes g, g ^ 1)
