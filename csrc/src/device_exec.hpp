@@ -740,20 +740,23 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
     // one iteration over UI super-groups; full super-groups beyond the last multiple of UU take the same
     // lane-interleaved layout one at a time (a slice of a few super-groups - DDP buckets, small pieces -
     // would otherwise fall to the contiguous layout's lane-strided instructions)
-    auto iter = [&](auto ucnt) {
+    // `lim` elements from super-group sg: UI * span, or fewer for the last, partial super-group, whose lanes
+    // past `lim` load zeros and drop their stores (the buffer descriptors' range check; lim is a multiple of
+    // G, so every sub-chunk access is wholly inside or outside)
+    auto iter = [&](auto ucnt, uint64_t lim) {
       constexpr int UI = decltype(ucnt)::value;
       // descriptors over this iteration's UI super-groups (<= UI * 16 KiB * 4 B: 32-bit offsets)
       __amdgpu_buffer_rsrc_t bs[K], bd[kMaxDst];
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const uint64_t es = isw(k) ? sizeof(W) : sizeof(T);
-        bs[k] = rsrc_of(s[k] + sg * span * es, (uint64_t)UI * span * es);
+        bs[k] = rsrc_of(s[k] + sg * span * es, lim * es);
       }
 #pragma unroll
       for (int dd = 0; dd < kMaxDst; ++dd) {
         if (dd >= nd) continue;
         const uint64_t es = (dm >> dd) & 1 ? sizeof(W) : sizeof(T);
-        bd[dd] = rsrc_of(d[dd] + sg * span * es, (uint64_t)UI * span * es);
+        bd[dd] = rsrc_of(d[dd] + sg * span * es, lim * es);
       }
       uint4 raw[UI][K][VM];
 #pragma unroll
@@ -785,11 +788,14 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
         }
       }
     };
-    for (; sg + UU <= nsg; sg += UU) iter(std::integral_constant<int, UU>{});
+    for (; sg + UU <= nsg; sg += UU) iter(std::integral_constant<int, UU>{}, (uint64_t)UU * span);
     if constexpr (UU > 1)
-      for (; sg < nsg; ++sg) iter(std::integral_constant<int, 1>{});
-    v = sg * nt + threadIdx.x;  // the contiguous-group loops below take the rest (< UU super-groups)
+      for (; sg < nsg; ++sg) iter(std::integral_constant<int, 1>{}, span);
+    if (sg * span < ng * G) iter(std::integral_constant<int, 1>{}, ng * G - sg * span);
+    v = ng;  // every whole group done; the scalar tail takes the last < G elements
   }
+  // the contiguous layout: write-through executors (their coherent loads take whole-group descriptors)
+  if constexpr (WT || VM == 1) {
   for (; v + (UU - 1) * nt < ng; v += UU * nt) {
     uint4 raw[UU][K][VM];
 #pragma unroll
@@ -801,6 +807,7 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
     uint4 raw[K][VM];
     load_group(v, raw);
     finish_group(v, raw);
+  }
   }
   // scalar tail (or the whole span when a caller buffer is not 16-B aligned)
   for (uint64_t i = ng * G + threadIdx.x; i < n; i += nt) {
@@ -1069,7 +1076,6 @@ __device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_
   constexpr bool NTS = PM == PM_FENCE_NTS;
   auto isw = [](int k) constexpr -> bool { return SP == SP_W || (SP == SP_TW && k > 0); };
   const uint64_t nt = blockDim.x;
-  const uint64_t nblk = (n + kMxBlock - 1) / kMxBlock;
   uint64_t v = threadIdx.x;  // next contiguous group of this lane
   if constexpr (!WT) {
     constexpr int VM = VT, SE = G / VM, RL = SE;  // lane l's run j: elements (j * nt + l) * SE .. + SE
@@ -1080,28 +1086,32 @@ __device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_
     const uint32_t lt = threadIdx.x * SBT, lw = threadIdx.x * SBW;
     const uint32_t lb = threadIdx.x / LPB;  // the lane's block within a run's row of nt * SE elements
     const bool lead = (threadIdx.x % LPB) == 0;
+    // the scale shadows cover the whole blocks only: the last partial block is the scalar tail's (mx_elem),
+    // so a lane of the partial super-group never writes its scale
+    const uint64_t nfull = n / kMxBlock;
     __amdgpu_buffer_rsrc_t rss[K], rsd[kMaxDst];
 #pragma unroll
-    for (int k = 0; k < K; ++k) rss[k] = rsrc_of(isw(k) ? (const char*)ss[k] : nullptr, isw(k) ? nblk : 0);
+    for (int k = 0; k < K; ++k) rss[k] = rsrc_of(isw(k) ? (const char*)ss[k] : nullptr, isw(k) ? nfull : 0);
 #pragma unroll
-    for (int dd = 0; dd < kMaxDst; ++dd) rsd[dd] = rsrc_of((const char*)sd[dd], sd[dd] ? nblk : 0);
+    for (int dd = 0; dd < kMaxDst; ++dd) rsd[dd] = rsrc_of((const char*)sd[dd], sd[dd] ? nfull : 0);
     uint64_t sg = 0;
     // one iteration over UI super-groups; full super-groups beyond the last multiple of UU take the same
     // lane-interleaved layout one at a time (a slice of a few super-groups - DDP buckets, small pieces -
     // would otherwise fall to the contiguous layout's lane-strided instructions)
-    auto iter = [&](auto ucnt) {
+    // `lim` elements from super-group sg (fewer for the last, partial one: see xfer_mx)
+    auto iter = [&](auto ucnt, uint64_t lim) {
       constexpr int UI = decltype(ucnt)::value;
       __amdgpu_buffer_rsrc_t bs[K], bd[kMaxDst];
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const uint64_t es = isw(k) ? 1 : sizeof(T);
-        bs[k] = rsrc_of(s[k] + sg * span * es, (uint64_t)UI * span * es);
+        bs[k] = rsrc_of(s[k] + sg * span * es, lim * es);
       }
 #pragma unroll
       for (int dd = 0; dd < kMaxDst; ++dd) {
         if (dd >= nd) continue;
         const uint64_t es = (dm >> dd) & 1 ? 1 : sizeof(T);
-        bd[dd] = rsrc_of(d[dd] + sg * span * es, (uint64_t)UI * span * es);
+        bd[dd] = rsrc_of(d[dd] + sg * span * es, lim * es);
       }
       // block of (u, j) = sboff(u, j) (uniform) + lb (per lane)
       auto sboff = [&](int u, int j) -> uint32_t { return (uint32_t)(((sg + u) * span + j * nt * SE) / kMxBlock); };
@@ -1145,12 +1155,15 @@ __device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_
         }
       }
     };
-    for (; sg + UU <= nsg; sg += UU) iter(std::integral_constant<int, UU>{});
+    const uint64_t nwhole = vec ? (n / kMxBlock) * kMxBlock : 0;
+    for (; sg + UU <= nsg; sg += UU) iter(std::integral_constant<int, UU>{}, (uint64_t)UU * span);
     if constexpr (UU > 1)
-      for (; sg < nsg; ++sg) iter(std::integral_constant<int, 1>{});
-    v = sg * nt + threadIdx.x;
+      for (; sg < nsg; ++sg) iter(std::integral_constant<int, 1>{}, span);
+    if (sg * span < nwhole) iter(std::integral_constant<int, 1>{}, nwhole - sg * span);
+    v = (n / kMxBlock) * 2;  // every whole block done
   }
-  // whole blocks, contiguous layout: group g = elements 16 g .. 16 g + 15, block g / 2 (lanes g, g ^ 1)
+  // whole blocks, contiguous layout (write-through executors): group g = elements 16 g .. 16 g + 15,
+  // block g / 2 (lanes g, g ^ 1)
   const uint64_t ng = vec ? (n / kMxBlock) * 2 : 0;
   auto ld = [&](int k, uint64_t byte) -> uint4 {
     if constexpr (WT) return ld16_sys(rsrc_of(s[k], isw(k) ? n : n * sizeof(T)), (uint32_t)byte);
@@ -1160,6 +1173,7 @@ __device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_
     if constexpr (WT) st16_sys(rsrc_of(d[dd], (dm >> dd) & 1 ? n : n * sizeof(T)), (uint32_t)byte, y);
     else st16<NTS>(d[dd] + byte, y);
   };
+  if constexpr (WT)
   for (; v < ng; v += nt) {
     uint4 raw[K][VT];
     uint32_t sb[K][1];
