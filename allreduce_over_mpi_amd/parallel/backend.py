@@ -115,6 +115,17 @@ class FlexarProcessGroup(dist.ProcessGroup):
         self._zc_min = int(os.environ.get("FLEXAR_PG_ZC_MIN_BYTES", str(1 << 20)))
         self._zc_sweep_every = max(1, int(os.environ.get("FLEXAR_PG_ZC_SWEEP", "16") or 16))
         self._ar_calls = 0
+        # opt-in lossy compression of the float SUM / AVG allreduces of at least FLEXAR_PG_COMPRESS_MIN_BYTES
+        # (1 MiB), for DDP / any caller of init_process_group("flexar") without a comm hook:
+        # FLEXAR_PG_COMPRESS=mx_e4m3 | mx_e5m2 puts OCP MX fp8 on the links (a scale per 32-element block,
+        # one launch: docs/DESIGN.md §9.2). Every rank must set the same value: the first allreduce checks
+        # it collectively (a mismatch would compile different schedules on different ranks).
+        comp = os.environ.get("FLEXAR_PG_COMPRESS", "").strip().lower()
+        if comp not in _COMPRESS:
+            raise ValueError(f"FLEXAR_PG_COMPRESS={comp!r}: expected one of {sorted(k for k in _COMPRESS if k)}")
+        self._compress = _COMPRESS[comp]
+        self._compress_min = int(os.environ.get("FLEXAR_PG_COMPRESS_MIN_BYTES", str(1 << 20)))
+        self._compress_agreed = False
 
     # ------------------------------------------------------------------ plumbing
     def getBackendName(self):
@@ -197,6 +208,24 @@ class FlexarProcessGroup(dist.ProcessGroup):
                 and nv.lib() is not None and (opname != "avg" or tensors[0].is_floating_point())
                 and not (opname in ("band", "bor", "bxor") and tensors[0].is_floating_point()))
 
+    def _compress_algo(self, t, opname):
+        """The spec of this allreduce under FLEXAR_PG_COMPRESS, or the plain one (self.algo)."""
+        if not self._compress_agreed:  # once, collectively: every rank's setting the same
+            code = _COMPRESS_CODES[self._compress]
+            t2 = torch.tensor([code, -code], dtype=torch.int32)
+            o = AllreduceOptions()
+            o.reduceOp = dist.ReduceOp.MIN
+            self._gloo.allreduce([t2], o).wait()
+            if int(t2[0]) != -int(t2[1]):  # min != max
+                raise RuntimeError("FLEXAR_PG_COMPRESS differs across ranks: every rank must set the same value")
+            self._compress_agreed = True
+        if (self._compress is None or self.hierarchical or self._world < 2 or opname not in ("sum", "avg")
+                or t.dtype not in (torch.float32, torch.bfloat16, torch.float16)
+                or t.numel() * t.element_size() < self._compress_min):
+            return self.algo
+        base = (self.algo or "flat+pull").replace("+zc", "")  # the MX wire runs on staging (no registration)
+        return base + self._compress
+
     def allreduce(self, tensor_list, opts=AllreduceOptions()):
         opname = _redop_name(opts.reduceOp)
         if not self._flexar_ok(tensor_list, opname) or self.algo == "rccl":  # FLEXAR_ALGO=rccl: vendor path
@@ -224,7 +253,10 @@ class FlexarProcessGroup(dist.ProcessGroup):
                               "band": "min", "bxor": "bxor"}[opname]
                     comm.all_reduce(t8, op=boolop, algo=self.algo)
                 else:
-                    comm.all_reduce(t, op=opname, algo=self.algo)
+                    algo = self._compress_algo(t, opname) if self._compress or not self._compress_agreed else self.algo
+                    comm.all_reduce(t, op=opname, algo=algo)
+                    if algo is not self.algo:
+                        self.stats["compressed"] = self.stats.get("compressed", 0) + 1
                 self.stats["flexar_allreduce"] += 1
             fut = torch.futures.Future(devices=[dev])
             fut.set_result(tensor_list)  # records an event on the side stream; wait() joins it
@@ -611,6 +643,10 @@ def flexar_allreduce_hook(state, bucket):
         fut.set_result(buf)  # CUDA-aware: DDP's wait joins the side stream, backward keeps overlapping
     state.calls += 1
     return fut
+
+
+_COMPRESS = {"": None, "0": None, "none": None, "mx_e4m3": "+mxe4m3", "mx_e5m2": "+mxe5m2"}
+_COMPRESS_CODES = {None: 0, "+mxe4m3": 1, "+mxe5m2": 2}
 
 
 def flexar_fp8_compress_hook(state, bucket):

@@ -155,3 +155,49 @@ def test_backend_agreements_over_the_host_page_bitmask():
             got, calls, mode = out[has_page]
             assert got == [True, False, True, False, True, False, True], (has_page, got)
             assert calls == (1 if has_page else 0) and mode is has_page
+
+
+def _compress_worker(rank, world, port, settings, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_PG_COMPRESS=settings[rank])
+        import torch.distributed as dist
+
+        import allreduce_over_mpi_amd.parallel.backend as fb  # noqa: F401  registers "flexar"
+
+        dist.init_process_group("flexar", rank=rank, world_size=world)
+        pg = dist.group.WORLD
+        try:
+            picks = [pg._compress_algo(torch.zeros(1 << 18), "avg"),  # 1 MiB fp32: compressed
+                     pg._compress_algo(torch.zeros(1 << 18, dtype=torch.bfloat16), "sum"),  # 512 KiB: too small
+                     pg._compress_algo(torch.zeros(1 << 18, dtype=torch.int32), "sum"),
+                     pg._compress_algo(torch.zeros(1 << 18), "max")]
+            err = None
+        except RuntimeError as e:
+            picks, err = None, str(e)
+        dist.destroy_process_group()
+        q.put((rank, picks, err, None))
+    except Exception:
+        import traceback
+
+        q.put((rank, None, None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("settings", [("mx_e4m3", "mx_e4m3"), ("mx_e4m3", "")])
+def test_backend_compression_option_is_agreed(settings):
+    """FLEXAR_PG_COMPRESS: float SUM / AVG allreduces of >= 1 MiB get the OCP MX wire; the setting is agreed
+    on the first call and a mismatch fails on every rank (it would compile different schedules)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_compress_worker, args=(r, 2, port, settings, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(2)]
+    for p in ps:
+        p.join(60)
+    for rank, picks, err, tb in res:
+        assert tb is None, tb
+        if settings[0] == settings[1]:
+            assert err is None and picks == ["flat+pull+mxe4m3", None, None, None], (rank, picks, err)
+        else:
+            assert picks is None and "differs across ranks" in err, (rank, picks, err)

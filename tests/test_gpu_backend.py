@@ -42,6 +42,9 @@ def _train(rank, world, port, q, mode, model_kind="mlp", fallback="gloo"):
             os.environ["FLEXAR_PG_ZC_SWEEP"] = "4"
             mode = "backend"
             steps, report_regs = 8, True
+        elif mode == "backend_mx":  # the backend with FLEXAR_PG_COMPRESS: OCP MX fp8 gradients, no comm hook
+            os.environ.update(FLEXAR_PG_COMPRESS="mx_e4m3", FLEXAR_PG_COMPRESS_MIN_BYTES="0", FLEXAR_PG_ZC="0")
+            steps, report_regs = 4, False
         elif mode == "nccl8":  # the RCCL reference of the 8-step run above
             mode = "nccl"
             steps, report_regs = 8, False
@@ -58,7 +61,7 @@ def _train(rank, world, port, q, mode, model_kind="mlp", fallback="gloo"):
 
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
-        pg_kind = {"backend": "flexar", "nccl": "nccl"}.get(mode, "gloo")
+        pg_kind = {"backend": "flexar", "backend_mx": "flexar", "nccl": "nccl"}.get(mode, "gloo")
         if pg_kind == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         else:
@@ -105,6 +108,7 @@ def _train(rank, world, port, q, mode, model_kind="mlp", fallback="gloo"):
         err = max((a - b).abs().max().item() for a, b in zip(model.parameters(), ref.parameters()))
         pg = dist.group.WORLD
         used = (getattr(pg, "stats", {}).get("flexar_allreduce", 0) if mode == "backend" else
+                getattr(pg, "stats", {}).get("compressed", 0) if mode == "backend_mx" else
                 1 if mode == "nccl" else state.calls)
         if mode == "backend" and model_kind == "gpt" and not pg.stats.get("zc_registrations"):
             used = 0  # the gradient buckets must have been registered (zero copy) by the backend's probe
@@ -151,14 +155,14 @@ def _spawn(target, world, *args, timeout=300):
 
 @pytest.mark.parametrize("mode,model_kind,fallback", [
     ("backend", "mlp", "gloo"), ("hook", "mlp", "gloo"), ("backend", "gpt", "gloo"), ("hook", "gpt", "gloo"),
-    ("fp8hook", "mlp", "gloo"), ("mxhook", "mlp", "gloo"), ("zchook", "mlp", "gloo"), ("zchook", "gpt", "gloo"), ("backend", "gpt", "nccl")])
+    ("fp8hook", "mlp", "gloo"), ("mxhook", "mlp", "gloo"), ("backend_mx", "mlp", "gloo"), ("zchook", "mlp", "gloo"), ("zchook", "gpt", "gloo"), ("backend", "gpt", "nccl")])
 def test_ddp_over_flexar(cuda, mode, model_kind, fallback):
     res = _spawn(_train, 2, mode, model_kind, fallback)
     for rank, err, used, tb, _ in res:
         assert tb is None, tb
         assert used and used > 0, "flexar path was not used"
         # fp8 on the wire: e4m3's 2^-4 relative step of each bucket's largest gradient, over 4 SGD steps
-        tol = 1e-2 if mode in ("fp8hook", "mxhook") else (1e-5 if model_kind == "mlp" else 2e-4)
+        tol = 1e-2 if mode in ("fp8hook", "mxhook", "backend_mx") else (1e-5 if model_kind == "mlp" else 2e-4)
         assert err < tol, (mode, model_kind, rank, err)
 
 
