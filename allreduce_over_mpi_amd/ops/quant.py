@@ -140,3 +140,27 @@ def mx_allreduce_reference(inputs, wire: str = "e4m3", op: str = "sum"):
             acc = acc * torch.tensor(1.0 / n, dtype=torch.float32)
         out[lo:hi] = mx_round(acc, wire)
     return out.to(dt)
+
+
+def mx_reduce_scatter_reference(inputs, wire: str = "e4m3", op: str = "sum"):
+    """What the flat reduce-scatter with the MX wire computes (planner.hpp build_flat_rs, "+mxe4m3"): rank r owns
+    block r (count / N elements) of every input; it sums its own block and then ranks 0, 1, ... (without r),
+    each rounded through MX with its sender's block scales (32-element blocks from the start of block r), in
+    fp32, applies AVG's 1/N and writes the result in the input dtype (no second MX rounding: nothing of the
+    result crosses a link)."""
+    import torch
+
+    n = len(inputs)
+    dt = inputs[0].dtype
+    m = inputs[0].numel() // n
+    outs = []
+    for r in range(n):
+        order = [r] + [p for p in range(n) if p != r]
+        acc = None
+        for p in order:
+            v = mx_round(inputs[p].reshape(-1)[r * m:(r + 1) * m].float(), wire)
+            acc = v if acc is None else acc + v
+        if op == "avg":
+            acc = acc * torch.tensor(1.0 / n, dtype=torch.float32)
+        outs.append(acc.to(dt))
+    return outs

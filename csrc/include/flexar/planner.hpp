@@ -211,6 +211,16 @@ class Planner {
     P->esize = esize;
     P->chan_start.push_back(0);
     stg = 0;
+    // the MX wire (wire 4 / 5) on the flat reduce-scatter (FSDP / ZeRO gradient shards): quantising pushes,
+    // the owner's reduction of its own value + N-1 wire contributions into OUT in the dtype
+    if (spec.wire) {
+      if (spec.wire < 4 || coll != Coll::REDUCE_SCATTER || spec.kind == AlgoKind::RING || spec.zc || spec.msg) {
+        if (err) *err = "typed staging on collectives: only the OCP MX wire on the flat reduce-scatter";
+        return false;
+      }
+      if (N > kMaxSrc) { if (err) *err = "MX wire reduce-scatter supports up to 8 ranks"; return false; }
+      if (!set_wire(spec, err)) return false;
+    }
     const bool ring = spec.kind == AlgoKind::RING && N > 2;
     if (spec.zc && (spec.kind == AlgoKind::RING || spec.msg)) {
       if (err) *err = "zero-copy (+zc) collectives run the direct exchange over IPC-registered buffers";
@@ -229,13 +239,18 @@ class Planner {
       P->desc = "flat-a2a";
     } else if (coll == Coll::REDUCE_SCATTER) {
       ring ? build_ring_rs(stride) : build_flat_rs(stride);
-      P->desc = ring ? "ring-rs" : "flat-rs";
+      P->desc = ring ? "ring-rs" : wire ? "flat-rs" + spec.str().substr(spec.str().rfind('+')) : "flat-rs";
     } else {
       ring ? build_ring_ag(stride) : build_flat_ag(stride);
       P->desc = ring ? "ring-ag" : "flat-ag";
     }
+    if (wire >= 4 && N > 1) {  // MX scale shadow (see build)
+      P->mx_shadow = round_up(stg);
+      stg = P->mx_shadow + round_up((stg + kMxBlock - 1) / kMxBlock);
+    }
     P->stg_elems = stg;
     P->nchan = (uint32_t)P->chan_start.size() - 1;
+    finish_types(*P);
     mark_runs(*P, r);
     return true;
   }
@@ -883,6 +898,7 @@ class Planner {
     std::vector<Loc> srcs;  // rank order: identical summation order for every block owner
     for (uint32_t p = 0; p < N; ++p)
       srcs.push_back(p == r ? loc(BUF_IN, r, (uint64_t)r * stride) : loc(BUF_STG, r, base + p * m_al));
+    if (wire) std::rotate(srcs.begin(), srcs.begin() + r, srcs.begin() + r + 1);  // typed: own value first
     xfer(m, srcs, {loc(BUF_OUT, r, 0)}, scale);
     finish_channel();
   }

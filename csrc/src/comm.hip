@@ -319,6 +319,13 @@ int run_rs_ag(flexar_comm* c, Coll coll, const void* in, void* out, size_t count
   int rc = resolve_spec(c, algo, (double)count * es * c->nranks, &s, call_kind(dtype, op));
   if (rc) return rc;
   if (s.kind != AlgoKind::RING) s.kind = AlgoKind::TREE, s.widths = {c->nranks}, s.ag = AgMode::PUSH;
+  if (s.wire) {  // the OCP MX wire on the flat reduce-scatter (planner.hpp build_coll); nothing else typed
+    if (coll != Coll::REDUCE_SCATTER || s.wire < 4) {
+      set_error("typed staging on collectives: only the OCP MX wire (+mxe4m3 / +mxe5m2) on the reduce-scatter");
+      return FLEXAR_ERR_UNSUPPORTED;
+    }
+    if ((rc = typed_spec(c, &s, dtype, op, false, (double)count * es * c->nranks))) return rc;
+  }
   if ((rc = executor_proto(c, &s))) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
   // registered buffers and no named spec: the direct exchange runs zero copy (the buffer the peers address
@@ -356,6 +363,8 @@ int run_rs_ag(flexar_comm* c, Coll coll, const void* in, void* out, size_t count
     la.grid = choose_grid(c, n * es * c->nranks, dp->prog.nchan);
     la.stream = st;
     la.proto = proto_of(s);
+    la.wire = dp->prog.wire;
+    la.max_fanin = (int)dp->prog.max_nsrc;
     // all-gather moves bytes only: run the SUM instantiation (the op is never applied, K == 1)
     if ((rc = launch_dtype(dtype, coll == Coll::ALL_GATHER ? FLEXAR_SUM : op, la))) return rc;
     c->launches++;

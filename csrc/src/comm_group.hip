@@ -198,7 +198,7 @@ int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const vo
   float fs = coll == 1 && op == FLEXAR_AVG ? 1.0f / (float)nranks : 1.0f;
   DevCtx* d_ctx = nullptr;
   std::vector<DevCtx> h(nranks);
-  int grid = 0;
+  int grid = 0, wire = 0, fanin = 0;
   int proto = PM_FENCE;
   bool zc = false;
   for (int r = 0; r < nranks; ++r) {
@@ -206,9 +206,18 @@ int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const vo
     int rc = resolve_spec(comms[r], algo, (double)count * es * nranks, &s, call_kind(dtype, op));
     if (rc) return rc;
     if (s.kind != AlgoKind::RING) s.kind = AlgoKind::TREE, s.widths = {nranks}, s.ag = AgMode::PUSH;
+    if (s.wire) {  // the OCP MX wire on the flat reduce-scatter only (as run_rs_ag)
+      if (coll != 1 || s.wire < 4) {
+        set_error("typed staging on collectives: only the OCP MX wire (+mxe4m3 / +mxe5m2) on the reduce-scatter");
+        return FLEXAR_ERR_UNSUPPORTED;
+      }
+      if ((rc = typed_spec(comms[r], &s, dtype, op, false, (double)count * es * nranks))) return rc;
+    }
     proto = proto_of(s);
     DevProgram* dp = nullptr;
     if ((rc = get_program(comms[r], s, count, es, fs, &dp, (Coll)coll, count))) return rc;
+    wire = dp->prog.wire;
+    fanin = std::max(fanin, (int)dp->prog.max_nsrc);
     if (dp->prog.stg_bytes() > comms[r]->exec_half) { set_error("group collective exceeds workspace"); return FLEXAR_ERR_NOMEM; }
     fill_ctx(comms[r], dp, ins[r], outs[r], &h[r]);
     zc = zc || dp->prog.zc;
@@ -224,6 +233,8 @@ int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const vo
   la.grid = grid;
   la.stream = st;
   la.proto = proto;
+  la.wire = wire;
+  la.max_fanin = fanin;
   int rc = launch_dtype(dtype, op, la);
   if (!rc) (void)group_ctx_launched(st);
   if (rc) return rc;

@@ -182,6 +182,16 @@ def _worker(rank, world, port, shared, q, transport="rccl", no_ipc=False, parts=
                     y = comm.all_reduce(xs[rank].to(dev), op="avg", algo=spec)
                     torch.cuda.synchronize()
                 results[("mx_mismatch", str(dtype), spec)] = int((y.cpu().view(torch.uint8) != want.view(torch.uint8)).sum())
+            from allreduce_over_mpi_amd.ops.quant import mx_reduce_scatter_reference
+
+            m = 100003
+            xs = inputs(world * m, 11, torch.bfloat16)
+            want = mx_reduce_scatter_reference(xs, "e4m3", "avg")[rank]
+            out = torch.empty(m, device=dev, dtype=torch.bfloat16)
+            for _ in range(2):
+                comm.reduce_scatter(xs[rank].to(dev), out, op="avg", algo="flat+mxe4m3")
+                torch.cuda.synchronize()
+            results[("mx_mismatch", "rs", "flat+mxe4m3")] = int((out.cpu().view(torch.uint8) != want.view(torch.uint8)).sum())
         if "all" in parts or "colls" in parts:
             m = 4099
             for spec in (None, "ring", "flat+wt"):

@@ -72,3 +72,23 @@ def test_group_mx_wire_keeps_small_blocks(cuda, groups):
     med = lambda y: float(((y - exact).abs() / exact.abs().clamp_min(1e-30)).median())
     assert med(mx) < 0.05, med(mx)
     assert med(glob) > 10 * med(mx), (med(glob), med(mx))
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_group_mx_reduce_scatter_bitwise(cuda, groups, n, dtype):
+    """The MX wire on the flat reduce-scatter, one launch, byte for byte against
+    ops.quant.mx_reduce_scatter_reference (block r of every rank: own value first, then the peers)."""
+    from allreduce_over_mpi_amd.ops.quant import mx_reduce_scatter_reference
+
+    for m, wire, op in ((250001, "e4m3", "avg"), (4099, "e5m2", "sum")):
+        xs = _xs(n, n * m, dtype, seed=n + m)
+        want = mx_reduce_scatter_reference(xs, wire, op)
+        for _ in range(2):
+            outs = [torch.empty(m, device=cuda, dtype=dtype) for _ in range(n)]
+            groups[n].collective("reduce_scatter", [x.to(cuda) for x in xs], outs, op=op, algo=f"flat+mx{wire}")
+            torch.cuda.synchronize()
+            for r, (o, w) in enumerate(zip(outs, want)):
+                bad = (o.cpu().view(torch.uint8) != w.view(torch.uint8)).nonzero().flatten()
+                assert bad.numel() == 0, (n, m, wire, op, r, bad[:8].tolist())
+    groups[n].check()

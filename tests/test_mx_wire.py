@@ -83,3 +83,29 @@ def test_mx_round_is_idempotent():
     x = _inputs(1, 999, torch.float32, seed=3)[0]
     y = mx_round(x, "e4m3")
     assert torch.equal(mx_round(y, "e4m3"), y)
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_reduce_scatter_mx_matches_reference_bitwise(n):
+    """The MX wire on the flat reduce-scatter (FSDP / ZeRO gradient shards): quantising pushes, the owner
+    sums its own value first and then the peers' in rank order, no second rounding of its block."""
+    from allreduce_over_mpi_amd.ops.quant import mx_reduce_scatter_reference
+
+    for dt in (torch.float32, torch.bfloat16):
+        for m in (33, 4099):
+            xs = _inputs(n, n * m, dt, seed=m + n)
+            for wire, op in (("e4m3", "avg"), ("e5m2", "sum")):
+                outs = nv.simulate_coll("reduce_scatter", f"flat+mx{wire}", [_raw(x) for x in xs], m, dtype=DT[dt],
+                                        op=op, grid=3)
+                for r, (o, w) in enumerate(zip(outs, mx_reduce_scatter_reference(xs, wire, op))):
+                    assert np.array_equal(o.view(np.uint8), _raw(w).view(np.uint8)), (n, m, DT[dt], wire, op, r)
+
+
+def test_mx_wire_only_on_allreduce_and_reduce_scatter():
+    ins = [np.ones(4 * 256, np.float32)] * 4
+    for coll in ("all_gather", "all_to_all"):
+        with pytest.raises(nv.FlexarError):
+            nv.simulate_coll(coll, "flat+mxe4m3", [np.ones(256 if coll == "all_gather" else 1024, np.float32)] * 4,
+                             256)
+    with pytest.raises(nv.FlexarError):  # the ring reduce-scatter has no typed form
+        nv.simulate_coll("reduce_scatter", "ring+mxe4m3", ins, 256)
