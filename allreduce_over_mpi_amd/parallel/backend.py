@@ -208,6 +208,12 @@ class FlexarProcessGroup(dist.ProcessGroup):
                 and nv.lib() is not None and (opname != "avg" or tensors[0].is_floating_point())
                 and not (opname in ("band", "bor", "bxor") and tensors[0].is_floating_point()))
 
+    def _rs_algo(self, t, opname):
+        """Reduce-scatter spec: the OCP MX wire under FLEXAR_PG_COMPRESS (the flat reduce-scatter's typed
+        form: FSDP / ZeRO gradient shards), otherwise the library's choice."""
+        a = self._compress_algo(t, opname) if self._compress or not self._compress_agreed else None
+        return a if a and "+mx" in a else None
+
     def _compress_algo(self, t, opname):
         """The spec of this allreduce under FLEXAR_PG_COMPRESS, or the plain one (self.algo)."""
         if not self._compress_agreed:  # once, collectively: every rank's setting the same
@@ -447,7 +453,7 @@ class FlexarProcessGroup(dist.ProcessGroup):
                 def run(c):
                     flat = torch.cat([t.reshape(-1) for t in chunks])
                     res = torch.empty(out.numel(), dtype=out.dtype, device=out.device)
-                    c.reduce_scatter(flat, res, op=opname)
+                    c.reduce_scatter(flat, res, op=opname, algo=self._rs_algo(flat, opname))
                     out.copy_(res.view_as(out))
                 return self._on_side([out] + list(chunks), run, output_tensors)
         return self._fallback(output_tensors).reduce_scatter(output_tensors, input_tensors, opts)
@@ -457,7 +463,8 @@ class FlexarProcessGroup(dist.ProcessGroup):
         if self._flexar_ok([input_tensor, output_tensor], opname) and input_tensor.dtype != torch.bool and \
                 input_tensor.numel() == output_tensor.numel() * self._world and self._flat_comm_ok(input_tensor):
             return self._on_side([input_tensor, output_tensor],
-                                 lambda c: c.reduce_scatter(input_tensor, output_tensor, op=opname), [output_tensor])
+                                 lambda c: c.reduce_scatter(input_tensor, output_tensor, op=opname,
+                                                            algo=self._rs_algo(input_tensor, opname)), [output_tensor])
         return self._fallback([input_tensor])._reduce_scatter_base(output_tensor, input_tensor, opts)
 
     def _on_side(self, tensors, fn, result):
@@ -486,7 +493,7 @@ class FlexarProcessGroup(dist.ProcessGroup):
 
         def run(c):
             for o, i in zip(output_tensors, input_tensors):
-                c.reduce_scatter(i, o, op=opname)
+                c.reduce_scatter(i, o, op=opname, algo=self._rs_algo(i, opname))
         return self._on_side(list(input_tensors) + list(output_tensors), run, list(output_tensors))
 
     def alltoall_base(self, output, input, output_split_sizes, input_split_sizes, opts=AllToAllOptions()):

@@ -482,3 +482,39 @@ def test_functional_collectives_over_flexar(cuda):
     for rank, err, used, tb in _spawn(_funcol, 2):
         assert tb is None, tb
         assert err == 0.0 and used >= 3, (rank, err, used)
+
+
+def _compressed_rs(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16", FLEXAR_PG_ZC="0",
+                          FLEXAR_PG_COMPRESS="mx_e4m3", FLEXAR_PG_COMPRESS_MIN_BYTES="0")
+        _fallback_env(rank, "gloo")
+        import torch.distributed as dist
+
+        import allreduce_over_mpi_amd.parallel.backend  # noqa: F401  registers "flexar"
+        from allreduce_over_mpi_amd.ops.quant import mx_reduce_scatter_reference
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("flexar", rank=rank, world_size=world)
+        m = 65537
+        xs = [torch.randn(world * m, generator=torch.Generator().manual_seed(50 + r)) for r in range(world)]
+        out = torch.empty(m, device="cuda")
+        dist.reduce_scatter_tensor(out, xs[rank].cuda(), op=dist.ReduceOp.AVG)
+        torch.cuda.synchronize()
+        want = mx_reduce_scatter_reference(xs, "e4m3", "avg")[rank]
+        bad = int((out.cpu().view(torch.uint8) != want.view(torch.uint8)).sum())
+        stats = dict(dist.group.WORLD.stats)
+        dist.destroy_process_group()
+        q.put((rank, bad, stats, None))
+    except Exception:
+        import traceback
+
+        q.put((rank, None, None, traceback.format_exc()))
+
+
+def test_backend_compressed_reduce_scatter(cuda):
+    """FLEXAR_PG_COMPRESS=mx_e4m3: the backend's reduce_scatter_tensor (FSDP's gradient path) runs the flat
+    reduce-scatter with the OCP MX wire, byte for byte the reference arithmetic."""
+    for rank, bad, stats, tb in _spawn(_compressed_rs, 2):
+        assert tb is None, tb
+        assert bad == 0, (rank, bad)
