@@ -30,6 +30,26 @@ def main():
     g = torch.Generator(device="cuda").manual_seed(1)
     xs = [torch.randn(count, device="cuda", generator=g).to(dt) for _ in range(n)]
     ys = [torch.empty_like(x) for x in xs]
+    coll = os.environ.get("TEP_COLL", "all_reduce")
+    if coll == "reduce_scatter":  # MIB per rank of input, MIB / N of output; "+mx..." specs: the MX wire
+        m = count // n
+        ins = [x[: n * m] for x in xs]
+        outs = [torch.empty(m, device="cuda", dtype=dt) for _ in range(n)]
+        op = "avg" if "+mx" in spec else "sum"
+        run = lambda: grp.collective("reduce_scatter", ins, outs, op=op, algo=spec)  # noqa: E731
+        for _ in range(3):
+            run()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(iters):
+            run()
+        b.record()
+        torch.cuda.synchronize()
+        print(json.dumps({"coll": coll, "spec": spec, "dtype": dtype, "ranks": n, "mib_per_rank": mib,
+                          "us_per_call": round(a.elapsed_time(b) * 1e3 / iters, 1)}), flush=True)
+        grp.close()
+        return
     if spec == "fp8":
         from allreduce_over_mpi_amd.ops.quant import fp8_amax
 
