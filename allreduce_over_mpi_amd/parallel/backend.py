@@ -116,7 +116,7 @@ class FlexarProcessGroup(dist.ProcessGroup):
         self._zc_sweep_every = max(1, int(os.environ.get("FLEXAR_PG_ZC_SWEEP", "16") or 16))
         self._ar_calls = 0
         # opt-in lossy compression of the float SUM / AVG allreduces of at least FLEXAR_PG_COMPRESS_MIN_BYTES
-        # (1 MiB), for DDP / any caller of init_process_group("flexar") without a comm hook:
+        # (4 MiB), for DDP / any caller of init_process_group("flexar") without a comm hook:
         # FLEXAR_PG_COMPRESS=mx_e4m3 | mx_e5m2 puts OCP MX fp8 on the links (a scale per 32-element block,
         # one launch: docs/DESIGN.md §9.2). Every rank must set the same value: the first allreduce checks
         # it collectively (a mismatch would compile different schedules on different ranks).
@@ -124,7 +124,9 @@ class FlexarProcessGroup(dist.ProcessGroup):
         if comp not in _COMPRESS:
             raise ValueError(f"FLEXAR_PG_COMPRESS={comp!r}: expected one of {sorted(k for k in _COMPRESS if k)}")
         self._compress = _COMPRESS[comp]
-        self._compress_min = int(os.environ.get("FLEXAR_PG_COMPRESS_MIN_BYTES", str(1 << 20)))
+        # below a few MiB a call is latency-bound and the quantisation only adds work (profiles/r4_layout: MX
+        # 63-67 us vs 46 us uncompressed at 1 MiB on one GPU)
+        self._compress_min = int(os.environ.get("FLEXAR_PG_COMPRESS_MIN_BYTES", str(4 << 20)))
         self._compress_agreed = False
 
     # ------------------------------------------------------------------ plumbing

@@ -167,8 +167,8 @@ def _compress_worker(rank, world, port, settings, q):
         dist.init_process_group("flexar", rank=rank, world_size=world)
         pg = dist.group.WORLD
         try:
-            picks = [pg._compress_algo(torch.zeros(1 << 18), "avg"),  # 1 MiB fp32: compressed
-                     pg._compress_algo(torch.zeros(1 << 18, dtype=torch.bfloat16), "sum"),  # 512 KiB: too small
+            picks = [pg._compress_algo(torch.zeros(1 << 20), "avg"),  # 4 MiB fp32: compressed
+                     pg._compress_algo(torch.zeros(1 << 20, dtype=torch.bfloat16), "sum"),  # 2 MiB: too small
                      pg._compress_algo(torch.zeros(1 << 18, dtype=torch.int32), "sum"),
                      pg._compress_algo(torch.zeros(1 << 18), "max")]
             err = None
@@ -184,7 +184,7 @@ def _compress_worker(rank, world, port, settings, q):
 
 @pytest.mark.parametrize("settings", [("mx_e4m3", "mx_e4m3"), ("mx_e4m3", "")])
 def test_backend_compression_option_is_agreed(settings):
-    """FLEXAR_PG_COMPRESS: float SUM / AVG allreduces of >= 1 MiB get the OCP MX wire; the setting is agreed
+    """FLEXAR_PG_COMPRESS: float SUM / AVG allreduces of >= 4 MiB get the OCP MX wire; the setting is agreed
     on the first call and a mismatch fails on every rank (it would compile different schedules)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
