@@ -412,7 +412,7 @@ def direct_links(classes, hops, self_rank: int) -> int:
 def kernel_info(dtype="float32", op="sum", kind: int = 0, proto: int = 0) -> dict:
     """Occupancy (512-thread workgroups per CU) and VGPRs of one kernel instantiation (needs a GPU).
     kind: 0 executor (proto 0 fence / 1 nts / 2 wt), 1 LL, 2 reduce, 3/4/5 typed executor (fp32 partials /
-    e4m3 wire / e5m2 wire)."""
+    e4m3 wire / e5m2 wire), 6/7 typed executor with the OCP MX e4m3 / e5m2 wire (the fan-in-8 class)."""
     occ, regs = ctypes.c_int(0), ctypes.c_int(0)
     check(lib().flexar_kernel_info(dtype_code(dtype), op_code(op), kind, proto, ctypes.byref(occ), ctypes.byref(regs)),
           "kernel_info")

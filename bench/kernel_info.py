@@ -28,7 +28,8 @@ def main():
                 print(json.dumps({"kernel": name, "dtype": dt, "proto": protos[p] if kind == 0 else None, **k,
                                   "resident_blocks": k["blocks_per_cu"] * cus}), flush=True)
     for dt, kind, name in (("bfloat16", 3, "exec_mx fp32 partials"), ("fp8_e4m3", 3, "exec_mx fp32 partials"),
-                           ("float32", 4, "exec_mx e4m3 wire"), ("bfloat16", 4, "exec_mx e4m3 wire")):
+                           ("float32", 4, "exec_mx e4m3 wire"), ("bfloat16", 4, "exec_mx e4m3 wire"),
+                           ("float32", 6, "exec_mx MX e4m3 wire"), ("bfloat16", 6, "exec_mx MX e4m3 wire")):
         for p in (0, 2):
             k = nv.kernel_info(dt, "sum", kind, p)
             print(json.dumps({"kernel": name, "dtype": dt, "proto": protos[p], **k,
