@@ -92,3 +92,14 @@ def test_group_mx_reduce_scatter_bitwise(cuda, groups, n, dtype):
                 bad = (o.cpu().view(torch.uint8) != w.view(torch.uint8)).nonzero().flatten()
                 assert bad.numel() == 0, (n, m, wire, op, r, bad[:8].tolist())
     groups[n].check()
+
+
+def test_kernel_info_reports_every_executor_class(cuda):
+    """flexar_kernel_info for the untyped, fp32-partials, global-scale fp8 and MX executors: each fits at least
+    one 512-thread workgroup per CU (the protocol's co-residency assumption, choose_grid)."""
+    from allreduce_over_mpi_amd import _native as nv
+
+    for dt, kind in (("float32", 0), ("bfloat16", 3), ("float32", 4), ("float32", 6), ("bfloat16", 7)):
+        for proto in (0, 2):
+            k = nv.kernel_info(dt, "sum", kind, proto)
+            assert k["blocks_per_cu"] >= 1 and 0 < k["vgprs"] <= 256, (dt, kind, proto, k)
