@@ -809,7 +809,8 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
     finish_group(v, raw);
   }
   }
-  // scalar tail (or the whole span when a caller buffer is not 16-B aligned)
+  // scalar tail: the last < G elements (or the whole span when FLEXAR_SCALAR_MISALIGNED=1 and a caller buffer is
+  // not 16-B aligned)
   for (uint64_t i = ng * G + threadIdx.x; i < n; i += nt) {
     float acc = 0.0f;
 #pragma unroll
