@@ -142,6 +142,7 @@ inline Partials partials_from_env() {
 struct CallKind {
   uint32_t esize = 4;
   bool narrow_sum = false;
+  bool wire_ok = false;  // fp32 / bf16 / fp16 SUM or AVG: an fp8 wire can carry it
 };
 
 // times a multi-hop schedule rounds its partials when they travel in the call's dtype

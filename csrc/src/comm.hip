@@ -41,6 +41,8 @@ CallKind call_kind(int dtype, int op) {
   k.narrow_sum = (op == FLEXAR_SUM || op == FLEXAR_AVG) &&
                  (dtype == FLEXAR_BFLOAT16 || dtype == FLEXAR_FLOAT16 || dtype == FLEXAR_FP8_E4M3 ||
                   dtype == FLEXAR_FP8_E5M2);
+  k.wire_ok = (op == FLEXAR_SUM || op == FLEXAR_AVG) &&
+              (dtype == FLEXAR_FLOAT32 || dtype == FLEXAR_BFLOAT16 || dtype == FLEXAR_FLOAT16);
   return k;
 }
 
@@ -60,6 +62,11 @@ int resolve_spec(flexar_comm* c, const char* algo, double bytes, AlgoSpec* out, 
       s = select_plan(c->model, c->nranks, bytes, nullptr, k);
     }
   }
+  // an fp8 wire in the communicator's default spec (FLEXAR_ALGO / FT_TOPO) applies to the calls it can carry:
+  // the MX wire to fp32 / bf16 / fp16 SUM / AVG, the global-scale wire only through flexar_allreduce_fp8
+  // (which names its own spec); every other call runs untyped instead of failing. A per-call spec is
+  // taken as written.
+  if (!(algo && *algo) && s.wire >= 2 && (s.wire < 4 || !k.wire_ok)) s.wire = 0;
   if (s.kind == AlgoKind::TREE && s.ag == AgMode::AUTO) s.ag = AgMode::PULL;
   if (!c->ipc) s.msg = true;  // no peer memory: every schedule runs over the message transport
   if (c->disabled) {
@@ -319,6 +326,7 @@ int run_rs_ag(flexar_comm* c, Coll coll, const void* in, void* out, size_t count
   int rc = resolve_spec(c, algo, (double)count * es * c->nranks, &s, call_kind(dtype, op));
   if (rc) return rc;
   if (s.kind != AlgoKind::RING) s.kind = AlgoKind::TREE, s.widths = {c->nranks}, s.ag = AgMode::PUSH;
+  if (s.wire && coll != Coll::REDUCE_SCATTER && !(algo && *algo)) s.wire = 0;  // a default-spec wire: RS only
   if (s.wire) {  // the OCP MX wire on the flat reduce-scatter (planner.hpp build_coll); nothing else typed
     if (coll != Coll::REDUCE_SCATTER || s.wire < 4) {
       set_error("typed staging on collectives: only the OCP MX wire (+mxe4m3 / +mxe5m2) on the reduce-scatter");

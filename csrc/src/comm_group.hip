@@ -206,6 +206,7 @@ int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const vo
     int rc = resolve_spec(comms[r], algo, (double)count * es * nranks, &s, call_kind(dtype, op));
     if (rc) return rc;
     if (s.kind != AlgoKind::RING) s.kind = AlgoKind::TREE, s.widths = {nranks}, s.ag = AgMode::PUSH;
+    if (s.wire && coll != 1 && !(algo && *algo)) s.wire = 0;  // a default-spec wire: reduce-scatter only
     if (s.wire) {  // the OCP MX wire on the flat reduce-scatter only (as run_rs_ag)
       if (coll != 1 || s.wire < 4) {
         set_error("typed staging on collectives: only the OCP MX wire (+mxe4m3 / +mxe5m2) on the reduce-scatter");

@@ -103,3 +103,29 @@ def test_kernel_info_reports_every_executor_class(cuda):
         for proto in (0, 2):
             k = nv.kernel_info(dt, "sum", kind, proto)
             assert k["blocks_per_cu"] >= 1 and 0 < k["vgprs"] <= 256, (dt, kind, proto, k)
+
+
+def test_default_spec_wire_applies_only_where_it_can(cuda, monkeypatch):
+    """FLEXAR_ALGO=flat+mxe4m3 as the communicator default: float SUM / AVG allreduces and reduce-scatters take
+    the MX wire; integer / MAX allreduces and the all-gather run untyped instead of failing."""
+    from allreduce_over_mpi_amd.parallel import LocalGroup
+
+    monkeypatch.setenv("FLEXAR_ALGO", "flat+mxe4m3")
+    n, count = 4, 4096
+    grp = LocalGroup(n, workspace_bytes=32 << 20)
+    try:
+        xs = _xs(n, count, torch.float32, seed=3)
+        outs = grp.all_reduce([x.to(cuda) for x in xs], "avg")
+        want = mx_allreduce_reference(xs, "e4m3", "avg")
+        assert torch.equal(outs[0].cpu().view(torch.uint8), want.view(torch.uint8))
+        ints = [torch.full((count,), r + 1, dtype=torch.int32, device=cuda) for r in range(n)]
+        assert bool((grp.all_reduce(ints, "sum")[0] == n * (n + 1) // 2).all())
+        fl = [torch.full((count,), float(r), device=cuda) for r in range(n)]
+        assert bool((grp.all_reduce(fl, "max")[0] == n - 1).all())
+        ag_in = [torch.full((count,), float(r), device=cuda) for r in range(n)]
+        ag_out = [torch.empty(n * count, device=cuda) for _ in range(n)]
+        grp.collective("all_gather", ag_in, ag_out)
+        assert torch.equal(ag_out[1].cpu(), torch.arange(n).float().repeat_interleave(count))
+        grp.check()
+    finally:
+        grp.close()
