@@ -332,7 +332,10 @@ def main():
         log(rank, f"flexar communicator unavailable on this node ({err}); measuring RCCL instead")
         return None
 
+    t_phase = time.perf_counter()
     comm = make_comm()
+    # start-up phases on stderr (rank 0): a failure early in a run then names the phase it reached
+    log(rank, f"phase: communicator ready after {time.perf_counter() - t_phase:.1f} s")
     if comm is None:
         comm, fallback = RcclOnly(dist), "flexar communicator could not be created"
     # the three buffers first, each its own allocation (registration maps whole allocations into the peers;
@@ -396,6 +399,7 @@ def main():
         if world > 1:
             dist.all_reduce(ref, op=dist.ReduceOp.AVG if op == "avg" else dist.ReduceOp.SUM)
     ref_f = ref.float()
+    log(rank, f"phase: RCCL reference ready after {time.perf_counter() - t_phase:.1f} s")
     ref_max = float(ref_f.abs().max().item()) + 1e-6
     tol = {torch.float32: 1e-5, torch.bfloat16: 2e-2, torch.float16: 4e-3, torch.float8_e4m3fn: 0.13}[dtype]
     tol = tol * math.sqrt(world) * 4 if dtype != torch.float8_e4m3fn else tol
