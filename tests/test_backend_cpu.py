@@ -170,7 +170,9 @@ def _compress_worker(rank, world, port, settings, q):
             picks = [pg._compress_algo(torch.zeros(1 << 20), "avg"),  # 4 MiB fp32: compressed
                      pg._compress_algo(torch.zeros(1 << 20, dtype=torch.bfloat16), "sum"),  # 2 MiB: too small
                      pg._compress_algo(torch.zeros(1 << 18, dtype=torch.int32), "sum"),
-                     pg._compress_algo(torch.zeros(1 << 18), "max")]
+                     pg._compress_algo(torch.zeros(1 << 18), "max"),
+                     pg._rs_algo(torch.zeros(1 << 21, dtype=torch.bfloat16), "avg"),  # reduce-scatter input
+                     pg._rs_algo(torch.zeros(16), "sum")]
             err = None
         except RuntimeError as e:
             picks, err = None, str(e)
@@ -198,6 +200,7 @@ def test_backend_compression_option_is_agreed(settings):
     for rank, picks, err, tb in res:
         assert tb is None, tb
         if settings[0] == settings[1]:
-            assert err is None and picks == ["flat+pull+mxe4m3", None, None, None], (rank, picks, err)
+            assert err is None and picks == ["flat+pull+mxe4m3", None, None, None, "flat+pull+mxe4m3", None], \
+                (rank, picks, err)
         else:
             assert picks is None and "differs across ranks" in err, (rank, picks, err)
