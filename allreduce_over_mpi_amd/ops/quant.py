@@ -88,7 +88,7 @@ def mx_scale_bytes(x, wire: str = "e4m3"):
     pad = (-n) % MX_BLOCK
     bits = x.float().contiguous().view(torch.int32).to(torch.int64) & 0x7FFFFFFF
     if pad:
-        bits = torch.cat([bits, torch.zeros(pad, dtype=torch.int64)])
+        bits = torch.cat([bits, torch.zeros(pad, dtype=torch.int64, device=bits.device)])
     am = bits.view(-1, MX_BLOCK).amax(1)
     e = (am >> 23) - _MX_EMAX[wire] + ((am & 0x7FFFFF) > 0x600000).to(torch.int64)
     return e.clamp(1, 254)
@@ -96,7 +96,8 @@ def mx_scale_bytes(x, wire: str = "e4m3"):
 
 def mx_quantize(x, wire: str = "e4m3"):
     """(q, scale bytes): the fp8 values q = rne(x / 2^X) of every block of the fp32 tensor ``x`` and the blocks'
-    e8m0 bytes - what the MX executor puts on the wire."""
+    e8m0 bytes - what the MX executor puts on the wire. Works on CPU and ROCm tensors (torch ops: the
+    hierarchical communicator's cross-node compression uses it on the device)."""
     import torch
 
     sb = mx_scale_bytes(x, wire)
@@ -164,3 +165,11 @@ def mx_reduce_scatter_reference(inputs, wire: str = "e4m3", op: str = "sum"):
             acc = acc * torch.tensor(1.0 / n, dtype=torch.float32)
         outs.append(acc.to(dt))
     return outs
+
+
+def mx_dequantize(q, scale_bytes, numel: int):
+    """fp32 values q * 2^X of an MX payload (``q`` float8, ``scale_bytes`` one e8m0 byte per 32 elements)."""
+    import torch
+
+    sc = torch.pow(2.0, (scale_bytes.to(torch.int64) - 127).double()).float().repeat_interleave(MX_BLOCK)[:numel]
+    return q.float() * sc

@@ -124,6 +124,7 @@ class FlexarProcessGroup(dist.ProcessGroup):
         if comp not in _COMPRESS:
             raise ValueError(f"FLEXAR_PG_COMPRESS={comp!r}: expected one of {sorted(k for k in _COMPRESS if k)}")
         self._compress = _COMPRESS[comp]
+        self._compress_name = comp if self._compress else None
         # below a few MiB a call is latency-bound and the quantisation only adds work (profiles/r4_layout: MX
         # 63-67 us vs 46 us uncompressed at 1 MiB on one GPU)
         self._compress_min = int(os.environ.get("FLEXAR_PG_COMPRESS_MIN_BYTES", str(4 << 20)))
@@ -210,6 +211,11 @@ class FlexarProcessGroup(dist.ProcessGroup):
                 and nv.lib() is not None and (opname != "avg" or tensors[0].is_floating_point())
                 and not (opname in ("band", "bor", "bxor") and tensors[0].is_floating_point()))
 
+    def _compress_eligible(self, t, opname):
+        return (self._compress is not None and self._world > 1 and opname in ("sum", "avg")
+                and t.dtype in (torch.float32, torch.bfloat16, torch.float16)
+                and t.numel() * t.element_size() >= self._compress_min)
+
     def _rs_algo(self, t, opname):
         """Reduce-scatter spec: the OCP MX wire under FLEXAR_PG_COMPRESS (the flat reduce-scatter's typed
         form: FSDP / ZeRO gradient shards), otherwise the library's choice."""
@@ -227,9 +233,7 @@ class FlexarProcessGroup(dist.ProcessGroup):
             if int(t2[0]) != -int(t2[1]):  # min != max
                 raise RuntimeError("FLEXAR_PG_COMPRESS differs across ranks: every rank must set the same value")
             self._compress_agreed = True
-        if (self._compress is None or self.hierarchical or self._world < 2 or opname not in ("sum", "avg")
-                or t.dtype not in (torch.float32, torch.bfloat16, torch.float16)
-                or t.numel() * t.element_size() < self._compress_min):
+        if self.hierarchical or not self._compress_eligible(t, opname):
             return self.algo
         base = (self.algo or "flat+pull").replace("+zc", "")  # the MX wire runs on staging (no registration)
         return base + self._compress
@@ -262,9 +266,14 @@ class FlexarProcessGroup(dist.ProcessGroup):
                     comm.all_reduce(t8, op=boolop, algo=self.algo)
                 else:
                     algo = self._compress_algo(t, opname) if self._compress or not self._compress_agreed else self.algo
-                    comm.all_reduce(t, op=opname, algo=algo)
-                    if algo is not self.algo:
+                    if self.hierarchical and self._compress and self._compress_eligible(t, opname):
+                        # several nodes: the intra-node steps stay exact, the network carries OCP MX fp8
+                        comm.all_reduce(t, op=opname, algo=self.algo, compress=self._compress_name)
                         self.stats["compressed"] = self.stats.get("compressed", 0) + 1
+                    else:
+                        comm.all_reduce(t, op=opname, algo=algo)
+                        if algo is not self.algo:
+                            self.stats["compressed"] = self.stats.get("compressed", 0) + 1
                 self.stats["flexar_allreduce"] += 1
             fut = torch.futures.Future(devices=[dev])
             fut.set_result(tensor_list)  # records an event on the side stream; wait() joins it

@@ -131,10 +131,45 @@ class HierarchicalCommunicator:
             t.copy_(h)
         return t
 
-    def all_reduce(self, tensor, op: str = "sum", out=None, algo: Optional[str] = None):
+    def _cross_gather(self, x):
+        """Every node's ``x`` (same shape) over the cross-node group, in node order."""
+        dist = self._dist
+        h = x.cpu() if self.cross_on_host else x
+        outs = [self._torch.empty_like(h) for _ in range(self.nodes)]
+        if self.cross_pg is not None:
+            self.cross_pg.allgather([outs], [h]).wait()
+        else:
+            dist.all_gather(outs, h, group=self.cross_group)
+        return [o.to(x.device) for o in outs]
+
+    def _cross_all_reduce_mx(self, t, wire: str):
+        """Cross-node SUM of a float shard with OCP MX fp8 on the network (a scale per 32-element block): each
+        node's shard is quantised once, the payloads and scales are all-gathered (1.03 bytes per element per
+        node instead of a ring allreduce's 2 (n-1)/n x 4), and every node sums the dequantised shards in node
+        order in fp32 - identical results everywhere. Worth it for up to ~4 nodes, where the all-gather moves
+        fewer bytes than the ring."""
+        from ..ops.quant import mx_dequantize, mx_quantize
+
+        if self.nodes == 1:
+            return t
+        q, sb = mx_quantize(t.float(), wire)
+        payloads = self._cross_gather(q.view(self._torch.uint8))
+        scales = self._cross_gather(sb.to(self._torch.uint8))
+        fp8 = q.dtype
+        acc = None
+        for p, s in zip(payloads, scales):
+            v = mx_dequantize(p.view(fp8), s, t.numel())
+            acc = v if acc is None else acc + v
+        t.copy_(acc.to(t.dtype))
+        return t
+
+    def all_reduce(self, tensor, op: str = "sum", out=None, algo: Optional[str] = None,
+                   compress: Optional[str] = None):
         """Allreduce ``tensor`` over every rank of every node (in place unless ``out`` is given).
         ops: sum, avg (sum then the 1/world scale), max, min, prod. ``algo`` picks the intra-node
-        reduce-scatter / all-gather form ("ring" or the direct exchange). Drop-in for a DDP hook state:
+        reduce-scatter / all-gather form ("ring" or the direct exchange). ``compress="mx_e4m3"`` /
+        ``"mx_e5m2"`` (float SUM / AVG): the cross-node step carries OCP MX fp8 (_cross_all_reduce_mx); the
+        intra-node steps stay exact. Drop-in for a DDP hook state:
         ``FlexarHookState(communicator=HierarchicalCommunicator())``."""
         torch = self._torch
         dst = tensor if out is None else out
@@ -148,7 +183,10 @@ class HierarchicalCommunicator:
         if m > 0:
             shard = torch.empty(m, dtype=flat.dtype, device=flat.device)
             self.local.reduce_scatter(flat[:main], shard, op=red, algo=algo)
-            self._cross_all_reduce(shard, red)
+            if compress and red == "sum" and flat.is_floating_point():
+                self._cross_all_reduce_mx(shard, {"mx_e4m3": "e4m3", "mx_e5m2": "e5m2"}[compress])
+            else:
+                self._cross_all_reduce(shard, red)
             self.local.all_gather(shard, flat[:main], algo=algo)
         if main < n:  # fewer than L trailing elements: node allreduce, then across nodes
             tail = flat[main:].clone()

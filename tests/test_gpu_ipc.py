@@ -172,6 +172,67 @@ def _hier_worker(rank, world, port, q):
         q.put((rank, None, traceback.format_exc()))
 
 
+def _hier_mx_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
+                          FLEXAR_TIMEOUT_MS="20000")
+        import torch.distributed as dist
+
+        from allreduce_over_mpi_amd.ops.quant import mx_round
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from allreduce_over_mpi_amd.parallel import HierarchicalCommunicator
+
+        hc = HierarchicalCommunicator(node_size=2, workspace_bytes=32 << 20)  # 2 virtual nodes x 2 ranks
+        dev = torch.device("cuda", 0)
+        errs = []
+        for size, wire, op in ((4096, "mx_e4m3", "sum"), (300002, "mx_e4m3", "avg"), (65538, "mx_e5m2", "sum")):
+            xs = [torch.randn(size, generator=torch.Generator().manual_seed(10 * r + size)) * (1 + r) for r in range(world)]
+            m = size // 2
+            want = torch.empty(size)
+            for l in range(2):  # local rank l owns shard l: node sums (exact pairs), MX per node, node order
+                sl = slice(l * m, (l + 1) * m)
+                nodes = [xs[2 * k][sl] + xs[2 * k + 1][sl] for k in range(2)]
+                want[sl] = mx_round(nodes[0], wire[3:]) + mx_round(nodes[1], wire[3:])
+            if op == "avg":
+                want.mul_(1.0 / world)
+            y = hc.all_reduce(xs[rank].to(dev), op=op, compress=wire)
+            torch.cuda.synchronize()
+            exact = torch.stack([x.double() for x in xs]).sum(0) * (1.0 / world if op == "avg" else 1.0)
+            rel = ((y.double().cpu() - exact).abs().max() / exact.abs().max()).item()
+            errs.append((size, wire, int((y.cpu() != want).sum()), rel))
+        hc.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, errs, None))
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_hierarchical_allreduce_mx_cross_node(cuda):
+    """compress="mx_e4m3"/"mx_e5m2": exact intra-node reduce-scatter, OCP MX fp8 shards all-gathered across the
+    (virtual) nodes and summed in node order - bitwise the torch reference, the same on every rank."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hier_mx_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(4)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, errs, tb in res:
+        assert tb is None, tb
+        for size, wire, mism, rel in errs:
+            assert mism == 0, (rank, size, wire, mism)
+            assert rel < (0.07 if wire == "mx_e4m3" else 0.13), (rank, size, wire, rel)
+
+
 def test_hierarchical_allreduce_virtual_nodes(cuda):
     """Intra-node flexar RS/AG over IPC + cross-node allreduce of 1/L shards (2 virtual nodes x 2 ranks)."""
     import torch.multiprocessing as mp
