@@ -371,6 +371,50 @@ def test_backend_hierarchical_virtual_nodes(cuda, fallback):
         assert err == 0.0 and ok, (rank, err, ok)
 
 
+def _hier_backend_mx(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
+                          FLEXAR_TIMEOUT_MS="20000", FLEXAR_NODE_SIZE="2", FLEXAR_PG_FALLBACK="gloo",
+                          FLEXAR_PG_COMPRESS="mx_e4m3", FLEXAR_PG_COMPRESS_MIN_BYTES="65536")
+        import torch.distributed as dist
+
+        from allreduce_over_mpi_amd.ops.quant import mx_round
+        from allreduce_over_mpi_amd.parallel import backend as fb  # noqa: F401
+
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        dist.init_process_group("flexar", rank=rank, world_size=world)
+        n = 100002
+        xs = [torch.randn(n, generator=torch.Generator().manual_seed(7 + r)) for r in range(world)]
+        m = n // 2
+        want = torch.empty(n)
+        for l in range(2):  # exact node pairs, MX per node shard, node order
+            sl = slice(l * m, (l + 1) * m)
+            want[sl] = mx_round(xs[0][sl] + xs[1][sl]) + mx_round(xs[2][sl] + xs[3][sl])
+        x = xs[rank].to(dev)
+        dist.all_reduce(x)  # 400 KB >= the 64 KiB threshold: compressed across nodes
+        small = torch.full((1000,), float(rank), device=dev)
+        dist.all_reduce(small)  # under the threshold: exact
+        pg = dist.group.WORLD
+        res = (int((x.cpu() != want).sum()), (small - 6).abs().max().item(), pg.stats.get("compressed", 0))
+        dist.destroy_process_group()
+        q.put((rank, res, None))
+    except Exception:
+        import traceback
+
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_backend_hierarchical_compressed(cuda):
+    """FLEXAR_NODE_SIZE=2 + FLEXAR_PG_COMPRESS=mx_e4m3: dist.all_reduce keeps the intra-node steps exact and
+    carries OCP MX fp8 across the (virtual) nodes - bitwise the torch reference; calls under the threshold
+    stay exact."""
+    for rank, res, tb in _spawn(_hier_backend_mx, 4):
+        assert tb is None, tb
+        mism, small_err, compressed = res
+        assert mism == 0 and small_err == 0.0 and compressed == 1, (rank, res)
+
+
 def _fsdp_worker(rank, world, port, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLEXAR_MAX_GRID="16",
