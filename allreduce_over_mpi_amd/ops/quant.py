@@ -173,3 +173,45 @@ def mx_dequantize(q, scale_bytes, numel: int):
 
     sc = torch.pow(2.0, (scale_bytes.to(torch.int64) - 127).double()).float().repeat_interleave(MX_BLOCK)[:numel]
     return q.float() * sc
+
+
+_MX_WIRE_CODES = {"e4m3": 4, "e5m2": 5}
+
+
+def mx_message_bytes(n: int) -> int:
+    """Bytes of an MX message of ``n`` elements: the fp8 values, then one scale byte per 32-element block."""
+    return n + (n + MX_BLOCK - 1) // MX_BLOCK
+
+
+def mx_pack(x, wire: str = "e4m3", out=None, stream=None):
+    """Native MX codec (csrc/src/k_mx_codec.hip): the uint8 message [q | scale bytes] of the contiguous
+    f32 / bf16 / f16 ROCm tensor ``x`` in one HBM pass - bitwise ``mx_quantize`` (fp8 bytes, then the scale
+    bytes)."""
+    import torch
+
+    if not x.is_cuda or not x.is_contiguous():
+        raise nv.FlexarError(1, "x must be a contiguous ROCm tensor")
+    n = x.numel()
+    msg = torch.empty(mx_message_bytes(n), dtype=torch.uint8, device=x.device) if out is None else out
+    if msg.numel() < mx_message_bytes(n) or msg.dtype != torch.uint8 or not msg.is_contiguous():
+        raise nv.FlexarError(1, "mx_pack: out must be contiguous uint8 of mx_message_bytes(n)")
+    nv.check(nv.lib().flexar_mx_pack(x.data_ptr(), nv.dtype_code(x.dtype), msg.data_ptr(), n,
+                                     _MX_WIRE_CODES[wire], _stream_handle(stream)), "mx_pack")
+    return msg
+
+
+def mx_unpack_sum(msgs, n: int, wire: str = "e4m3", out=None, stream=None):
+    """Sum of the dequantised MX messages ``msgs`` (uint8 [k, >= mx_message_bytes(n)], contiguous) in row
+    order, fp32, in one pass (csrc/src/k_mx_codec.hip) - bitwise ``mx_dequantize`` of each row summed in
+    order."""
+    import torch
+
+    if not msgs.is_cuda or msgs.dim() != 2 or msgs.dtype != torch.uint8 or not msgs.is_contiguous():
+        raise nv.FlexarError(1, "msgs must be a contiguous 2-D uint8 ROCm tensor")
+    y = torch.empty(n, dtype=torch.float32, device=msgs.device) if out is None else out
+    if y.dtype != torch.float32 or y.numel() != n or not y.is_contiguous():
+        raise nv.FlexarError(1, "mx_unpack_sum: out must be contiguous float32 of n elements")
+    nv.check(nv.lib().flexar_mx_unpack_sum(msgs.data_ptr(), msgs.shape[1], msgs.shape[0], n,
+                                           _MX_WIRE_CODES[wire], y.data_ptr(), _stream_handle(stream)),
+             "mx_unpack_sum")
+    return y

@@ -132,15 +132,17 @@ class HierarchicalCommunicator:
         return t
 
     def _cross_gather(self, x):
-        """Every node's ``x`` (same shape) over the cross-node group, in node order."""
-        dist = self._dist
+        """Every node's 1-D ``x`` over the cross-node group, in node order: a [nodes, numel] tensor on x's
+        device."""
+        dist, torch = self._dist, self._torch
         h = x.cpu() if self.cross_on_host else x
-        outs = [self._torch.empty_like(h) for _ in range(self.nodes)]
+        big = torch.empty((self.nodes, h.numel()), dtype=h.dtype, device=h.device)
+        outs = list(big.unbind(0))  # rows of one buffer: the device codec reads them with one stride
         if self.cross_pg is not None:
             self.cross_pg.allgather([outs], [h]).wait()
         else:
             dist.all_gather(outs, h, group=self.cross_group)
-        return [o.to(x.device) for o in outs]
+        return big.to(x.device)
 
     def _cross_all_reduce_mx(self, t, wire: str):
         """Cross-node SUM of a float shard with OCP MX fp8 on the network (a scale per 32-element block): each
@@ -154,6 +156,15 @@ class HierarchicalCommunicator:
             return t
         torch = self._torch
         n = t.numel()
+        if t.is_cuda:  # native codec (csrc/src/k_mx_codec.hip): one pass to pack, one to dequantise and sum
+            from ..ops.quant import mx_pack, mx_unpack_sum
+
+            msgs = self._cross_gather(mx_pack(t.contiguous(), wire))
+            if t.dtype == torch.float32 and t.is_contiguous():
+                mx_unpack_sum(msgs, n, wire, out=t.view(-1))
+            else:
+                t.copy_(mx_unpack_sum(msgs, n, wire).view(t.shape))
+            return t
         q, sb = mx_quantize(t.float(), wire)
         # one message per node: the fp8 payload followed by its scale bytes
         msgs = self._cross_gather(torch.cat([q.view(torch.uint8), sb.to(torch.uint8)]))

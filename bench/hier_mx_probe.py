@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Device cost of the hierarchical communicator's cross-node MX step outside the network
+(parallel/hierarchical.py _cross_all_reduce_mx): quantise one shard (ops.quant.mx_quantize), pack payload +
+scale bytes, then dequantise and sum `nodes` received messages in node order - the torch-op form and the
+native codec (csrc/src/k_mx_codec.hip), checked bitwise equal. One JSON line per shard size."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from allreduce_over_mpi_amd.ops.quant import mx_dequantize, mx_quantize  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    nodes = int(os.environ.get("HMP_NODES", "4"))
+    for n in (1 << 20, 1 << 22, 1 << 25):
+        t = torch.randn(n, device=dev)
+
+        def quant():
+            q, sb = mx_quantize(t, "e4m3")
+            return torch.cat([q.view(torch.uint8), sb.to(torch.uint8)]), q.dtype
+
+        msg, fp8 = quant()
+        msgs = [msg.clone() for _ in range(nodes)]
+
+        def combine():
+            acc = None
+            for m in msgs:
+                v = mx_dequantize(m[:n].view(fp8), m[n:], n)
+                acc = v if acc is None else acc + v
+            return acc
+
+        from allreduce_over_mpi_amd.ops.quant import mx_pack, mx_unpack_sum
+
+        big = torch.stack(msgs)
+
+        def native_pack():
+            return mx_pack(t, "e4m3")
+
+        def native_combine():
+            return mx_unpack_sum(big, n, "e4m3")
+
+        assert torch.equal(native_pack(), msg) and torch.equal(native_combine(), combine())
+        res = {"elements": n, "nodes": nodes}
+        for name, fn in (("torch_quantise_us", quant), ("torch_dequant_sum_us", combine),
+                         ("native_pack_us", native_pack), ("native_unpack_sum_us", native_combine)):
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(10):
+                fn()
+            torch.cuda.synchronize()
+            res[name] = round((time.perf_counter() - t0) / 10 * 1e6, 1)
+        # fp32 bytes a ring allreduce over `nodes` moves per rank, at 50 GB/s of network per GPU
+        res["ring_fp32_net_us_at_50GBps"] = round(2 * (nodes - 1) / nodes * 4 * n / 50e9 * 1e6, 1)
+        res["mx_allgather_net_us_at_50GBps"] = round((nodes - 1) * n * 33 / 32 / 50e9 * 1e6, 1)
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

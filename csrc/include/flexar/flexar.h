@@ -264,6 +264,13 @@ int flexar_quantize_fp8(const void* x, int dtype, void* q, size_t n, const float
 int flexar_dequantize_fp8(const void* q, void* x, int dtype, size_t n, const float* amax_parts, float num,
                           void* hip_stream);
 
+/* ---- OCP MX fp8 message codec (hierarchical cross-node step) --------------- */
+/* msg = n fp8 values then ceil(n/32) e8m0 block-scale bytes; wire 4 = e4m3, 5 = e5m2 (x: f32/bf16/f16). */
+int flexar_mx_pack(const void* x, int dtype, void* msg, size_t n, int wire, void* hip_stream);
+/* out[i] = sum over nmsg messages (msg_stride bytes apart), in order, of q_k[i] * 2^X_k (fp32). */
+int flexar_mx_unpack_sum(const void* msgs, size_t msg_stride, int nmsg, size_t n, int wire, float* out,
+                         void* hip_stream);
+
 /* ---- helpers --------------------------------------------------------------- */
 int flexar_pointer_is_device(const void* p); /* 1 if p is device memory */
 int flexar_current_device(void);

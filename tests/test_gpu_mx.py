@@ -129,3 +129,31 @@ def test_default_spec_wire_applies_only_where_it_can(cuda, monkeypatch):
         grp.check()
     finally:
         grp.close()
+
+
+@pytest.mark.parametrize("wire", ["e4m3", "e5m2"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_mx_codec_matches_reference(cuda, wire, dtype):
+    """Native MX message codec (csrc/src/k_mx_codec.hip, the hierarchical cross-node step): pack is bitwise
+    [mx_quantize bytes | scale bytes]; unpack_sum is bitwise the dequantised rows summed in order. Sizes off
+    the 32-element block and an all-zero block included."""
+    from allreduce_over_mpi_amd.ops.quant import (mx_dequantize, mx_message_bytes, mx_pack, mx_quantize,
+                                                  mx_unpack_sum)
+
+    for n in (1, 31, 33, 4096, 100003):
+        xs = []
+        for k in range(3):
+            x = torch.randn(n, generator=torch.Generator().manual_seed(n + k)) * 10.0 ** (k - 1)
+            x[: min(n, 32)] = 0.0 if k == 1 else x[: min(n, 32)]
+            xs.append(x.to(dtype))
+        msgs = torch.stack([mx_pack(x.cuda(), wire) for x in xs])
+        assert msgs.shape == (3, mx_message_bytes(n))
+        want_sum = None
+        for k, x in enumerate(xs):
+            q, sb = mx_quantize(x.float(), wire)
+            want = torch.cat([q.view(torch.uint8), sb.to(torch.uint8)])
+            assert torch.equal(msgs[k].cpu(), want), (n, k)
+            v = mx_dequantize(q, sb, n)
+            want_sum = v if want_sum is None else want_sum + v
+        got = mx_unpack_sum(msgs, n, wire).cpu()
+        assert torch.equal(got, want_sum), (n, int((got != want_sum).sum()))
