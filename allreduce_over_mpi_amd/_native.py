@@ -48,7 +48,12 @@ def _sig(lib):
         "flexar_comm_destroy_local": (i, [vp]),
         "flexar_comm_resync": (i, [vp]),
         "flexar_comm_host_agree": (i, [vp, c.c_uint64, i, c.POINTER(c.c_uint64)]),
+        "flexar_comm_host_page_check": (i, [vp, c.POINTER(i)]),
+        "flexar_comm_host_page_drop": (i, [vp]),
         "flexar_host_barrier_run": (i, [cp, i, i, i, c.c_uint64, i]),
+        "flexar_host_page_open": (vp, [cp, i, i, u64]),
+        "flexar_host_page_shared": (i, [vp, u64, c.POINTER(i)]),
+        "flexar_host_page_close": (None, [vp]),
         "flexar_comm_selftest_note": (i, [vp, cp, sz]),
         "flexar_comm_rank": (i, [vp]),
         "flexar_comm_size": (i, [vp]),
@@ -136,6 +141,10 @@ def _sig(lib):
         "flexar_calib_load": (i, [cp, cp, c.POINTER(d)]),
         "flexar_calib_store": (i, [cp, cp, c.POINTER(d), i, cp, c.POINTER(d), c.POINTER(d)]),
         "flexar_calib_points": (i, [i, cp, sz]),
+        "flexar_crash_report_install": (None, []),
+        "flexar_crash_report_dump": (None, [cp]),
+        "flexar_crumb": (None, [cp, cp, i, i, u64, u64]),
+        "flexar_test_fatal": (None, [i]),
     }
     for name, (res, args) in table.items():
         fn = getattr(lib, name)
@@ -164,6 +173,9 @@ def lib():
             l = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
             _sig(l)
             _load_fastcall(l)
+            # fatal-signal / std::terminate report of the last flexar launches (crumbs.hpp); chains to the
+            # handlers installed before (Python's faulthandler under pytest); FLEXAR_CRASH_REPORT=0: off
+            l.flexar_crash_report_install()
             _lib = l
     return _lib
 
@@ -197,6 +209,36 @@ def log_warn(msg: str):
         import sys
 
         print(f"[flexar W] {msg}", file=sys.stderr, flush=True)
+
+
+def crumb(what: str, label: str = "", rank: int = -1, nranks: int = 0, epoch: int = 0, nbytes: int = 0):
+    """A phase breadcrumb in the native ring (printed by the crash report)."""
+    lib().flexar_crumb(what.encode(errors="replace"), label.encode(errors="replace"), int(rank), int(nranks),
+                       int(epoch), int(nbytes))
+
+
+_T0 = None
+
+
+def phase(what: str, rank: int = -1, nranks: int = 0, echo: bool = None):
+    """A start-up / section phase: a native breadcrumb, and (FLEXAR_PHASE_LOG=1, or echo=True) one stderr
+    line from THIS rank with the wall-clock time (comparable with torch's log stamps) and the seconds since
+    this process first logged a phase - so a failure on any rank names the phase that rank reached."""
+    import time
+
+    global _T0
+    if _T0 is None:
+        _T0 = time.monotonic()
+    if _lib is not None:
+        crumb("phase", what, rank, nranks)
+    if echo is None:
+        echo = os.environ.get("FLEXAR_PHASE_LOG") == "1"
+    if echo:
+        import sys
+
+        now = time.time()
+        stamp = time.strftime("%H:%M:%S", time.localtime(now)) + f".{int(now * 1000) % 1000:03d}"
+        print(f"[phase r{rank} {stamp} +{time.monotonic() - _T0:.3f}s] {what}", file=sys.stderr, flush=True)
 
 
 def last_error() -> str:

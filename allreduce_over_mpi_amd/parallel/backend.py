@@ -129,6 +129,7 @@ class FlexarProcessGroup(dist.ProcessGroup):
         # 63-67 us vs 46 us uncompressed at 1 MiB on one GPU)
         self._compress_min = int(os.environ.get("FLEXAR_PG_COMPRESS_MIN_BYTES", str(4 << 20)))
         self._compress_agreed = False
+        self._mx_carrier = None  # the flat spec the MX wire rides on, "" when it cannot (decided once)
 
     # ------------------------------------------------------------------ plumbing
     def getBackendName(self):
@@ -216,13 +217,41 @@ class FlexarProcessGroup(dist.ProcessGroup):
                 and t.dtype in (torch.float32, torch.bfloat16, torch.float16)
                 and t.numel() * t.element_size() >= self._compress_min)
 
-    def _rs_algo(self, t, opname):
+    def _rs_algo(self, t, opname, comm=None):
         """Reduce-scatter spec: the OCP MX wire under FLEXAR_PG_COMPRESS (the flat reduce-scatter's typed
         form: FSDP / ZeRO gradient shards), otherwise the library's choice."""
-        a = self._compress_algo(t, opname) if self._compress or not self._compress_agreed else None
+        a = self._compress_algo(t, opname, comm) if self._compress or not self._compress_agreed else None
         return a if a and "+mx" in a else None
 
-    def _compress_algo(self, t, opname):
+    def _mx_carrier_spec(self, comm):
+        """The spec the OCP MX wire can ride on, or "" (ADVICE r4): the planner takes the wire only on the flat
+        schedule (tree:N), with at most 8 ranks (one reduction of every contribution), over IPC staging - not
+        on a ring / RHD / tree / oneshot / LL FLEXAR_ALGO, not beyond 8 ranks, not on the message transport
+        (IPC unavailable: every call runs over RCCL). Otherwise the call runs uncompressed, with one warning.
+        The inputs (FLEXAR_ALGO, world size, the agreed transport) are the same on every rank, so every rank
+        decides the same."""
+        if self._mx_carrier is not None:
+            return self._mx_carrier
+        base = (self.algo or "flat+pull").replace("+zc", "")
+        head, *mods = base.split("+")
+        why = None
+        if head not in ("flat", "auto", f"tree:{self._world}"):
+            why = f"FLEXAR_ALGO={self.algo!r} is not the flat schedule"
+        elif not 2 <= self._world <= 8:
+            why = f"{self._world} ranks (the MX wire reduces every contribution once: at most 8)"
+        elif any(m in ("rccl", "msg", "bidir") for m in mods):
+            why = f"FLEXAR_ALGO={self.algo!r} runs over the message transport / bidirectional flat form"
+        elif comm is not None and not comm.topology().get("ipc", True):
+            why = "IPC is unavailable: every call runs over the RCCL message transport"
+        if why:
+            if self._rank == 0:
+                nv.log_warn(f"FLEXAR_PG_COMPRESS={self._compress_name}: not applied ({why}); calls run uncompressed")
+            self._mx_carrier = ""
+        else:
+            self._mx_carrier = "flat+pull" + "".join("+" + m for m in mods) if head == "auto" else base
+        return self._mx_carrier
+
+    def _compress_algo(self, t, opname, comm=None):
         """The spec of this allreduce under FLEXAR_PG_COMPRESS, or the plain one (self.algo)."""
         if not self._compress_agreed:  # once, collectively: every rank's setting the same
             code = _COMPRESS_CODES[self._compress]
@@ -235,8 +264,8 @@ class FlexarProcessGroup(dist.ProcessGroup):
             self._compress_agreed = True
         if self.hierarchical or not self._compress_eligible(t, opname):
             return self.algo
-        base = (self.algo or "flat+pull").replace("+zc", "")  # the MX wire runs on staging (no registration)
-        return base + self._compress
+        base = self._mx_carrier_spec(comm)  # the MX wire runs on staging (no registration), flat, <= 8 ranks
+        return base + self._compress if base else self.algo
 
     def allreduce(self, tensor_list, opts=AllreduceOptions()):
         opname = _redop_name(opts.reduceOp)
@@ -265,7 +294,8 @@ class FlexarProcessGroup(dist.ProcessGroup):
                               "band": "min", "bxor": "bxor"}[opname]
                     comm.all_reduce(t8, op=boolop, algo=self.algo)
                 else:
-                    algo = self._compress_algo(t, opname) if self._compress or not self._compress_agreed else self.algo
+                    algo = self._compress_algo(t, opname, comm) if self._compress or not self._compress_agreed \
+                        else self.algo
                     if self.hierarchical and self._compress and self._compress_eligible(t, opname):
                         # several nodes: the intra-node steps stay exact, the network carries OCP MX fp8
                         comm.all_reduce(t, op=opname, algo=self.algo, compress=self._compress_name)
@@ -464,7 +494,7 @@ class FlexarProcessGroup(dist.ProcessGroup):
                 def run(c):
                     flat = torch.cat([t.reshape(-1) for t in chunks])
                     res = torch.empty(out.numel(), dtype=out.dtype, device=out.device)
-                    c.reduce_scatter(flat, res, op=opname, algo=self._rs_algo(flat, opname))
+                    c.reduce_scatter(flat, res, op=opname, algo=self._rs_algo(flat, opname, c))
                     out.copy_(res.view_as(out))
                 return self._on_side([out] + list(chunks), run, output_tensors)
         return self._fallback(output_tensors).reduce_scatter(output_tensors, input_tensors, opts)
@@ -475,7 +505,7 @@ class FlexarProcessGroup(dist.ProcessGroup):
                 input_tensor.numel() == output_tensor.numel() * self._world and self._flat_comm_ok(input_tensor):
             return self._on_side([input_tensor, output_tensor],
                                  lambda c: c.reduce_scatter(input_tensor, output_tensor, op=opname,
-                                                            algo=self._rs_algo(input_tensor, opname)), [output_tensor])
+                                                            algo=self._rs_algo(input_tensor, opname, c)), [output_tensor])
         return self._fallback([input_tensor])._reduce_scatter_base(output_tensor, input_tensor, opts)
 
     def _on_side(self, tensors, fn, result):
@@ -504,7 +534,7 @@ class FlexarProcessGroup(dist.ProcessGroup):
 
         def run(c):
             for o, i in zip(output_tensors, input_tensors):
-                c.reduce_scatter(i, o, op=opname, algo=self._rs_algo(i, opname))
+                c.reduce_scatter(i, o, op=opname, algo=self._rs_algo(i, opname, c))
         return self._on_side(list(input_tensors) + list(output_tensors), run, list(output_tensors))
 
     def alltoall_base(self, output, input, output_split_sizes, input_split_sizes, opts=AllToAllOptions()):

@@ -149,10 +149,15 @@ class Communicator:
         err.agreed = True
         return err
 
+    def _phase(self, what: str):
+        """Breadcrumb (+ stderr line under FLEXAR_PHASE_LOG=1) of a creation phase on this rank."""
+        nv.phase("comm: " + what, self.rank, self.world_size)
+
     def _open(self, workspace_bytes, exchange, transport):
         """Create, export, connect and verify the native communicator (collective)."""
         import torch
 
+        self._phase(f"create (workspace {int(workspace_bytes)} B, transport {transport})")
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
             nv.check(self._lib.flexar_comm_create(self.rank, self.world_size, self.device, int(workspace_bytes),
@@ -161,8 +166,11 @@ class Communicator:
         self._hi = int(h.value or 0)  # the handle as an int, for the fast-call path
         self.selftest_failed = []
         self.selftest_notes = {}
+        self.selftest_recovered = []
+        self.selftest_flaky = []
         self.calibration = None
         self.transport_note = None
+        self.host_page_note = None
         self._exchange = None
         self._regs = {}
         self._zc_ok = None  # zero-copy readiness: None = not checked yet (first register())
@@ -173,7 +181,9 @@ class Communicator:
         buf = ctypes.create_string_buffer(hs)
         nv.check(self._lib.flexar_comm_export(self._h, buf), "comm_export")
         self._exchange = exchange
+        self._phase("handle exchange")
         allb = b"".join(exchange(bytes(buf.raw)))
+        self._phase("connect (map every peer)")
         rc = self._lib.flexar_comm_connect(self._h, allb)
         # agreement round (also the barrier: everyone has mapped everyone before the first collective);
         # a rank that failed to map a peer must not leave the others waiting in a later collective
@@ -187,15 +197,39 @@ class Communicator:
         if bad and not fallback:
             err = nv.FlexarError(rc or 5, "comm_connect: " + "; ".join(b.split(":", 1)[1] for b in bad))
             raise self._agreed(err) if mapping_only else err  # settings mismatches would only fail again
+        self._verify_host_page(exchange)
         if transport == "rccl" or fallback:
+            self._phase("message transport (ncclCommInitRank)")
             self._init_msg(exchange)
             if fallback:
                 nv.check(self._lib.flexar_comm_connect_msg_only(self._h), "connect_msg_only")
                 self.transport_note = "IPC unavailable (" + "; ".join(b.split(":", 1)[1] for b in bad) + \
                                       "): every call runs over the RCCL message transport"
+        self._phase("probe agreement")
         self._agree_probe(exchange)
         self._readiness(exchange)
+        self._phase("calibration")
         self._calibrate(exchange)
+        self._phase("ready")
+
+    def _verify_host_page(self, exchange):
+        """Is the teardown / agreement page (csrc/src/host_barrier.hpp) shared by every rank? Every rank wrote
+        its mark into the page at connect; the exchange right after connect was the barrier, so the check is
+        immediate: a rank whose page lacks a peer's mark (one container per rank, a private /dev/shm) says so,
+        and then every rank drops the page - teardown parks exported buffers instead of waiting out the
+        timeout, host agreements go to the bootstrap."""
+        ok = ctypes.c_int(0)
+        if self.topology().get("host_page"):
+            nv.check(self._lib.flexar_comm_host_page_check(self._h, ctypes.byref(ok)), "host_page_check")
+        rows = exchange(b"1" if ok.value else b"0")
+        if all(r == b"1" for r in rows):
+            self.host_page_note = None
+            return
+        nv.check(self._lib.flexar_comm_host_page_drop(self._h), "host_page_drop")
+        self.host_page_note = ("host page not shared (no mark from rank(s) "
+                               f"{[i for i, r in enumerate(rows) if r != b'1']}): teardown falls back to deferred frees")
+        if self.rank == 0:
+            nv.log_warn(self.host_page_note)
 
     def _init_msg(self, exchange):
         """Create the RCCL communicator of the message transport (collective): rank 0's unique id is
@@ -269,6 +303,7 @@ class Communicator:
             the downgrade chain goes on; only an error that left the device unusable (rc != 0) ends creation,
             with every rank's message, on every rank."""
             nonlocal late_ms
+            self._phase(f"self-test {','.join(nv.family_names(fam))}")
             exchange(b"")
             if late_ms:
                 import time
@@ -303,17 +338,23 @@ class Communicator:
         mask = 0
         for fam in nv.FAMILIES.values():
             mask |= run(fam)
-        # a failure must repeat to disable a family: a transient one (a rank descheduled past the watchdog)
-        # passes the second time, a broken protocol fails again (families a communicator cannot run at all,
-        # e.g. peer-memory ones without IPC mappings, fail at once without launching anything)
+        # Every failed family runs a second time. A broken protocol fails again (families a communicator
+        # cannot run at all, e.g. peer-memory ones without IPC mappings, fail at once without launching
+        # anything). One that passes the second time is kept only when ranks share a GPU, where a rank
+        # descheduled past its peers' watchdog is expected; with one GPU per rank a family that failed once
+        # is a bug signal and stays disabled (selftest_policy).
         self.selftest_recovered = []
+        self.selftest_flaky = []
         if mask:
             again = 0
             for fam in nv.FAMILIES.values():
                 if mask & fam:
                     again |= run(fam)
-            self.selftest_recovered = nv.family_names(mask & ~again)
-            mask = again
+            local_shared = any(p["link"] == "same" for p in self.topology()["peers"] if p["rank"] != self.rank)
+            shared_any = any(r == b"1" for r in exchange(b"1" if local_shared else b"0"))
+            mask, recovered, flaky = selftest_policy(mask, again, shared_any)
+            self.selftest_recovered = nv.family_names(recovered)
+            self.selftest_flaky = nv.family_names(flaky)
         if mask:
             nv.check(self._lib.flexar_comm_set_disabled(self._h, mask), "set_disabled")
             self.selftest_failed = nv.family_names(mask)
@@ -724,6 +765,22 @@ class Communicator:
             self.close(collective=False)  # GC order differs per rank: never wait for peers here
         except Exception:
             pass
+
+
+def selftest_policy(first: int, second: int, shared_gpu: bool, mode: Optional[str] = None):
+    """Families disabled after the connect-time self-test: ``first`` failed the first pass on some rank,
+    ``second`` (a subset of them) failed again. Returns (disabled, recovered, flaky):
+    * ranks sharing a GPU (``shared_gpu``: any rank has a peer on its own device): a family that passed the
+      second time is kept (``recovered``) - a rank descheduled past its peers' watchdog is expected there;
+    * one GPU per rank: it is disabled anyway (``flaky``) - an intermittent failure of a protocol on
+      dedicated GPUs is a bug signal (e.g. a cross-device visibility problem), never descheduling.
+    FLEXAR_SELFTEST_RETRY=keep | disable overrides the choice (``mode``)."""
+    mode = mode if mode is not None else os.environ.get("FLEXAR_SELFTEST_RETRY", "")
+    passed_again = first & ~second
+    keep = shared_gpu if mode not in ("keep", "disable") else mode == "keep"
+    if keep:
+        return second, passed_again, 0
+    return first, 0, passed_again
 
 
 def store_exchange(store, rank: int, world_size: int, prefix: str = "flexar"):

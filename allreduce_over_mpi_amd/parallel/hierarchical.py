@@ -144,6 +144,16 @@ class HierarchicalCommunicator:
             dist.all_gather(outs, h, group=self.cross_group)
         return big.to(x.device)
 
+    def _mx_applies(self, dtype) -> bool:
+        """The MX cross-node step runs for fp32 / bf16 / fp16 shards and up to FLEXAR_HIER_MX_MAX_NODES (4)
+        nodes: its all-gather moves nodes x 1.03 bytes per element to every node - it grows linearly with the
+        node count, where a ring allreduce's 2 (n-1)/n x element bytes does not - so beyond a few nodes the
+        exact ring is cheaper. float64 (and every other dtype) takes the exact path."""
+        torch = self._torch
+        if dtype not in (torch.float32, torch.bfloat16, torch.float16):
+            return False
+        return self.nodes <= int(os.environ.get("FLEXAR_HIER_MX_MAX_NODES", "4") or 4)
+
     def _cross_all_reduce_mx(self, t, wire: str):
         """Cross-node SUM of a float shard with OCP MX fp8 on the network (a scale per 32-element block): each
         node's shard is quantised once, payload and scales are all-gathered in one message (1.03 bytes per
@@ -195,7 +205,7 @@ class HierarchicalCommunicator:
         if m > 0:
             shard = torch.empty(m, dtype=flat.dtype, device=flat.device)
             self.local.reduce_scatter(flat[:main], shard, op=red, algo=algo)
-            if compress and red == "sum" and flat.is_floating_point():
+            if compress and red == "sum" and self._mx_applies(flat.dtype):
                 self._cross_all_reduce_mx(shard, {"mx_e4m3": "e4m3", "mx_e5m2": "e5m2"}[compress])
             else:
                 self._cross_all_reduce(shard, red)

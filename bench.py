@@ -76,6 +76,20 @@ def log(rank, *a):
         print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+_NV = None  # the native module once imported (phase breadcrumbs)
+
+
+def phase(rank, what):
+    """A phase line from EVERY rank (a fault on rank k names the phase rank k reached):
+    rank, wall-clock time (comparable with torch's / RCCL's log stamps) and seconds since this process
+    started, on stderr; also a native breadcrumb that the crash report prints."""
+    now = time.time()
+    stamp = time.strftime("%H:%M:%S", time.localtime(now)) + f".{int(now * 1000) % 1000:03d}"
+    print(f"[phase r{rank} {stamp} +{time.monotonic() - _T_START:.3f}s] bench: {what}", file=sys.stderr, flush=True)
+    if _NV is not None:
+        _NV.crumb("phase", "bench: " + what, rank)
+
+
 class RcclOnly:
     """Stand-in communicator when flexar cannot run on this node: every call is RCCL's allreduce."""
 
@@ -244,6 +258,9 @@ def main():
     ap.add_argument("--config5-mb", type=float, default=256.0, help="config #5 buffer MiB (fp32 in, e4m3 wire)")
     ap.add_argument("--transport", default="rccl", choices=["rccl", "auto", "ipc"],
                     help="Communicator transport at N > 1 (rccl: IPC + the '+rccl' message transport candidates)")
+    ap.add_argument("--no-reduce-kernel", action="store_true",
+                    help="N = 1: skip the fan-in 2/4/8 reduction-kernel section (reduce_kernel)")
+    ap.add_argument("--reduce-kernel-mb", type=float, default=256.0, help="reduce_kernel: MiB per source")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -259,10 +276,16 @@ def main():
         import faulthandler
 
         faulthandler.dump_traceback_later(tb_s, repeat=True)
+    if world > 1:  # every rank's start-up phases on stderr (the Python communicator's too)
+        os.environ.setdefault("FLEXAR_PHASE_LOG", "1")
+    phase_log = os.environ.get("FLEXAR_PHASE_LOG") == "1"
+    ph = (lambda what: phase(rank, what)) if phase_log else (lambda what: None)
+    ph(f"start (world {world}, local rank {local})")
 
     import torch
     import torch.distributed as dist
 
+    ph("torch imported")
     local, shared, shared_rccl = configure_env(world, rank, local, os.environ)
     host_ref = shared and not shared_rccl  # gloo process group: references and reductions on the host
     if shared:
@@ -274,17 +297,25 @@ def main():
         local = local % ndev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    ph(f"device {local} set")
     if world > 1:
         if host_ref:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+        ph("process group ready (" + ("gloo" if host_ref else "nccl, eager RCCL init") + ")")
     if args.gpus != world:
         log(rank, f"note: --gpus {args.gpus} but WORLD_SIZE={world}; benchmarking {world} rank(s)")
 
     from allreduce_over_mpi_amd import _native as nv
     from allreduce_over_mpi_amd.parallel.comm import Communicator
     from allreduce_over_mpi_amd.utils.perf import algbw_gbps, busbw_gbps
+
+    global _NV
+    nv.lib()
+    _NV = nv
+    nv._T0 = _T_START  # the communicator's phase lines count from this process's start too
+    ph("native library loaded")
 
     dtype = getattr(torch, args.dtype)
     esize = torch.tensor([], dtype=dtype).element_size()
@@ -318,11 +349,15 @@ def main():
     # RHD schedules over ncclSend/ncclRecv ("+rccl"); if RCCL cannot be set up, IPC alone
     transports = ["ipc"] if (world == 1 or host_ref) else [args.transport, "ipc"] if args.transport != "ipc" else ["ipc"]
 
+    creations = []  # one entry per communicator this run built (rebuilds included): what readiness did
+
     def make_comm():
         err = None
         for tr in transports:
             try:
-                return Communicator(workspace_bytes=ws_bytes, transport=tr)
+                cm = Communicator(workspace_bytes=ws_bytes, transport=tr)
+                creations.append(creation_record(cm, tr))
+                return cm
             except nv.FlexarError as e:
                 err = e
                 if world > 1 and not shared:
@@ -333,9 +368,9 @@ def main():
         return None
 
     t_phase = time.perf_counter()
+    ph("communicator creation")
     comm = make_comm()
-    # start-up phases on stderr (rank 0): a failure early in a run then names the phase it reached
-    log(rank, f"phase: communicator ready after {time.perf_counter() - t_phase:.1f} s")
+    ph(f"communicator ready after {time.perf_counter() - t_phase:.1f} s")
     if comm is None:
         comm, fallback = RcclOnly(dist), "flexar communicator could not be created"
     # the three buffers first, each its own allocation (registration maps whole allocations into the peers;
@@ -399,7 +434,7 @@ def main():
         if world > 1:
             dist.all_reduce(ref, op=dist.ReduceOp.AVG if op == "avg" else dist.ReduceOp.SUM)
     ref_f = ref.float()
-    log(rank, f"phase: RCCL reference ready after {time.perf_counter() - t_phase:.1f} s")
+    ph(f"RCCL reference ready after {time.perf_counter() - t_phase:.1f} s")
     ref_max = float(ref_f.abs().max().item()) + 1e-6
     tol = {torch.float32: 1e-5, torch.bfloat16: 2e-2, torch.float16: 4e-3, torch.float8_e4m3fn: 0.13}[dtype]
     tol = tol * math.sqrt(world) * 4 if dtype != torch.float8_e4m3fn else tol
@@ -463,6 +498,7 @@ def main():
     # ---------------------------------------------------------------- cost model (no tune table)
     model = None
     if world > 1 and not fallback:
+        ph("cost-model measurement")
         choice = comm.describe(count, dtype)
         spec0 = choice.split(" ")[0]
         failed0, err0 = check("auto")
@@ -503,12 +539,14 @@ def main():
         # flat-stage protocols, rings on 1..4 arc-disjoint channels, RHD, two-stage FlexTree factorizations,
         # the copy engines (and the latency protocols for small buffers)
         cands = default_candidates(world, nbytes, esize=esize)
+        ph(f"tuner ({len(cands)} candidates + registered / RCCL ones)")
         if comm.topology().get("rccl"):  # the schedules over RCCL send/recv as well
             cands += ["flat+rccl", "ring+rccl"] + (["rhd+rccl"] if world > 2 and not world & (world - 1) else [])
         if zc:  # registered buffers: the flat schedule straight from / to the peers' x and y (put: remote writes only)
             cands += ["flat+zc", "flat+zc+nts", "flat+zc+wt", "flat+zc+push", "flat+zc+push+nts", "flat+zc+push+wt",
                       "flat+zc+put", "flat+zc+put+nts", "flat+zc+put+wt"]
         for spec in cands:
+            ph(f"tuner candidate {spec}")
             failed, err = check(spec)
             failed = max_over_ranks(failed)  # one agreement per candidate, on every rank
             t = timed(spec, 5, warm=2) if failed == 0.0 else None
@@ -609,6 +647,7 @@ def main():
             log(rank, f"{algo}: {rejected[algo]}; trying the next candidate")
             continue
         desc = comm.describe(count, dtype) if algo == "auto" else algo
+        ph(f"timed region: {algo} (attempt {attempt})")
         log(rank, f"correctness vs {'RCCL' if world > 1 else 'input'}: max rel err {err:.3g} (ok); running {desc}")
         a = None if algo == "auto" else algo
         run_failed = 0.0
@@ -654,9 +693,11 @@ def main():
         del z
 
     # ---------------------------------------------------------------- BASELINE configs #3 / #4 / #5
+    ph("timed region done")
     sections = {}
     flex = not isinstance(comm, RcclOnly)
     if world > 1 and flex and not args.no_configs:
+        ph("BASELINE configs #5 / #3 / #4")
         if budget.allow("config5", COMPANION_AT):
             sections["config5"] = run_config5(comm, world, dev, dist, timed_fn, max_vec, host_ref, args, rank)
         if budget.allow("config3", COMPANION_AT):
@@ -711,11 +752,7 @@ def main():
     value = busbw  # rccl-tests busbw; 0 at N = 1 by definition (see the module docstring)
     readiness = None
     if world > 1 and isinstance(comm, Communicator):
-        topo = comm.topology()
-        readiness = {"links": topo["links"], "links_local": topo.get("links_local"), "selftested": topo["selftested"],
-                     "disabled": topo["disabled"],
-                     "peer_links": sorted({p["link"] for p in topo["peers"] if p["link"] != "self"}),
-                     "calibration": comm.calibration}
+        readiness = readiness_record(comm, creations)
     out = {
         "metric": "allreduce bus bandwidth (GB/s)",
         "value": round(value, 2),
@@ -765,11 +802,14 @@ def main():
     if world == 1:
         out["note"] = ("N=1: no inter-GPU traffic, busbw = 0 by definition (value); algbw_GBps is the device copy "
                        "through the flexar executor kernel and is not comparable with busbw")
+        if not args.no_reduce_kernel:  # outside the timed region; the headline `value` is unchanged
+            out["reduce_kernel"] = run_reduce_kernel(dev, args.reduce_kernel_mb)
     out["dropped"] = budget.dropped or None
     out["budget_s"] = budget.seconds
     out["bench_wall_s"] = round(budget.elapsed(), 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    ph("teardown")
     comm.close()
     if world > 1:
         dist.destroy_process_group()
@@ -864,6 +904,94 @@ def run_config5(comm, world, dev, dist, timed_fn, max_vec, host_ref, args, rank)
                    rccl_fp32_avg_busbw_GBps=round(busbw_gbps(4 * n, tr, world), 2) if tr else None)
     del x, y, ref
     return out
+
+
+def creation_record(comm, transport):
+    """What the readiness gate did while building one communicator (kept for every rebuild)."""
+    return {"transport": transport, "retried": getattr(comm, "retried", None),
+            "selftest_failed": list(getattr(comm, "selftest_failed", []) or []),
+            "selftest_recovered": list(getattr(comm, "selftest_recovered", []) or []),
+            "selftest_flaky": list(getattr(comm, "selftest_flaky", []) or [])}
+
+
+def readiness_record(comm, creations=()):
+    """The bench JSON's `readiness` block (a failure is never silent, as the reference's
+    exit(1) in allreduce_over_mpi/mpi_mod.hpp:916 never is): the final communicator's probe (links, peer link
+    classes), the families the self-test ran and disabled, the ones that failed once and passed on the
+    second pass (`selftest_recovered`: kept, ranks share a GPU; `selftest_flaky`: disabled anyway, one GPU
+    per rank), every rank's failure notes (truncated), whether creation was retried after an agreed failure,
+    the transport note (IPC unavailable -> message transport), whether the host agreement page is joined and
+    verified shared, the calibration, and the same facts for every communicator the run built."""
+    topo = comm.topology()
+    notes = {}
+    for r, v in sorted((getattr(comm, "selftest_notes", None) or {}).items()):
+        txt = " / ".join(v)
+        notes[str(r)] = txt if len(txt) <= 300 else txt[:297] + "..."
+    return {"links": topo["links"], "links_local": topo.get("links_local"), "selftested": topo["selftested"],
+            "disabled": topo["disabled"],
+            "peer_links": sorted({p["link"] for p in topo["peers"] if p["link"] != "self"}),
+            "selftest_recovered": list(getattr(comm, "selftest_recovered", []) or []),
+            "selftest_flaky": list(getattr(comm, "selftest_flaky", []) or []),
+            "selftest_notes": notes or None,
+            "retried": getattr(comm, "retried", None),
+            "transport_note": getattr(comm, "transport_note", None),
+            "host_page": {"joined": bool(topo.get("host_page")), "verified_shared": topo.get("host_page_shared"),
+                          "note": getattr(comm, "host_page_note", None)},
+            "calibration": getattr(comm, "calibration", None),
+            "creations": list(creations) or None}
+
+
+def run_reduce_kernel(dev, mib=256.0, fanins=(2, 4, 8), dtypes=("float32", "bfloat16", "float8_e4m3fn"), iters=10):
+    """N = 1 companion section: the hand-written gfx950 fan-in reduction kernel that is
+    the reference's hot loop (reduce_sum, allreduce_over_mpi/mpi_mod.hpp:245-452), measured by the driver's
+    own run. dst = src_0 + ... + src_{K-1} over `mib` MiB sources (flexar_reduce: 16-B loads, fp32
+    accumulation, one rounding to the dtype); effective HBM rate = (K + 1) x bytes / time (K reads + one
+    write). Checked against the order-defined fp32 sum in torch (((s0 + s1) + s2) + ...), rounded once to the
+    dtype: `bit_exact` is an exact comparison of every element, `max_rel_err` the largest |out - ref| over
+    max |ref| (fp32 accumulation, so exact in every dtype unless the kernel's rounding differs)."""
+    import torch
+
+    from allreduce_over_mpi_amd.ops import reduce as flexar_reduce
+
+    rows = []
+    t0 = time.perf_counter()
+    gen = torch.Generator(device=dev)
+    for dname in dtypes:
+        dt = getattr(torch, dname)
+        es = torch.tensor([], dtype=dt).element_size()
+        n = int(mib * (1 << 20)) // es
+        srcs = []
+        for k in range(max(fanins)):
+            gen.manual_seed(99 + k)
+            srcs.append(torch.randn(n, device=dev, generator=gen).to(dt))
+        out = torch.empty_like(srcs[0])
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for k in fanins:
+            sk = srcs[:k]
+            for _ in range(2):
+                flexar_reduce(sk, "sum", out=out)
+            torch.cuda.synchronize()
+            st.record()
+            for _ in range(iters):
+                flexar_reduce(sk, "sum", out=out)
+            en.record()
+            torch.cuda.synchronize()
+            t = st.elapsed_time(en) / iters * 1e-3
+            ref = sk[0].float()
+            for s in sk[1:]:
+                ref = ref + s.float()
+            ref_d = ref.to(dt)
+            exact = bool(torch.equal(out.view(torch.uint8), ref_d.view(torch.uint8)))
+            err = float((out.float() - ref).abs().max().item()) / (float(ref.abs().max().item()) + 1e-30)
+            rows.append({"dtype": dname, "fanin": k, "bytes_per_src": n * es, "us": round(t * 1e6, 1),
+                         "eff_TBps": round((k + 1) * n * es / t / 1e12, 3), "bit_exact": exact,
+                         "max_rel_err": float(f"{err:.3g}")})
+            del ref, ref_d
+        del srcs, out
+        torch.cuda.empty_cache()
+    return {"what": "flexar_reduce: dst = sum of K sources (fp32 accumulate), effective TB/s = (K+1) x bytes / time; "
+                    "checked against torch's order-defined fp32 sum rounded once to the dtype",
+            "rows": rows, "wall_s": round(time.perf_counter() - t0, 2)}
 
 
 def run_config3(comm, world, rank, dev, dist, timed_fn, max_vec, host_ref, args):

@@ -96,6 +96,12 @@ int flexar_comm_destroy_local(flexar_comm_t comm);
 /* Collective host-side agreement (shared-memory page of a connected communicator): *out = the maximum
  * (op 0) or bitwise OR (op 1) of `mine` over the ranks. FLEXAR_ERR_STATE when the communicator has no page. */
 int flexar_comm_host_agree(flexar_comm_t comm, uint64_t mine, int op, uint64_t* out);
+/* Connect-time check that the host page is shared by every rank (call on every rank after a bootstrap
+ * barrier that follows flexar_comm_connect): *shared = 1, or 0 and the page is dropped on this rank. If any
+ * rank reports 0, every rank calls flexar_comm_host_page_drop: teardown then parks exported buffers instead
+ * of waiting out FLEXAR_TIMEOUT_MS, and host agreements report FLEXAR_ERR_STATE. */
+int flexar_comm_host_page_check(flexar_comm_t comm, int* shared);
+int flexar_comm_host_page_drop(flexar_comm_t comm);
 int flexar_comm_rank(flexar_comm_t comm);
 int flexar_comm_size(flexar_comm_t comm);
 
@@ -285,10 +291,26 @@ void flexar_device_free(void* p);
  * Writes workgroups resident per CU (512 threads) and VGPRs. */
 int flexar_kernel_info(int dtype, int op, int kind, int proto, int* blocks_per_cu, int* vgprs);
 
+/* ---- fault attribution (crumbs.hpp) ------------------------------------------ */
+/* Every launch, copy, RCCL group and phase is appended to a per-process ring of breadcrumbs; on a fatal
+ * signal or std::terminate the ring and each live communicator's device progress (epoch started / finished
+ * by executor workgroup 0, host-mapped) are written to stderr. Installed once per process by the Python
+ * layer and at the first communicator; FLEXAR_CRASH_REPORT=0 disables it. */
+void flexar_crash_report_install(void);
+void flexar_crash_report_dump(const char* why); /* write the report now */
+/* A phase breadcrumb (start-up phases of bench.py / the Python communicator). */
+void flexar_crumb(const char* what, const char* label, int rank, int nranks, uint64_t epoch, uint64_t bytes);
+void flexar_test_fatal(int kind); /* tests only: 0 = std::terminate(), 1 = abort() */
+
 /* ---- host-only planning utilities (no GPU needed) ------------------------ */
 /* The collective-teardown agreement alone (tests): `phases` host barriers of `nranks` processes on the
  * shared-memory page `name`. 0, or FLEXAR_ERR_TIMEOUT with the straggler in flexar_last_error(). */
 int flexar_host_barrier_run(const char* name, int rank, int nranks, int phases, uint64_t timeout_ms, int delay_ms);
+/* The connect-time shared-page check alone (tests): open = join + mark; shared = every rank's mark present
+ * (call after a barrier of the caller's); close = unlink + release. */
+void* flexar_host_page_open(const char* name, int rank, int nranks, uint64_t token);
+int flexar_host_page_shared(void* page, uint64_t token, int* missing);
+void flexar_host_page_close(void* page);
 /* Readiness downgrade chain (see flexar_comm_selftest) applied to `spec` for nranks with the given
  * failed-family mask; writes the spec a call would run, or returns FLEXAR_ERR_UNSUPPORTED. */
 int flexar_downgrade_spec(const char* spec, int nranks, uint32_t disabled, int allow_dma, char* out, size_t outlen);

@@ -640,6 +640,32 @@ int flexar_reduce_host(void* dst, const void* const* srcs, int nsrc, size_t coun
 // The teardown agreement (host_barrier.hpp) on its own, for CPU tests: join `name` as `rank` of `nranks`,
 // pass `phases` barriers, sleeping `delay_ms` before each. Returns 0, or FLEXAR_ERR_TIMEOUT naming the
 // straggler (flexar_last_error). Rank 0 removes the name after the first barrier.
+// The connect-time shared-page check on its own (tests): join `name` and write this rank's mark; after the
+// caller's own barrier, flexar_host_page_shared tells whether every rank's mark is in this rank's page.
+void* flexar_host_page_open(const char* name, int rank, int nranks, uint64_t token) {
+  if (!name || nranks < 1 || nranks > (int)kMaxRanks || rank < 0 || rank >= nranks) {
+    set_error("bad arguments");
+    return nullptr;
+  }
+  std::unique_ptr<HostBarrier> hb(new HostBarrier);
+  std::string err;
+  if (!hb->join(name, rank, nranks, &err)) {
+    set_error(err);
+    return nullptr;
+  }
+  hb->mark(token);
+  return hb.release();
+}
+int flexar_host_page_shared(void* h, uint64_t token, int* missing) {
+  if (!h) return 0;
+  return static_cast<HostBarrier*>(h)->shared(token, missing) ? 1 : 0;
+}
+void flexar_host_page_close(void* h) {
+  if (!h) return;
+  static_cast<HostBarrier*>(h)->unlink();
+  delete static_cast<HostBarrier*>(h);
+}
+
 int flexar_host_barrier_run(const char* name, int rank, int nranks, int phases, uint64_t timeout_ms, int delay_ms) {
   if (!name || nranks < 1 || nranks > (int)kMaxRanks || rank < 0 || rank >= nranks) {
     set_error("bad arguments");

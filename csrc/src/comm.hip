@@ -175,6 +175,8 @@ int get_program(flexar_comm* c, const AlgoSpec& s, uint64_t count, uint32_t esiz
   auto it = c->cache.find(key);
   if (it != c->cache.end()) { *out = it->second.get(); return 0; }
   std::unique_ptr<DevProgram> dp(new DevProgram);
+  dp->spec = (coll == Coll::ALLREDUCE ? "" : coll == Coll::REDUCE_SCATTER ? "rs:" : coll == Coll::ALL_GATHER ? "ag:"
+              : coll == Coll::ALL_TO_ALL ? "a2a:" : "bcast:") + s.str();
   std::string err;
   Planner pl(c->nranks, c->rank, count, esize, fscale);
   if (!pl.build_coll(coll, s, stride, &dp->prog, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
@@ -279,6 +281,7 @@ void fill_ctx(flexar_comm* c, DevProgram* dp, const void* in, void* out, DevCtx*
   x->epochs = c->epochs;
   x->stg_half_bytes = c->half_bytes;
   x->err = c->err_dev;
+  x->progress = reinterpret_cast<uint64_t*>(c->err_dev) + 1;
   x->timeout_ticks = c->timeout_ticks;
   x->vec_ok = vec_ok_for(((uintptr_t)in) | ((uintptr_t)out));
   x->fi_kind = c->fi_kind;
@@ -373,6 +376,9 @@ int run_rs_ag(flexar_comm* c, Coll coll, const void* in, void* out, size_t count
     la.proto = proto_of(s);
     la.wire = dp->prog.wire;
     la.max_fanin = (int)dp->prog.max_nsrc;
+    la.tag = dp->spec.c_str();
+    la.epoch = c->launches + 1;
+    la.bytes = n * es * c->nranks;
     // all-gather moves bytes only: run the SUM instantiation (the op is never applied, K == 1)
     if ((rc = launch_dtype(dtype, coll == Coll::ALL_GATHER ? FLEXAR_SUM : op, la))) return rc;
     c->launches++;
@@ -430,6 +436,9 @@ int run_bcast(flexar_comm* c, const void* in, void* out, size_t count, int dtype
     la.grid = choose_grid(c, n * es, dp->prog.nchan);
     la.stream = st;
     la.proto = proto_of(s);
+    la.tag = dp->spec.c_str();
+    la.epoch = c->launches + 1;
+    la.bytes = n * es;
     if ((rc = launch_dtype(dtype, FLEXAR_SUM, la))) return rc;
     c->launches++;
   }
@@ -578,6 +587,9 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     la.ctx.scale = fs;
     la.grid = hit ? m.grid : ll_grid(c, count, es);
     la.stream = st;
+    la.tag = "ll";
+    la.epoch = c->launches + 1;
+    la.bytes = count * es;
     if (roctx().push) roctx().push(("flexar allreduce ll " + std::to_string(count * es) + "B").c_str());
     c->calls++;
     c->bytes += count * es;
@@ -614,6 +626,9 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     la.proto = proto_of(s);
     la.wire = dp->prog.wire;
     la.max_fanin = (int)dp->prog.max_nsrc;
+    la.tag = dp->spec.c_str();
+    la.epoch = c->launches + 1;
+    la.bytes = count * es;
     std::unique_ptr<DeviceTimer> tm(c->profile ? new DeviceTimer : nullptr);
     if (tm) tm->start(st);
     c->calls++;
@@ -653,6 +668,9 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     la.proto = proto_of(s);
     la.wire = dp->prog.wire;
     la.max_fanin = (int)dp->prog.max_nsrc;
+    la.tag = dp->spec.c_str();
+    la.epoch = c->launches + 1;
+    la.bytes = n * es;
     rc = launch_dtype(dtype, op, la);
     if (rc) break;
     c->launches++;
@@ -759,6 +777,9 @@ int flexar_allreduce_fp8(flexar_comm_t c, const void* in, void* out, size_t coun
     la.proto = proto_of(s);
     la.wire = dp->prog.wire;
     la.max_fanin = (int)dp->prog.max_nsrc;
+    la.tag = dp->spec.c_str();
+    la.epoch = c->launches + 1;
+    la.bytes = n * es;
     if ((rc = launch_dtype(dtype, op, la))) return rc;
     c->launches++;
   }

@@ -160,6 +160,8 @@ int flexar_comm_create(int rank, int nranks, int device, size_t workspace_bytes,
     set_error("invalid rank/nranks (nranks must be 1..16)");
     return FLEXAR_ERR_INVALID;
   }
+  crash_report_install();  // once per process; FLEXAR_CRASH_REPORT=0 disables it
+  crumb_phase("comm_create", "workspace + flags + error page", rank, nranks);
   std::unique_ptr<flexar_comm> c(new flexar_comm);
   c->rank = rank;
   c->nranks = nranks;
@@ -168,6 +170,7 @@ int flexar_comm_create(int rank, int nranks, int device, size_t workspace_bytes,
   size_t ws = workspace_bytes ? workspace_bytes : env_u64("FLEXAR_WORKSPACE_BYTES", 512ull << 20);
   int rc = alloc_workspace(c.get(), ws);
   if (rc) return rc;
+  c->crumb_slot = crumb_register_comm(rank, nranks, device, reinterpret_cast<const volatile uint64_t*>(c->err_host) + 1);
   c->resident = resident_blocks(device);
   c->model.stg_cap = (double)c->exec_half;  // the selector prices pieces of programs larger than a half
   c->peer_stg[rank] = c->stg;
@@ -209,6 +212,7 @@ static int exportable(flexar_comm* c, char** buf, size_t bytes, bool uncached, h
     (void)hipGetLastError();
     logf(LOG_WARN, c->rank, "export: hipIpcGetMemHandle(%s) failed (%s); re-allocating the %s", what,
          hipGetErrorString(e), what);
+    crumb_phase("comm_export", "re-allocating a buffer whose export failed", c->rank, c->nranks);
     char* nb = nullptr;
     hipError_t a = uncached ? hipExtMallocWithFlags((void**)&nb, bytes, hipDeviceMallocUncached) : hipMalloc(&nb, bytes);
     if (a != hipSuccess || hipMemset(nb, 0, bytes) != hipSuccess) {
@@ -231,6 +235,7 @@ static int exportable(flexar_comm* c, char** buf, size_t bytes, bool uncached, h
 int flexar_comm_export(flexar_comm_t c, void* handle_out) {
   if (!c || !handle_out) { set_error("null argument"); return FLEXAR_ERR_INVALID; }
   FX_HIP(hipSetDevice(c->device));
+  crumb_phase("comm_export", "hipIpcGetMemHandle of workspace and flags", c->rank, c->nranks);
   CommHandle h;
   memset(&h, 0, sizeof(h));
   h.magic = kHandleMagic;
@@ -266,15 +271,26 @@ int flexar_comm_connect(flexar_comm_t c, const void* all) {
   FX_HIP(hipSetDevice(c->device));
   const CommHandle* hs = (const CommHandle*)all;
   const CommHandle& me = hs[c->rank];
+  crumb_phase("comm_connect", "host page join, probe, hipIpcOpenMemHandle of every peer", c->rank, c->nranks);
   // Join the teardown agreement first (every rank gets the same handle bytes, so every rank that reaches
   // connect joins, whatever fails below): flexar_comm_destroy is collective from here on.
   if (!c->hb && c->nranks > 1 && hs[0].magic == kHandleMagic && hs[0].nranks == c->nranks) {
-    char name[96];
+    char name[128];
     snprintf(name, sizeof(name), "/flexar.%d.%016llx", (int)hs[0].pid, (unsigned long long)hs[0].nonce);
+    // FLEXAR_TEST_PAGE_PRIVATE=1 (tests only): every rank joins a page of its own, as with one container per
+    // rank (a private /dev/shm) - what flexar_comm_host_page_check must detect
+    if (env_u64("FLEXAR_TEST_PAGE_PRIVATE", 0))
+      snprintf(name + strlen(name), sizeof(name) - strlen(name), ".r%d", c->rank);
     std::unique_ptr<HostBarrier> hb(new HostBarrier);
     std::string err;
-    if (hb->join(name, c->rank, c->nranks, &err)) c->hb = std::move(hb);
-    else logf(LOG_WARN, c->rank, "connect: %s: teardown falls back to deferred frees", err.c_str());
+    if (hb->join(name, c->rank, c->nranks, &err)) {
+      c->hb = std::move(hb);
+      c->hb_token = hs[0].nonce;
+      c->hb_shared = -1;
+      c->hb->mark(c->hb_token);  // checked by flexar_comm_host_page_check after the caller's next barrier
+    } else {
+      logf(LOG_WARN, c->rank, "connect: %s: teardown falls back to deferred frees", err.c_str());
+    }
   }
   for (int r = 0; r < c->nranks; ++r) {
     const CommHandle& h = hs[r];
@@ -362,6 +378,17 @@ int flexar_comm_connect(flexar_comm_t c, const void* all) {
     }
     c->peer_flags[r] = (uint64_t*)p;
     c->opened[r] = true;
+    {
+      CrumbArgs ca;
+      ca.type = CRUMB_HOST;
+      ca.what = "peer mapped";
+      ca.rank = (int16_t)c->rank;
+      ca.nranks = (int16_t)c->nranks;
+      ca.grid = (uint32_t)r;  // the peer
+      ca.bytes = h.ws_bytes;
+      ca.label = link_name(c->link_cls[r]);
+      crumb(ca);
+    }
   }
   // FLEXAR_TEST_PROBE="RANK:class=pcie|xgmi|same|other" or "RANK:links=K" (tests only): that rank reports
   // a different link class for every peer, or a different link count - what probe agreement must catch
@@ -450,10 +477,20 @@ int flexar_comm_selftest(flexar_comm_t c, uint32_t families, uint32_t* failed_ou
     if (k.fam == PF_LL && !ll_usable(c, n, 4)) continue;
     c->selftested |= k.fam;
     logf(LOG_INFO, c->rank, "self-test: %s", k.spec);
+    crumb_phase("self-test family", k.spec, c->rank, c->nranks);
     for (int call = 0; call < 3 && !rc; ++call) {
       const std::string at = std::string(k.spec) + " call " + std::to_string(call);
       const uint32_t salt = (uint32_t)(call * 131 + k.fam * 17);
       const bool inject = (c->test_hip_fail & k.fam) != 0;  // tests: an invalid block size
+      CrumbArgs ca;
+      ca.type = CRUMB_LAUNCH;
+      ca.rank = (int16_t)c->rank;
+      ca.nranks = (int16_t)c->nranks;
+      ca.grid = 64;
+      ca.bytes = n * sizeof(int);
+      ca.label = k.spec;
+      ca.what = "selftest_fill";
+      crumb(ca);
       hipLaunchKernelGGL(selftest_fill, dim3(64), dim3(inject ? 4096 : 256), 0, st, in, out, n, c->rank, salt);
       const hipError_t le = hipGetLastError();
       if (le != hipSuccess) fail(k.fam, at + ": selftest_fill launch: " + hipGetErrorString(le));
@@ -462,6 +499,8 @@ int flexar_comm_selftest(flexar_comm_t c, uint32_t families, uint32_t* failed_ou
       const int e = flexar_allreduce_ex(c, in, out, n, FLEXAR_INT32, FLEXAR_SUM, st, k.spec, 1.0f);
       if (e) fail(k.fam, at + ": " + (*flexar_last_error() ? flexar_last_error() : "error " + std::to_string(e)));
       __atomic_store_n(c->st_bad, 0u, __ATOMIC_RELEASE);
+      ca.what = "selftest_check";
+      crumb(ca);
       hipLaunchKernelGGL(selftest_check, dim3(64), dim3(256), 0, st, out, n, N, salt, c->st_bad_dev);
       const hipError_t ce = hipGetLastError();
       if (ce != hipSuccess) fail(k.fam, at + ": selftest_check launch: " + hipGetErrorString(ce));
@@ -522,6 +561,7 @@ int flexar_comm_selftest_note(flexar_comm_t c, char* buf, size_t buflen) {
 // peers'); a plain watchdog timeout only needs flexar_comm_clear_error.
 int flexar_comm_resync(flexar_comm_t c) {
   if (!c) return FLEXAR_ERR_INVALID;
+  crumb_phase("comm_resync", "memsets of flags, epochs, staging", c->rank, c->nranks);
   FX_HIP(hipSetDevice(c->device));
   FX_HIP(hipDeviceSynchronize());
   FX_HIP(hipMemset(c->flags, 0, kFlagWords * sizeof(uint64_t)));
@@ -565,6 +605,7 @@ int flexar_comm_init_msg(flexar_comm_t c, const void* unique_id) {
   if (!rccl().ok) { set_error("RCCL not found (librccl.so)"); return FLEXAR_ERR_UNSUPPORTED; }
   if (c->nccl) return 0;
   FX_HIP(hipSetDevice(c->device));
+  crumb_phase("comm_init_msg", "ncclCommInitRank of the message transport", c->rank, c->nranks);
   ncclUniqueId id;
   memcpy(&id, unique_id, sizeof(id));
   int rc = rccl_check(rccl().CommInitRank(&c->nccl, c->nranks, id, c->rank), "ncclCommInitRank");
@@ -620,7 +661,8 @@ int flexar_comm_topology(flexar_comm_t c, char* buf, size_t buflen) {
                   std::to_string(c->resident) + ", \"selftested\": \"" + family_names(c->selftested) +
                   "\", \"disabled\": \"" + (c->disabled ? family_names(c->disabled) : std::string()) +
                   "\", \"ipc\": " + (c->ipc ? "true" : "false") + ", \"rccl\": " + (c->nccl ? "true" : "false") +
-                  ", \"host_page\": " + (c->hb ? "true" : "false") +
+                  ", \"host_page\": " + (c->hb ? "true" : "false") + ", \"host_page_shared\": " +
+                  (c->hb_shared < 0 ? "null" : c->hb_shared ? "true" : "false") +
                   ", \"peers\": [";
   for (int r = 0; r < c->nranks; ++r) {
     char t[256];
@@ -639,21 +681,25 @@ int flexar_comm_topology(flexar_comm_t c, char* buf, size_t buflen) {
 namespace flexar {
 
 // Exported buffers a teardown could not agree on (a peer never reached it, or a local destroy): a peer
-// may still map them, so they stay allocated - their virtual addresses are then never handed out again
-// while that mapping lives (a fresh allocation exported at a still-mapped address is what ROCm's dmabuf
-// IPC mishandles, see exportable()). Bounded: beyond kGraveMax entries the oldest is freed.
+// may still map them, so they stay allocated for the life of the process - their virtual addresses are then
+// never handed out again while that mapping lives (a fresh allocation exported at a still-mapped address is
+// what ROCm's dmabuf IPC mishandles, see exportable()). Never freed (freeing the oldest past a
+// count cap was exactly the case a peer may still map); the parked bytes are counted and a warning names
+// them every time they pass another FLEXAR_GRAVE_WARN_BYTES (default 8 GiB).
 static std::mutex g_grave_mu;
 static std::vector<std::pair<int, void*>> g_grave;  // (device, pointer)
-constexpr size_t kGraveMax = 16;
+static uint64_t g_grave_bytes = 0, g_grave_warned = 0;
 
-static void grave_keep(int device, void* p) {
+static void grave_keep(int device, void* p, uint64_t bytes, int rank) {
   if (!p) return;
   std::lock_guard<std::mutex> lk(g_grave_mu);
   g_grave.emplace_back(device, p);
-  while (g_grave.size() > kGraveMax) {
-    (void)hipSetDevice(g_grave.front().first);
-    (void)hipFree(g_grave.front().second);
-    g_grave.erase(g_grave.begin());
+  g_grave_bytes += bytes;
+  const uint64_t step = std::max<uint64_t>(1, env_u64("FLEXAR_GRAVE_WARN_BYTES", 8ull << 30));
+  if (g_grave_bytes / step > g_grave_warned) {
+    g_grave_warned = g_grave_bytes / step;
+    logf(LOG_WARN, rank, "destroy: %zu exported buffers (%.2f GiB) parked until the process exits: their peers "
+         "never agreed that they were unmapped", g_grave.size(), (double)g_grave_bytes / (1ull << 30));
   }
 }
 
@@ -664,6 +710,7 @@ static void grave_keep(int device, void* p) {
 // still holds a mapping of this communicator's. A peer that does not arrive within FLEXAR_TIMEOUT_MS
 // (or a local destroy) leaves this rank's exported buffers parked (grave_keep) instead of freed.
 static int destroy_impl(flexar_comm* c, bool agree) {
+  crumb_phase("comm_destroy", agree ? "collective" : "local", c->rank, c->nranks);
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
   const uint64_t timeout_ms = std::max<uint64_t>(1000, c->timeout_ticks / 100000ull);
@@ -728,8 +775,8 @@ static int destroy_impl(flexar_comm* c, bool agree) {
     (void)hipFree(c->stg);
     (void)hipFree(c->flags);
   } else {
-    grave_keep(c->device, c->stg);
-    grave_keep(c->device, c->flags);
+    grave_keep(c->device, c->stg, c->ws_bytes, c->rank);
+    grave_keep(c->device, c->flags, kFlagWords * sizeof(uint64_t), c->rank);
     if (agree && c->hb) {
       set_error("destroy: " + why + "; this rank's workspace stays allocated until the process exits");
       logf(LOG_WARN, c->rank, "destroy: %s; keeping this rank's exported workspace allocated", why.c_str());
@@ -739,6 +786,7 @@ static int destroy_impl(flexar_comm* c, bool agree) {
   if (c->hb) c->hb->unlink();  // every rank joined long before (connect): the name is no longer needed
   c->hb.reset();
   (void)hipFree(c->epochs);
+  crumb_unregister_comm(c->crumb_slot);  // before its progress words are freed
   (void)hipHostFree(c->err_host);
   delete c;
   // teardown ignores failures (e.g. closing a mapping a peer already released), but HIP keeps the last one
@@ -763,9 +811,48 @@ int flexar_comm_host_agree(flexar_comm_t c, uint64_t mine, int op, uint64_t* out
   int late = -1;
   const uint64_t tmo = std::max<uint64_t>(1000, c->timeout_ticks / 100000ull);
   if (!c->hb->exchange(mine, out, tmo, &late, op == 1)) {
-    set_error("host agreement: rank " + std::to_string(late) + " did not arrive within " + std::to_string(tmo) + " ms");
+    set_error("host agreement: rank " + std::to_string(late) + " did not arrive within " + std::to_string(tmo) +
+              " ms; the host page is dropped on this rank (its phase counter no longer matches the peers')");
+    // a timed-out agreement left this rank's phase advanced: later agreements could pair wrong phases, so the
+    // page is gone for good on this rank (its peers time out on their next agreement and drop theirs too)
+    c->hb->unlink();
+    c->hb.reset();
+    c->hb_shared = 0;
     return FLEXAR_ERR_TIMEOUT;
   }
+  return 0;
+}
+
+// Step 2 of the connect-time page check (step 1, HostBarrier::mark, ran in flexar_comm_connect): after a
+// barrier of the caller's bootstrap that every rank passed after connecting, is every rank's identity word
+// in this rank's page? *shared = 1 yes, 0 no (then the page is dropped on this rank and a named warning
+// says why; the caller agrees on the answer and drops it everywhere with flexar_comm_host_page_drop).
+int flexar_comm_host_page_check(flexar_comm_t c, int* shared) {
+  if (!c || !shared) return FLEXAR_ERR_INVALID;
+  *shared = 0;
+  if (!c->hb) return 0;
+  int missing = -1;
+  if (c->hb->shared(c->hb_token, &missing)) {
+    c->hb_shared = 1;
+    *shared = 1;
+    return 0;
+  }
+  logf(LOG_WARN, c->rank, "host page not shared: rank %d's mark is missing from %s (a private /dev/shm?): teardown "
+       "falls back to deferred frees and host agreements to the bootstrap", missing, c->hb->name().c_str());
+  c->hb->unlink();
+  c->hb.reset();
+  c->hb_shared = 0;
+  return 0;
+}
+
+// Drop the host page on this rank (collective in effect: every rank, when any rank's check failed).
+int flexar_comm_host_page_drop(flexar_comm_t c) {
+  if (!c) return FLEXAR_ERR_INVALID;
+  if (c->hb) {
+    c->hb->unlink();
+    c->hb.reset();
+  }
+  c->hb_shared = 0;
   return 0;
 }
 
@@ -1001,6 +1088,7 @@ int flexar_comm_calibrate(flexar_comm_t c, int mode, char* json, size_t jlen) {
     }
     std::vector<double> t(pts.size() + 1, 0.0);
     double failed = 0;
+    crumb_phase("calibration", "timing the calibration points", c->rank, c->nranks);
     for (size_t i = 0; i < pts.size(); ++i) {
       AlgoSpec s;
       std::string err;
@@ -1044,14 +1132,21 @@ int flexar_comm_calibrate(flexar_comm_t c, int mode, char* json, size_t jlen) {
       uint64_t any = 0;
       int late = -1;
       const uint64_t tmo = std::max<uint64_t>(1000, saved_timeout / 100000ull);
+      auto drop = [&]() {  // a timed-out agreement: phase counters no longer match (see host_agree)
+        c->hb->unlink();
+        c->hb.reset();
+        c->hb_shared = 0;
+      };
       if (!c->hb->exchange_max(failed != 0 ? 1 : 0, &any, tmo, &late)) {
         set_error("calibration: rank " + std::to_string(late) + " did not reach the failure agreement");
+        drop();
         return finish(FLEXAR_ERR_TIMEOUT);
       }
       if (any) {
         if ((rc = flexar_comm_resync(c)) != 0) return finish(rc);
         if (!c->hb->arrive_and_wait(tmo, &late)) {
           set_error("calibration: rank " + std::to_string(late) + " did not finish the resync");
+          drop();
           return finish(FLEXAR_ERR_TIMEOUT);
         }
       }

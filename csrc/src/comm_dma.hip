@@ -32,6 +32,8 @@ int reduce_chain(char* dst, char* dst2, const char* const* srcs, int nsrc, uint6
     la.grid = grid;
     la.stream = st;
     la.proto = proto;
+    la.tag = proto == PM_WT ? "dma: reduce of the landed blocks" : "flexar_reduce";
+    la.bytes = count * es;
     int rc = launch_dtype(dtype, op, la);
     if (rc) return rc;
   }
@@ -95,6 +97,14 @@ static int dma_wait(flexar_comm* c, uint32_t slot, const int* srcs, int n, uint6
   w.value = e;
   w.timeout_ticks = c->timeout_ticks;
   w.err = c->err_dev;
+  CrumbArgs ca;
+  ca.type = CRUMB_LAUNCH;
+  ca.what = "dma_wait_kernel";
+  ca.rank = (int16_t)c->rank;
+  ca.nranks = (int16_t)c->nranks;
+  ca.epoch = e;
+  ca.label = slot == kDmaSlotRS ? "dma: wait for the peers' reduce-scatter flags" : "dma: wait for a peer's all-gather flag";
+  crumb(ca);
   hipLaunchKernelGGL(dma_wait_kernel, dim3(1), dim3(64), 0, st, w);
   FX_HIP(hipGetLastError());
   return 0;
@@ -113,6 +123,20 @@ static int dma_phase(flexar_comm* c, int phase, const char* in, char* out, uint6
     const uint64_t s0 = (uint64_t)i * B;
     return s0 >= count ? 0 : std::min<uint64_t>(B, count - s0);
   };
+  {
+    CrumbArgs ca;
+    ca.type = CRUMB_COPY;
+    ca.what = "dma phase";
+    ca.rank = (int16_t)r;
+    ca.nranks = (int16_t)N;
+    ca.epoch = e;
+    ca.bytes = count * es;
+    static const char* names[] = {"fork", "reduce-scatter copies (hipMemcpyAsync into peers' staging) + flag writes",
+                                  "wait + reduce + all-gather flag writes", "all-gather copies from peers' result slots",
+                                  "join + epoch_set_kernel"};
+    ca.label = names[phase < 0 || phase > 4 ? 0 : phase];
+    crumb(ca);
+  }
   if (phase == 0) {  // the streams start after everything the caller enqueued before this call
     FX_HIP(hipEventRecord(c->dma_fork, st));
     for (int p = 0; p < N; ++p) {

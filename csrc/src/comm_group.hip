@@ -113,6 +113,8 @@ static int group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
     la.nranks = nranks;
     la.grid = grid;
     la.stream = st;
+    la.epoch = comms[0]->launches + 1;
+    la.tag = "in-process group";
     int rc = launch_dtype(dtype, op, la);
     if (!rc) (void)group_ctx_launched(st);
     if (rc) return rc;
@@ -156,6 +158,8 @@ static int group_allreduce(flexar_comm_t* comms, int nranks, const void* const* 
     la.nranks = nranks;
     la.grid = grid;
     la.stream = st;
+    la.epoch = comms[0]->launches + 1;
+    la.tag = "in-process group";
     la.proto = proto_of(specs[0]);
     la.wire = wire;
     la.max_fanin = fanin;
@@ -233,6 +237,8 @@ int flexar_group_collective(flexar_comm_t* comms, int nranks, int coll, const vo
   la.nranks = nranks;
   la.grid = grid;
   la.stream = st;
+  la.epoch = comms[0]->launches + 1;
+  la.tag = "in-process group";
   la.proto = proto;
   la.wire = wire;
   la.max_fanin = fanin;
@@ -281,6 +287,8 @@ int flexar_group_broadcast(flexar_comm_t* comms, int nranks, int root, const voi
   la.nranks = nranks;
   la.grid = grid;
   la.stream = st;
+  la.epoch = comms[0]->launches + 1;
+  la.tag = "in-process group";
   la.proto = proto;
   int rc = launch_dtype(dtype, FLEXAR_SUM, la);
   if (!rc) (void)group_ctx_launched(st);

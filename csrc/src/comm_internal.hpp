@@ -24,6 +24,7 @@
 #include <string>
 #include <vector>
 
+#include "crumbs.hpp"
 #include "host_barrier.hpp"
 #include "launch.hpp"
 #include "flexar/calibration.hpp"
@@ -67,6 +68,7 @@ struct CommHandle {
 };
 
 struct DevProgram {
+  std::string spec;  // the schedule it runs (breadcrumb tag)
   Program prog;
   Op* d_ops = nullptr;
   uint32_t* d_chan = nullptr;
@@ -139,6 +141,7 @@ inline RcclApi& rccl() {
 
 // A message plan with its executor segments uploaded.
 struct DevMsgPlan {
+  std::string spec;  // breadcrumb tag ("msg:" + schedule)
   MsgPlan plan;
   std::vector<Op*> d_ops;
   std::vector<uint32_t*> d_chan;
@@ -287,6 +290,9 @@ struct flexar_comm {
   // collective teardown (host_barrier.hpp): joined at connect, agreed on in flexar_comm_destroy
   uint64_t nonce = 0;
   std::unique_ptr<HostBarrier> hb;
+  int crumb_slot = -1;  // live-communicator slot of the crash report (crumbs.hpp)
+  uint64_t hb_token = 0;  // rank 0's nonce: the identity every rank writes into the page (HostBarrier::mark)
+  int hb_shared = -1;     // the page verified shared by every rank: 1 yes, 0 no (dropped), -1 not checked
 };
 
 namespace flexar {

@@ -21,6 +21,7 @@ int get_msg_plan(flexar_comm* c, const AlgoSpec& s, uint64_t count, uint32_t es,
   auto it = c->msg_cache.find(key);
   if (it != c->msg_cache.end()) { *out = it->second.get(); return 0; }
   std::unique_ptr<DevMsgPlan> dp(new DevMsgPlan);
+  dp->spec = "msg:" + s.str();
   std::string err;
   if (!build_msg_plan(c->nranks, c->rank, count, es, fs, s, &dp->plan, &err, coll, stride)) {
     set_error(err);
@@ -102,9 +103,22 @@ int run_msg(flexar_comm* c, const AlgoSpec& s, Coll coll, const void* in, void* 
       la.grid = choose_grid(c, span * es * 2, 1);
       la.stream = st;
       la.proto = PM_FENCE;
+      la.tag = dp->spec.c_str();
+      la.bytes = span * es;
       if ((rc = launch_dtype(dtype, op_k, la))) return rc;
       ++ex;
       continue;
+    }
+    {
+      CrumbArgs ca;
+      ca.type = CRUMB_RCCL;
+      ca.what = "ncclSend/ncclRecv group";
+      ca.rank = (int16_t)c->rank;
+      ca.nranks = (int16_t)c->nranks;
+      for (const MsgXfer& m : stp.sends) ca.bytes += m.bytes;
+      ca.grid = (uint32_t)(stp.sends.size() * 1000 + stp.recvs.size());  // sends x 1000 + receives
+      ca.label = dp->spec.c_str();
+      crumb(ca);
     }
     if ((rc = rccl_check(rccl().GroupStart(), "ncclGroupStart"))) return rc;
     for (const MsgXfer& m : stp.sends)

@@ -58,6 +58,9 @@ struct DevCtx {
   const float* amax_parts;  // FLEXAR_AMAX_PARTIALS per-workgroup max |x| of this rank's input
   uint64_t amax_off;        // byte offset of the amax granule slots in each staging parity half
   uint64_t mx_shadow;       // MX wire: byte offset of the block-scale shadow in each staging parity half
+  // fault attribution (crumbs.hpp): host-mapped {started, finished} epoch words of this communicator;
+  // workgroup 0 stores the epoch it starts and finishes (one system-scope store each; null = not recorded)
+  uint64_t* progress;
 };
 constexpr uint32_t kAmaxParts = 256;    // == FLEXAR_AMAX_PARTIALS
 constexpr uint64_t kAmaxRegion = 256;   // bytes reserved per parity half for the amax granules
@@ -1405,6 +1408,7 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
   const uint64_t epoch = c.epochs[b] + 1;
   const uint64_t par = (epoch & 1) ? c.stg_half_bytes : 0;
   if (tid == 0) s_abort = 0;
+  if (b == 0 && tid == 0 && c.progress) __hip_atomic_store(c.progress, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   float pre = 1.0f;
   if constexpr (TYPED && sizeof(WT_) == 1 && !IsMx<WT_>::value) {
     if (tid < 64) {
@@ -1495,6 +1499,7 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
   // implies b2 == b.
   // All lanes share the stores: one lane alone serialises up to 1024 stores at small grids.
   for (uint32_t j = b + tid * grid; j < kMaxGridBlocks; j += blockDim.x * grid) c.epochs[j] = epoch;
+  if (b == 0 && tid == 0 && c.progress) __hip_atomic_store(c.progress + 1, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1530,6 +1535,7 @@ __device__ FX_INLINE void ll_body(const DevCtx& c, const uint32_t b, const uint3
   if (tid == 0) s_abort = 0;
   __syncthreads();
   const uint64_t epoch = c.epochs[b] + 1;
+  if (b == 0 && tid == 0 && c.progress) __hip_atomic_store(c.progress, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const uint64_t par = ((epoch & 1) ? c.stg_half_bytes : 0) + c.ll_off;  // LL-only region: stale bytes
   const uint64_t nbytes = c.count * sizeof(T), W = (nbytes + 3) / 4;        // there are older granules
   const uint32_t N = c.nranks, r = c.rank;
@@ -1585,6 +1591,7 @@ __device__ FX_INLINE void ll_body(const DevCtx& c, const uint32_t b, const uint3
   __syncthreads();
   // All lanes share the stores: one lane alone serialises up to 1024 stores at small grids.
   for (uint32_t j = b + tid * grid; j < kMaxGridBlocks; j += blockDim.x * grid) c.epochs[j] = epoch;
+  if (b == 0 && tid == 0 && c.progress) __hip_atomic_store(c.progress + 1, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <typename T, typename OP>

@@ -35,6 +35,7 @@ class HostBarrier {
   struct Page {
     std::atomic<uint64_t> arrived[kMaxRanks];   // phases rank r has reached (1 = joined)
     std::atomic<uint64_t> value[2][kMaxRanks];  // exchange_max payload of rank r, by phase parity
+    std::atomic<uint64_t> ident[kMaxRanks];     // mark(): rank r's proof that it wrote into THIS page
   };
   static_assert(sizeof(Page) <= kPageBytes, "one page");
   static_assert(std::atomic<uint64_t>::is_always_lock_free, "cross-process atomics need lock-free words");
@@ -76,6 +77,25 @@ class HostBarrier {
   }
 
   bool joined() const { return page_ != nullptr; }
+
+  // Is the page really shared by every rank? (One container per rank, or a private /dev/shm, gives each
+  // rank its own page of the same name: every agreement would then wait out its timeout at the worst
+  // moment, teardown.) Two steps around one bootstrap barrier, so the answer is immediate, not a timeout:
+  // mark() writes this rank's identity word (`token`, the same on every rank, mixed with the rank);
+  // after every rank has marked (the caller's barrier), shared() checks every rank's word.
+  static uint64_t ident_of(uint64_t token, int rank) { return token ^ (0x9E3779B97F4A7C15ull * (uint64_t)(rank + 1)); }
+  void mark(uint64_t token) {
+    if (page_) page_->ident[rank_].store(ident_of(token, rank_), std::memory_order_release);
+  }
+  bool shared(uint64_t token, int* missing) const {
+    if (!page_) return false;
+    for (int r = 0; r < nranks_; ++r)
+      if (page_->ident[r].load(std::memory_order_acquire) != ident_of(token, r)) {
+        if (missing) *missing = r;
+        return false;
+      }
+    return true;
+  }
   const std::string& name() const { return name_; }
 
   // Next phase: this rank arrives, then waits until every rank has arrived. false = timed out

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include "crumbs.hpp"
 #include "device_exec.hpp"
 
 namespace flexar {
@@ -34,6 +35,10 @@ struct LaunchArgs {
   int max_fanin = 0;     // typed programs: the widest XFER fan-in (Program::max_nsrc; 0 = unknown, widest kernel)
   int wire = 0;          // EXEC / GROUP / QUERY of a typed program (Program::wire): 1 fp32, 2 e4m3, 3 e5m2,
                          // 4 / 5 MX e4m3 / e5m2
+  // breadcrumb of this launch (crumbs.hpp): the spec / purpose, the device epoch it runs as, its bytes
+  const char* tag = nullptr;
+  uint64_t epoch = 0;
+  uint64_t bytes = 0;
 };
 
 // Typed-program executors (exec_mx_kernel), SUM/AVG only: fp32 partials for 16/8-bit dtypes
@@ -94,7 +99,27 @@ FX_DECLARE_LAUNCH(u64)
 FX_DECLARE_LAUNCH(boolean)
 #undef FX_DECLARE_LAUNCH
 
+inline void launch_crumb(int dtype, int op, const LaunchArgs& a) {
+  CrumbArgs c;
+  c.type = CRUMB_LAUNCH;
+  c.launch_kind = (uint8_t)a.kind;
+  c.proto = (uint8_t)a.proto;
+  c.wire = (uint8_t)a.wire;
+  const bool grouped = a.kind == LAUNCH_GROUP || a.kind == LAUNCH_LL_GROUP;
+  c.rank = grouped ? (int16_t)-1 : (a.kind == LAUNCH_REDUCE ? (int16_t)-1 : (int16_t)a.ctx.rank);
+  c.nranks = (int16_t)(grouped ? a.nranks : a.ctx.nranks);
+  c.dtype = (int16_t)dtype;
+  c.op = (int16_t)op;
+  c.grid = (uint32_t)(grouped ? a.grid * a.nranks : a.grid);
+  c.epoch = a.epoch;
+  c.bytes = a.bytes;
+  c.what = a.kind == LAUNCH_REDUCE ? "reduce" : grouped ? "group" : "executor";
+  c.label = a.tag;
+  crumb(c);
+}
+
 inline int launch_dtype(int dtype, int op, const LaunchArgs& a) {
+  if (a.kind != LAUNCH_QUERY) launch_crumb(dtype, op, a);
   if (a.wire && (a.kind == LAUNCH_EXEC || a.kind == LAUNCH_GROUP || a.kind == LAUNCH_QUERY)) {
     if (op != FLEXAR_SUM && op != FLEXAR_AVG) return FLEXAR_ERR_UNSUPPORTED;
     return launch_mx(dtype, a);

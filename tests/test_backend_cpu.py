@@ -204,3 +204,43 @@ def test_backend_compression_option_is_agreed(settings):
                 (rank, picks, err)
         else:
             assert picks is None and "differs across ranks" in err, (rank, picks, err)
+
+
+class _PgStub:
+    def __init__(self, algo, world):
+        self.algo, self._world, self._rank = algo, world, 1
+        self._compress_name, self._mx_carrier = "mx_e4m3", None
+
+
+class _CommStub:
+    def __init__(self, ipc):
+        self.ipc = ipc
+
+    def topology(self):
+        return {"ipc": self.ipc}
+
+
+@pytest.mark.parametrize("algo,world,ipc,want", [
+    (None, 4, True, "flat+pull"),
+    ("flat+push", 8, True, "flat+push"),
+    ("flat+zc+push", 2, True, "flat+push"),  # the MX wire runs on staging: the zero-copy modifier is dropped
+    ("tree:4", 4, True, "tree:4"),
+    ("ring", 4, True, ""),              # the planner rejects a wire on a ring
+    ("rhd", 8, True, ""),
+    ("tree:2,4", 8, True, ""),
+    ("oneshot", 4, True, ""),
+    ("ll", 4, True, ""),
+    (None, 9, True, ""),                # more than 8 ranks: one reduction of every contribution is impossible
+    (None, 16, True, ""),
+    ("flat+rccl", 4, True, ""),         # message transport
+    (None, 4, False, ""),               # IPC unavailable: every call runs over RCCL
+])
+def test_backend_mx_wire_only_where_the_spec_carries_it(algo, world, ipc, want):
+    """FLEXAR_PG_COMPRESS applies the MX suffix only to a flat schedule of 2..8 ranks over
+    IPC; otherwise the call runs uncompressed instead of raising FlexarError inside the DDP / FSDP step."""
+    from allreduce_over_mpi_amd.parallel.backend import FlexarProcessGroup
+
+    pg = _PgStub(algo, world)
+    got = FlexarProcessGroup._mx_carrier_spec(pg, _CommStub(ipc))
+    assert got == want, (algo, world, ipc, got)
+    assert FlexarProcessGroup._mx_carrier_spec(pg, None) == want  # decided once

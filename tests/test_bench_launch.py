@@ -100,3 +100,58 @@ def test_main_dispatches_to_self_launch_without_touching_the_gpu(monkeypatch):
     import torch
 
     assert not torch.cuda.is_initialized()
+
+
+class _StubComm:
+    """What bench.readiness_record reads from a Communicator."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+    def topology(self):
+        return {"links": 7, "links_local": 7, "selftested": "fence,wt,ll,dma", "disabled": "wt",
+                "host_page": True, "host_page_shared": True,
+                "peers": [{"rank": 0, "link": "self"}, {"rank": 1, "link": "xgmi"}, {"rank": 2, "link": "xgmi"}]}
+
+
+def test_readiness_record_reports_what_readiness_did():
+    """the bench JSON names recovered / flaky families, every rank's notes (truncated),
+    the creation retry, the transport note and the host page, for the final and every earlier communicator."""
+    long_note = "x" * 500
+    comm = _StubComm(selftest_recovered=[], selftest_flaky=["wt"], selftest_notes={1: ["flat+pull+wt call 0: timeout"],
+                                                                                   2: [long_note]},
+                     retried="comm_connect: mapping failed", transport_note=None, host_page_note=None,
+                     calibration={"source": "measured"}, selftest_failed=["wt"])
+    creations = [bench.creation_record(comm, "rccl")]
+    rec = json.loads(json.dumps(bench.readiness_record(comm, creations)))  # JSON-serialisable
+    for k in ("links", "selftested", "disabled", "peer_links", "selftest_recovered", "selftest_flaky", "selftest_notes",
+              "retried", "transport_note", "host_page", "calibration", "creations"):
+        assert k in rec, k
+    assert rec["selftest_flaky"] == ["wt"] and rec["disabled"] == "wt" and rec["peer_links"] == ["xgmi"]
+    assert rec["selftest_notes"]["1"].startswith("flat+pull+wt") and len(rec["selftest_notes"]["2"]) == 300
+    assert rec["retried"] == "comm_connect: mapping failed"
+    assert rec["host_page"] == {"joined": True, "verified_shared": True, "note": None}
+    assert rec["creations"] == [{"transport": "rccl", "retried": "comm_connect: mapping failed",
+                                 "selftest_failed": ["wt"], "selftest_recovered": [], "selftest_flaky": ["wt"]}]
+
+
+def test_selftest_retry_policy_per_gpu_vs_shared():
+    """a family that fails once and passes the second pass is kept only when ranks share a
+    GPU (a descheduled rank is expected there); with one GPU per rank - the driver's N-GPU bench - it stays
+    disabled (flaky). A family that fails twice is disabled either way."""
+    from allreduce_over_mpi_amd.parallel.comm import selftest_policy
+
+    fence, wt = 1, 2
+    # shared GPU: fence recovered (kept), wt failed twice (disabled)
+    assert selftest_policy(fence | wt, wt, shared_gpu=True, mode="") == (wt, fence, 0)
+    # one GPU per rank: fence is flaky -> disabled as well
+    assert selftest_policy(fence | wt, wt, shared_gpu=False, mode="") == (fence | wt, 0, fence)
+    # overrides
+    assert selftest_policy(fence, 0, shared_gpu=False, mode="keep") == (0, fence, 0)
+    assert selftest_policy(fence, 0, shared_gpu=True, mode="disable") == (fence, 0, fence)
+    # nothing failed: nothing disabled
+    assert selftest_policy(0, 0, shared_gpu=False, mode="") == (0, 0, 0)
+    # the driver's one-GPU-per-rank environment sets no override
+    env = {}
+    bench.configure_env(8, 3, 3, env)
+    assert "FLEXAR_SELFTEST_RETRY" not in env

@@ -103,3 +103,19 @@ def test_bench_budget_drops_in_order(cuda):
     for k in ("config3", "config4", "config5", "small_msg"):
         assert k in items and k not in out, (k, items)
     assert out["value"] > 0 and out["cost_model_fit"] is None and out["bench_wall_s"] > 1
+
+
+def test_bench_json_names_a_recovered_selftest_family(cuda):
+    """rank 1 starts the first self-test family 1.5 s late (FLEXAR_SELFTEST_SKEW), past its
+    peer's 300 ms self-test watchdog: the fence family fails once and passes the second pass. The ranks
+    share one GPU, so it is kept - and the bench JSON says so (readiness.selftest_recovered, the notes and
+    the per-creation record); nothing is silent."""
+    out = _bench({"FLEXAR_SELFTEST_SKEW": "1:1500", "FLEXAR_SELFTEST_TIMEOUT_MS": "300"},
+                 ["--size-mb", "4", "--no-configs", "--no-calibrate", "--no-small", "--no-tune", "--algo", "flat+pull"])
+    rd = out["readiness"]
+    assert rd["selftest_recovered"] == ["fence"] and rd["selftest_flaky"] == [], rd
+    assert rd["disabled"] == "", rd
+    assert rd["selftest_notes"] and any("flat+pull" in v for v in rd["selftest_notes"].values()), rd
+    assert rd["creations"][0]["selftest_recovered"] == ["fence"], rd
+    assert rd["host_page"]["joined"] is True and rd["host_page"]["verified_shared"] is True, rd
+    assert out["value"] > 0

@@ -52,6 +52,9 @@ def _worker(rank, world, port, mode, q):
             os.environ["FLEXAR_TEST_SELFTEST_HIP"] = "0:15:1"  # rank 0, every IPC family, first communicator
         if mode == "absent":
             os.environ["FLEXAR_TIMEOUT_MS"] = "2000"
+        if mode == "private":  # every rank joins a page of its own (a private /dev/shm per container)
+            os.environ["FLEXAR_TEST_PAGE_PRIVATE"] = "1"
+            os.environ["FLEXAR_TIMEOUT_MS"] = "8000"
         import torch.distributed as dist
 
         torch.cuda.set_device(0)
@@ -90,6 +93,15 @@ def _worker(rank, world, port, mode, q):
                 comm.close()
                 out["close_s"] = time.monotonic() - t0
             dist.barrier()
+        elif mode == "private":
+            comm = Communicator(workspace_bytes=64 << 20)
+            topo = comm.topology()
+            out["page"] = (topo["host_page"], topo["host_page_shared"], comm.host_page_note)
+            out["err"] = _exact(comm, rank, world, 1 << 18)
+            comm.check()
+            t0 = time.monotonic()
+            comm.close()  # no page: no agreement to wait out; the exported buffers are parked
+            out["close_s"] = time.monotonic() - t0
         elif mode in ("hiperr", "retry"):
             comm = Communicator(workspace_bytes=64 << 20)
             out["failed"] = list(comm.selftest_failed)
@@ -148,6 +160,19 @@ def test_close_with_an_absent_peer_times_out_named(cuda):
     out, _ = _run(2, "absent")
     assert out[0]["err"] == 0.0 and out[1]["err"] == 0.0
     assert 1.5 < out[0]["close_s"] < 15.0, out[0]
+
+
+def test_private_host_page_is_detected_at_connect(cuda):
+    """ranks that do not share /dev/shm are told at connect (not by a teardown timeout):
+    the page is dropped on every rank, calls stay exact and close() returns without waiting out
+    FLEXAR_TIMEOUT_MS (8 s here)."""
+    out, _ = _run(2, "private")
+    for r in range(2):
+        o = out[r]
+        assert o["page"][0] is False and o["page"][1] is False, (r, o)
+        assert o["err"] == 0.0, (r, o)
+        assert o["close_s"] < 4.0, (r, o)
+    assert "host page not shared" in (out[0]["page"][2] or ""), out[0]
 
 
 @pytest.mark.parametrize("world", [2, 4])

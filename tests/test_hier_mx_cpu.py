@@ -60,3 +60,19 @@ def test_cross_node_mx_sum(wire):
     for rank, mism, same, tb in res:
         assert tb is None, tb
         assert mism == 0 and same, (rank, mism, same)
+
+
+def test_mx_cross_step_only_for_narrow_floats_and_few_nodes(monkeypatch):
+    """float64 (and integer) shards take the exact cross-node path; the MX all-gather grows
+    linearly with the node count, so beyond FLEXAR_HIER_MX_MAX_NODES (4) nodes the exact ring runs."""
+    from allreduce_over_mpi_amd.parallel.hierarchical import HierarchicalCommunicator
+
+    hc = object.__new__(HierarchicalCommunicator)
+    hc._torch = torch
+    for nodes, dt, want in [(2, torch.float32, True), (4, torch.bfloat16, True), (3, torch.float16, True),
+                            (2, torch.float64, False), (2, torch.int32, False), (5, torch.float32, False)]:
+        hc.nodes = nodes
+        assert hc._mx_applies(dt) is want, (nodes, dt)
+    monkeypatch.setenv("FLEXAR_HIER_MX_MAX_NODES", "8")
+    hc.nodes = 5
+    assert hc._mx_applies(torch.float32) is True

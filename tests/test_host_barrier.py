@@ -58,3 +58,49 @@ def test_barrier_names_the_absent_rank():
         assert "rank 2 did not arrive" in err, err
         assert 0.7 < dt < 10.0, dt
     assert not os.path.exists("/dev/shm" + name)
+
+
+def _page(name, rank, world, token, bdir, q):
+    from allreduce_over_mpi_amd import _native as nv
+    from allreduce_over_mpi_amd.parallel.comm import file_exchange
+    import ctypes
+
+    lib = nv.lib()
+    ex = file_exchange(bdir, rank, world, timeout_s=60)
+    h = lib.flexar_host_page_open(name.encode(), rank, world, token)
+    ex(b"")  # the bootstrap barrier after connect (every rank has marked)
+    t0 = time.monotonic()
+    missing = ctypes.c_int(-1)
+    shared = lib.flexar_host_page_shared(h, token, ctypes.byref(missing))
+    dt = time.monotonic() - t0
+    ex(b"")
+    lib.flexar_host_page_close(h)
+    q.put((rank, shared, missing.value, dt))
+
+
+@pytest.mark.parametrize("private", [False, True])
+def test_page_shared_check_is_immediate(private, tmp_path):
+    """at connect each rank writes a mark into the page; after one bootstrap barrier every
+    rank checks every mark. Ranks that joined different pages (one container per rank: a private /dev/shm,
+    simulated by per-rank names) learn it at once, not by an agreement timing out at teardown."""
+    world = 3
+    base = f"/flexar.test.{os.getpid()}.{uuid.uuid4().hex[:12]}"
+    token = 0x1234_5678_9ABC_DEF0
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_page, args=(base + (f".r{r}" if private else ""), r, world, token,
+                                             str(tmp_path), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in procs:
+        r, shared, missing, dt = q.get(timeout=90)
+        out[r] = (shared, missing, dt)
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for r, (shared, missing, dt) in out.items():
+        assert shared == (0 if private else 1), (r, out)
+        assert dt < 0.5, (r, dt)
+        if private:
+            assert missing != r and 0 <= missing < world, (r, missing)
