@@ -91,6 +91,7 @@ def _sig(lib):
         "flexar_dequantize_fp8": (i, [vp, vp, i, sz, vp, f, vp]),
         "flexar_mx_pack": (i, [vp, i, vp, sz, i, vp]),
         "flexar_mx_unpack_sum": (i, [vp, sz, i, sz, i, vp, vp]),
+        "flexar_mx_unpack_sum_scaled": (i, [vp, sz, i, sz, i, f, vp, vp]),
         "flexar_group_broadcast": (i, [c.POINTER(vp), i, i, c.POINTER(vp), c.POINTER(vp), sz, i, vp, cp]),
         "flexar_simulate_bcast": (i, [cp, i, sz, i, i, c.POINTER(vp), c.POINTER(vp), i, i]),
         "flexar_simulate_typed": (i, [cp, i, sz, i, i, c.POINTER(vp), c.POINTER(vp), i, i, f, f]),

@@ -200,10 +200,10 @@ def mx_pack(x, wire: str = "e4m3", out=None, stream=None):
     return msg
 
 
-def mx_unpack_sum(msgs, n: int, wire: str = "e4m3", out=None, stream=None):
+def mx_unpack_sum(msgs, n: int, wire: str = "e4m3", out=None, stream=None, post: float = 1.0):
     """Sum of the dequantised MX messages ``msgs`` (uint8 [k, >= mx_message_bytes(n)], contiguous) in row
     order, fp32, in one pass (csrc/src/k_mx_codec.hip) - bitwise ``mx_dequantize`` of each row summed in
-    order."""
+    order, times ``post`` (AVG's 1 / world fused into the same pass; 1 = none)."""
     import torch
 
     if not msgs.is_cuda or msgs.dim() != 2 or msgs.dtype != torch.uint8 or not msgs.is_contiguous():
@@ -211,7 +211,7 @@ def mx_unpack_sum(msgs, n: int, wire: str = "e4m3", out=None, stream=None):
     y = torch.empty(n, dtype=torch.float32, device=msgs.device) if out is None else out
     if y.dtype != torch.float32 or y.numel() != n or not y.is_contiguous():
         raise nv.FlexarError(1, "mx_unpack_sum: out must be contiguous float32 of n elements")
-    nv.check(nv.lib().flexar_mx_unpack_sum(msgs.data_ptr(), msgs.shape[1], msgs.shape[0], n,
-                                           _MX_WIRE_CODES[wire], y.data_ptr(), _stream_handle(stream)),
-             "mx_unpack_sum")
+    nv.check(nv.lib().flexar_mx_unpack_sum_scaled(msgs.data_ptr(), msgs.shape[1], msgs.shape[0], n,
+                                                  _MX_WIRE_CODES[wire], float(post), y.data_ptr(),
+                                                  _stream_handle(stream)), "mx_unpack_sum")
     return y

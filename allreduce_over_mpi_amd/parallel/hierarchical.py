@@ -154,26 +154,29 @@ class HierarchicalCommunicator:
             return False
         return self.nodes <= int(os.environ.get("FLEXAR_HIER_MX_MAX_NODES", "4") or 4)
 
-    def _cross_all_reduce_mx(self, t, wire: str):
+    def _cross_all_reduce_mx(self, t, wire: str, post: float = 1.0):
         """Cross-node SUM of a float shard with OCP MX fp8 on the network (a scale per 32-element block): each
         node's shard is quantised once, payload and scales are all-gathered in one message (1.03 bytes per
         element per node instead of a ring allreduce's 2 (n-1)/n x 4), and every node sums the dequantised
-        shards in node order in fp32 - identical results everywhere. Worth it for up to ~4 nodes, where the
-        all-gather moves fewer bytes than the ring."""
+        shards in node order in fp32 - identical results everywhere; ``post`` (AVG's 1 / world) multiplies the
+        fp32 sum in the same pass. Worth it for up to ~4 nodes, where the all-gather moves fewer bytes than the
+        ring."""
         from ..ops.quant import mx_dequantize, mx_quantize
 
-        if self.nodes == 1:
-            return t
         torch = self._torch
+        if self.nodes == 1:
+            if post != 1.0:
+                t.copy_((t.float() * post).to(t.dtype))
+            return t
         n = t.numel()
         if t.is_cuda:  # native codec (csrc/src/k_mx_codec.hip): one pass to pack, one to dequantise and sum
             from ..ops.quant import mx_pack, mx_unpack_sum
 
             msgs = self._cross_gather(mx_pack(t.contiguous(), wire))
             if t.dtype == torch.float32 and t.is_contiguous():
-                mx_unpack_sum(msgs, n, wire, out=t.view(-1))
+                mx_unpack_sum(msgs, n, wire, out=t.view(-1), post=post)
             else:
-                t.copy_(mx_unpack_sum(msgs, n, wire).view(t.shape))
+                t.copy_(mx_unpack_sum(msgs, n, wire, post=post).view(t.shape))
             return t
         q, sb = mx_quantize(t.float(), wire)
         # one message per node: the fp8 payload followed by its scale bytes
@@ -182,7 +185,7 @@ class HierarchicalCommunicator:
         for msg in msgs:
             v = mx_dequantize(msg[:n].view(q.dtype), msg[n:], n)
             acc = v if acc is None else acc + v
-        t.copy_(acc.to(t.dtype))
+        t.copy_((acc * post if post != 1.0 else acc).to(t.dtype))
         return t
 
     def all_reduce(self, tensor, op: str = "sum", out=None, algo: Optional[str] = None,
@@ -202,11 +205,16 @@ class HierarchicalCommunicator:
         n = flat.numel()
         m = n // self.L
         main = m * self.L
+        scaled_upto = 0  # elements whose AVG scale is already applied (fused into the MX unpack-sum)
         if m > 0:
             shard = torch.empty(m, dtype=flat.dtype, device=flat.device)
             self.local.reduce_scatter(flat[:main], shard, op=red, algo=algo)
             if compress and red == "sum" and self._mx_applies(flat.dtype):
-                self._cross_all_reduce_mx(shard, {"mx_e4m3": "e4m3", "mx_e5m2": "e5m2"}[compress])
+                # AVG's 1 / world rides in the unpack-sum pass: no separate pass over the
+                # shard or over the gathered buffer
+                post = 1.0 / self.world if op == "avg" else 1.0
+                self._cross_all_reduce_mx(shard, {"mx_e4m3": "e4m3", "mx_e5m2": "e5m2"}[compress], post)
+                scaled_upto = main if op == "avg" else 0
             else:
                 self._cross_all_reduce(shard, red)
             self.local.all_gather(shard, flat[:main], algo=algo)
@@ -215,8 +223,8 @@ class HierarchicalCommunicator:
             self.local.all_reduce(tail, op=red)
             self._cross_all_reduce(tail, red)
             flat[main:].copy_(tail)
-        if op == "avg":
-            flat.mul_(1.0 / self.world)
+        if op == "avg" and scaled_upto < n:
+            flat[scaled_upto:].mul_(1.0 / self.world)
         return dst
 
     def close(self):

@@ -57,6 +57,23 @@ def main():
                 fn()
             torch.cuda.synchronize()
             res[name] = round((time.perf_counter() - t0) / 10 * 1e6, 1)
+        # device time of the native kernels alone (hipEvents around 20 back-to-back calls) and their effective
+        # HBM rate: pack reads 4 B and writes 1 + 1/32 B per element; unpack-sum reads nodes x (1 + 1/32) B and
+        # writes 4 B (VERDICT r4 item 6 targets: >= 5 / >= 4.5 TB/s at 32 M elements)
+        for name, fn, nbytes in (("native_pack", native_pack, n * 4 + n * 33 / 32),
+                                 ("native_unpack_sum", native_combine, nodes * n * 33 / 32 + n * 4)):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(20):
+                fn()
+            b.record()
+            torch.cuda.synchronize()
+            us = a.elapsed_time(b) / 20 * 1e3
+            res[name + "_event_us"] = round(us, 1)
+            res[name + "_TBps"] = round(nbytes / (us * 1e-6) / 1e12, 2)
+        # AVG fused into the unpack-sum: bitwise the separate multiply in fp32
+        from allreduce_over_mpi_amd.ops.quant import mx_unpack_sum as _mus
+        assert torch.equal(_mus(big, n, "e4m3", post=0.25), combine() * 0.25)
         # fp32 bytes a ring allreduce over `nodes` moves per rank, at 50 GB/s of network per GPU
         res["ring_fp32_net_us_at_50GBps"] = round(2 * (nodes - 1) / nodes * 4 * n / 50e9 * 1e6, 1)
         res["mx_allgather_net_us_at_50GBps"] = round((nodes - 1) * n * 33 / 32 / 50e9 * 1e6, 1)

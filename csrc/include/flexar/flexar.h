@@ -276,6 +276,9 @@ int flexar_mx_pack(const void* x, int dtype, void* msg, size_t n, int wire, void
 /* out[i] = sum over nmsg messages (msg_stride bytes apart), in order, of q_k[i] * 2^X_k (fp32). */
 int flexar_mx_unpack_sum(const void* msgs, size_t msg_stride, int nmsg, size_t n, int wire, float* out,
                          void* hip_stream);
+/* Same, times `post` (AVG's 1 / world fused into the pass; 1 = none). */
+int flexar_mx_unpack_sum_scaled(const void* msgs, size_t msg_stride, int nmsg, size_t n, int wire, float post,
+                                float* out, void* hip_stream);
 
 /* ---- helpers --------------------------------------------------------------- */
 int flexar_pointer_is_device(const void* p); /* 1 if p is device memory */

@@ -615,6 +615,17 @@ __device__ FX_INLINE void fp8_round_g(float (&x)[G]) {
 // ~4-8 outstanding 16-B loads per lane as the untyped path).
 enum : int { SP_T = 0, SP_TW = 1, SP_W = 2 };
 
+// Per-lane batch of the typed executors (xfer_mx / xfer_mxb): UU super-groups' loads are issued before the
+// first conversion - 4 when a group needs at most FLEXAR_TYPED_UU4_MAXV 16-B vectors per lane, 2 up to
+// FLEXAR_TYPED_UU2_MAXV, else 1. Build-time knobs for A/B builds (bytes in flight).
+#ifndef FLEXAR_TYPED_UU4_MAXV
+#define FLEXAR_TYPED_UU4_MAXV 2
+#endif
+#ifndef FLEXAR_TYPED_UU2_MAXV
+#define FLEXAR_TYPED_UU2_MAXV 4
+#endif
+constexpr int typed_uu(int v) { return v <= FLEXAR_TYPED_UU4_MAXV ? 4 : (v <= FLEXAR_TYPED_UU2_MAXV ? 2 : 1); }
+
 template <typename T, typename W, int K, int SP, int PM>
 __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (&d)[kMaxDst], int nd, uint32_t dm,
                                   uint64_t n, float scale, float pre, float post_inv, bool vec) {
@@ -623,7 +634,7 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
   constexpr int VT = (int)sizeof(T) * G / 16, VW = (int)sizeof(W) * G / 16;
   constexpr int VM = VT > VW ? VT : VW;
   constexpr int V = SP == SP_T ? K * VT : (SP == SP_TW ? VT + (K - 1) * VW : K * VW);
-  constexpr int UU = V <= 2 ? 4 : (V <= 4 ? 2 : 1);
+  constexpr int UU = typed_uu(V);
   constexpr bool FP8 = sizeof(W) == 1;
   constexpr bool WT = PM == PM_WT;
   constexpr bool NTS = PM == PM_FENCE_NTS;
@@ -1075,7 +1086,7 @@ __device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_
   constexpr int G = 16;
   constexpr int VT = (int)sizeof(T);  // 16-B vectors per group of T (W: one)
   constexpr int V = SP == SP_T ? VT : (SP == SP_TW ? VT + (K - 1) : K);
-  constexpr int UU = V <= 2 ? 4 : (V <= 4 ? 2 : 1);
+  constexpr int UU = typed_uu(V);
   constexpr bool WT = PM == PM_WT;
   constexpr bool NTS = PM == PM_FENCE_NTS;
   auto isw = [](int k) constexpr -> bool { return SP == SP_W || (SP == SP_TW && k > 0); };

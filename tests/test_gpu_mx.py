@@ -157,3 +157,12 @@ def test_mx_codec_matches_reference(cuda, wire, dtype):
             want_sum = v if want_sum is None else want_sum + v
         got = mx_unpack_sum(msgs, n, wire).cpu()
         assert torch.equal(got, want_sum), (n, int((got != want_sum).sum()))
+        # AVG's 1 / world fused into the same pass (hierarchical.py): bitwise the fp32 multiply after the sum
+        got = mx_unpack_sum(msgs, n, wire, post=1.0 / 3).cpu()
+        assert torch.equal(got, want_sum * (1.0 / 3)), (n, int((got != want_sum * (1.0 / 3)).sum()))
+        # unaligned message rows (the all-gathered rows are mx_message_bytes(n) apart): the 16-B accesses
+        mb = mx_message_bytes(n)
+        buf = torch.zeros(3 * mb + 8, dtype=torch.uint8, device=cuda)
+        buf[3:3 + 3 * mb] = msgs.reshape(-1)
+        got = mx_unpack_sum(buf[3:3 + 3 * mb].view(3, mb), n, wire).cpu()  # base 3 B past an allocation
+        assert torch.equal(got, want_sum), n
