@@ -350,7 +350,7 @@ class Communicator:
             for fam in nv.FAMILIES.values():
                 if mask & fam:
                     again |= run(fam)
-            local_shared = any(p["link"] == "same" for p in self.topology()["peers"] if p["rank"] != self.rank)
+            local_shared = shares_gpu(self.topology(), self.rank)
             shared_any = any(r == b"1" for r in exchange(b"1" if local_shared else b"0"))
             mask, recovered, flaky = selftest_policy(mask, again, shared_any)
             self.selftest_recovered = nv.family_names(recovered)
@@ -765,6 +765,11 @@ class Communicator:
             self.close(collective=False)  # GC order differs per rank: never wait for peers here
         except Exception:
             pass
+
+
+def shares_gpu(topology: dict, rank: int) -> bool:
+    """True when some peer of ``rank`` runs on the same device (the probe's "same-device" link class)."""
+    return any(p["link"] == "same-device" for p in topology["peers"] if p["rank"] != rank)
 
 
 def selftest_policy(first: int, second: int, shared_gpu: bool, mode: Optional[str] = None):

@@ -52,70 +52,90 @@ __device__ __forceinline__ uint32_t mxc_f32_bits(const uint32_t* w, int e) {
   else return __float_as_uint(f16_to_f32((uint16_t)((w[e / 2] >> (16 * (e & 1))) & 0xffffu)));
 }
 
-// Pack, 16 elements per lane: a 32-element block is a lane pair (2m, 2m + 1) - one xor-shuffle combines the
-// halves' amax - and a lane's 16 fp8 values are ONE 16-B store; the input is 1 (fp16 / bf16: 2, fp32: 4)
-// 16-B loads per lane. q = rne(x / 2^X) through gfx950's scaled converts (v_cvt_scalef32_pk_fp8_*: only the
-// scale's exponent counts, as in the MX executor), the same values mx_quantize gives. Whole blocks only; the
-// last partial block (< 32 elements) is mx_pack_tail's.
+// Pack. A wave takes chunks of 64 x 16 elements (32 blocks); 16-B sub-chunk j of lane l holds elements
+// 64 E j + E l .. + E (E = 16 / sizeof(T): 4 fp32, 8 bf16 / fp16), so every load instruction covers 1 KiB
+// contiguous across the wave, and so does every fp8 store (E bytes per lane). A 32-element block is
+// 32 / E consecutive lanes of one sub-chunk: its amax takes log2(32 / E) xor-shuffles. q = rne(x / 2^X)
+// through gfx950's scaled converts (v_cvt_scalef32_pk_fp8_*: only the scale's exponent counts, as in the MX
+// executor), the values mx_quantize gives. Whole blocks only (`nwhole` elements, a multiple of 32: a block is
+// wholly inside or outside); the last partial block is mx_pack_tail's.
 template <typename T, typename W>
 __global__ void __launch_bounds__(kMxcThreads) mx_pack16_kernel(const T* __restrict__ x, uint8_t* __restrict__ msg,
-                                                                uint64_t n, uint64_t nhalf) {
+                                                                uint64_t n, uint64_t nwhole) {
   constexpr bool E4 = __is_same(W, mxe4m3_t);
-  constexpr int VT = (int)sizeof(T);  // 16-B vectors per 16 elements
-  const uint64_t stride = (uint64_t)gridDim.x * kMxcThreads;  // even: lane pairs never split
-  for (uint64_t g = (uint64_t)blockIdx.x * kMxcThreads + threadIdx.x; g < nhalf; g += stride) {
-    uint32_t w[4 * VT];
+  constexpr int E = 16 / (int)sizeof(T);  // elements per 16-B sub-chunk
+  constexpr int J = (int)sizeof(T);       // sub-chunks per lane per chunk (64 x 16 elements)
+  constexpr int LPB = kMxBlock / E;       // lanes per block
+  constexpr uint64_t kChunk = 64 * 16;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t)blockIdx.x * (kMxcThreads / 64) + (threadIdx.x >> 6);
+  const uint64_t nwaves = (uint64_t)gridDim.x * (kMxcThreads / 64);
+  for (uint64_t base = wave * kChunk; base < nwhole; base += nwaves * kChunk) {
+    uint4 raw[J];
 #pragma unroll
-    for (int j = 0; j < VT; ++j) {
-      const uint4 v = mxc_ld16((const char*)x + (g * 16 * sizeof(T)) + 16 * j);
-      w[4 * j] = v.x; w[4 * j + 1] = v.y; w[4 * j + 2] = v.z; w[4 * j + 3] = v.w;
+    for (int j = 0; j < J; ++j) {
+      const uint64_t e0 = base + (uint64_t)(64 * j + lane) * E;
+      raw[j] = e0 < nwhole ? mxc_ld16((const char*)x + e0 * sizeof(T)) : uint4{0, 0, 0, 0};
     }
-    uint32_t am = 0;
 #pragma unroll
-    for (int e = 0; e < 16; ++e) am = max(am, mxc_f32_bits<T>(w, e) & 0x7fffffffu);
-    am = max(am, (uint32_t)__shfl_xor((int)am, 1));
-    const uint32_t xr = mx_scale_byte(am, E4);
-    const float sc = mx_scale_value(xr);
-    uint32_t q[4];
+    for (int j = 0; j < J; ++j) {
+      const uint64_t e0 = base + (uint64_t)(64 * j + lane) * E;
+      const uint32_t w[4] = {raw[j].x, raw[j].y, raw[j].z, raw[j].w};
+      uint32_t am = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      mxc_s2 r = {0, 0};
-      if constexpr (sizeof(T) == 4) {
-        const float* f = reinterpret_cast<const float*>(w);
-        if constexpr (E4) {
-          r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(r, f[4 * i], f[4 * i + 1], sc, false);
-          r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(r, f[4 * i + 2], f[4 * i + 3], sc, true);
+      for (int e = 0; e < E; ++e) am = max(am, mxc_f32_bits<T>(w, e) & 0x7fffffffu);
+#pragma unroll
+      for (int o = LPB / 2; o > 0; o >>= 1) am = max(am, (uint32_t)__shfl_xor((int)am, o));
+      const uint32_t xr = mx_scale_byte(am, E4);
+      const float sc = mx_scale_value(xr);
+      uint32_t q[E / 4];
+#pragma unroll
+      for (int i = 0; i < E / 4; ++i) {
+        mxc_s2 r = {0, 0};
+        if constexpr (sizeof(T) == 4) {
+          const float* f = reinterpret_cast<const float*>(w);
+          if constexpr (E4) {
+            r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(r, f[4 * i], f[4 * i + 1], sc, false);
+            r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(r, f[4 * i + 2], f[4 * i + 3], sc, true);
+          } else {
+            r = __builtin_amdgcn_cvt_scalef32_pk_bf8_f32(r, f[4 * i], f[4 * i + 1], sc, false);
+            r = __builtin_amdgcn_cvt_scalef32_pk_bf8_f32(r, f[4 * i + 2], f[4 * i + 3], sc, true);
+          }
+        } else if constexpr (__is_same(T, bf16_t)) {
+          mxc_bf2 a, b;
+          __builtin_memcpy(&a, &w[2 * i], 4);
+          __builtin_memcpy(&b, &w[2 * i + 1], 4);
+          if constexpr (E4) {
+            r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, a, sc, false);
+            r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, b, sc, true);
+          } else {
+            r = __builtin_amdgcn_cvt_scalef32_pk_bf8_bf16(r, a, sc, false);
+            r = __builtin_amdgcn_cvt_scalef32_pk_bf8_bf16(r, b, sc, true);
+          }
         } else {
-          r = __builtin_amdgcn_cvt_scalef32_pk_bf8_f32(r, f[4 * i], f[4 * i + 1], sc, false);
-          r = __builtin_amdgcn_cvt_scalef32_pk_bf8_f32(r, f[4 * i + 2], f[4 * i + 3], sc, true);
+          mxc_h2 a, b;
+          __builtin_memcpy(&a, &w[2 * i], 4);
+          __builtin_memcpy(&b, &w[2 * i + 1], 4);
+          if constexpr (E4) {
+            r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(r, a, sc, false);
+            r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(r, b, sc, true);
+          } else {
+            r = __builtin_amdgcn_cvt_scalef32_pk_bf8_f16(r, a, sc, false);
+            r = __builtin_amdgcn_cvt_scalef32_pk_bf8_f16(r, b, sc, true);
+          }
         }
-      } else if constexpr (__is_same(T, bf16_t)) {
-        mxc_bf2 a, b;
-        __builtin_memcpy(&a, &w[2 * i], 4);
-        __builtin_memcpy(&b, &w[2 * i + 1], 4);
-        if constexpr (E4) {
-          r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, a, sc, false);
-          r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, b, sc, true);
-        } else {
-          r = __builtin_amdgcn_cvt_scalef32_pk_bf8_bf16(r, a, sc, false);
-          r = __builtin_amdgcn_cvt_scalef32_pk_bf8_bf16(r, b, sc, true);
-        }
-      } else {
-        mxc_h2 a, b;
-        __builtin_memcpy(&a, &w[2 * i], 4);
-        __builtin_memcpy(&b, &w[2 * i + 1], 4);
-        if constexpr (E4) {
-          r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(r, a, sc, false);
-          r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(r, b, sc, true);
-        } else {
-          r = __builtin_amdgcn_cvt_scalef32_pk_bf8_f16(r, a, sc, false);
-          r = __builtin_amdgcn_cvt_scalef32_pk_bf8_f16(r, b, sc, true);
-        }
+        __builtin_memcpy(&q[i], &r, 4);
       }
-      __builtin_memcpy(&q[i], &r, 4);
+      if (e0 < nwhole) {
+        if constexpr (E == 4) {
+          *(uint32_t*)(msg + e0) = q[0];  // 4 B per lane, 256 B contiguous across the wave
+        } else {
+          typedef unsigned int u2a1 __attribute__((ext_vector_type(2), aligned(1)));
+          *(u2a1*)(msg + e0) = u2a1{q[0], q[1]};  // 8 B per lane, 512 B contiguous across the wave
+        }
+        if (lane % LPB == 0) msg[n + e0 / kMxBlock] = (uint8_t)xr;
+      }
     }
-    mxc_st16(msg + g * 16, uint4{q[0], q[1], q[2], q[3]});
-    if (!(g & 1)) msg[n + g / 2] = (uint8_t)xr;
   }
 }
 
@@ -219,16 +239,16 @@ using namespace flexar;
 
 template <typename T, typename W>
 static void mx_pack_launch(const void* x, void* msg, uint64_t n, hipStream_t s) {
-  const uint64_t nhalf = (n / kMxBlock) * 2;  // 16-element halves of whole blocks
-  if (nhalf) {
+  const uint64_t nwhole = (n / kMxBlock) * kMxBlock;  // elements in whole blocks
+  if (nwhole) {
+    const int g = mxc_grid((nwhole + 15) / 16);  // one 16-element item per lane
     CrumbArgs ca;
     ca.type = CRUMB_LAUNCH;
     ca.what = "mx_pack16_kernel";
     ca.bytes = n * sizeof(T);
-    ca.grid = (uint32_t)mxc_grid(nhalf);
+    ca.grid = (uint32_t)g;
     crumb(ca);
-    hipLaunchKernelGGL((mx_pack16_kernel<T, W>), mxc_grid(nhalf), kMxcThreads, 0, s, (const T*)x, (uint8_t*)msg, n,
-                       nhalf);
+    hipLaunchKernelGGL((mx_pack16_kernel<T, W>), g, kMxcThreads, 0, s, (const T*)x, (uint8_t*)msg, n, nwhole);
   }
   if (n % kMxBlock)
     hipLaunchKernelGGL((mx_pack_tail_kernel<T, W>), 1, 64, 0, s, (const T*)x, (uint8_t*)msg, n,

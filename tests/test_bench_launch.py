@@ -151,6 +151,12 @@ def test_selftest_retry_policy_per_gpu_vs_shared():
     assert selftest_policy(fence, 0, shared_gpu=True, mode="disable") == (fence, 0, fence)
     # nothing failed: nothing disabled
     assert selftest_policy(0, 0, shared_gpu=False, mode="") == (0, 0, 0)
+    # the link-class names the probe reports (csrc/include/flexar/readiness.hpp link_name)
+    from allreduce_over_mpi_amd.parallel.comm import shares_gpu
+
+    topo = {"peers": [{"rank": 0, "link": "self"}, {"rank": 1, "link": "same-device"}]}
+    assert shares_gpu(topo, 0) and not shares_gpu({"peers": [{"rank": 0, "link": "self"},
+                                                            {"rank": 1, "link": "xgmi"}]}, 0)
     # the driver's one-GPU-per-rank environment sets no override
     env = {}
     bench.configure_env(8, 3, 3, env)

@@ -569,6 +569,9 @@ def _readiness_worker(rank, world, port, q, fault):
                           FLEXAR_TIMEOUT_MS="20000", FLEXAR_SELFTEST_TIMEOUT_MS="300")
         if fault.startswith("skew:"):
             os.environ["FLEXAR_SELFTEST_SKEW"] = fault[5:]
+        elif fault.startswith("skewstrict:"):  # the one-GPU-per-rank policy, forced on the shared GPU
+            os.environ["FLEXAR_SELFTEST_SKEW"] = fault[11:]
+            os.environ["FLEXAR_SELFTEST_RETRY"] = "disable"
         elif fault:
             os.environ["FLEXAR_FAULT_INJECT"] = fault
         import torch.distributed as dist
@@ -599,7 +602,7 @@ def _readiness_worker(rank, world, port, q, fault):
         q.put((rank, None, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("fault", ["", "drop:1:0:0", "skew:1:1500"])
+@pytest.mark.parametrize("fault", ["", "drop:1:0:0", "skew:1:1500", "skewstrict:1:1500"])
 def test_ipc_connect_readiness_gate(cuda, fault):
     """Connect-time probe + exact self-test (readiness.hpp). Healthy: every family verified, peers on the
     same GPU. With rank 1 dropping its slot-0 SIGNAL (every executor schedule then breaks), the self-test
@@ -628,6 +631,8 @@ def test_ipc_connect_readiness_gate(cuda, fault):
         assert stats["resident_blocks"] >= 256, stats
         if fault.startswith("skew:"):
             assert recovered == ["fence"] and failed == [] and stats["disabled"] == "", (recovered, failed, stats)
+        elif fault.startswith("skewstrict:"):  # passed the repeat, disabled anyway
+            assert recovered == [] and failed == ["fence"] and stats["disabled"] == "fence", (recovered, failed, stats)
         elif fault:
             assert failed == ["fence", "wt"], failed
             assert stats["disabled"] == "fence,wt"
