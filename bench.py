@@ -298,6 +298,16 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     ph(f"device {local} set")
+    # the native library (and its fatal-signal / terminate report) before the process group: a fault inside
+    # torch's eager RCCL initialisation - where the round-4 rehearsal fault surfaced, docs/ROUND5.md - then
+    # prints this rank's breadcrumbs too, which show that no flexar launch had been issued
+    from allreduce_over_mpi_amd import _native as nv
+
+    global _NV
+    nv.lib()
+    _NV = nv
+    nv._T0 = _T_START  # the communicator's phase lines count from this process's start too
+    ph("native library loaded")
     if world > 1:
         if host_ref:
             dist.init_process_group("gloo")
@@ -307,15 +317,8 @@ def main():
     if args.gpus != world:
         log(rank, f"note: --gpus {args.gpus} but WORLD_SIZE={world}; benchmarking {world} rank(s)")
 
-    from allreduce_over_mpi_amd import _native as nv
     from allreduce_over_mpi_amd.parallel.comm import Communicator
     from allreduce_over_mpi_amd.utils.perf import algbw_gbps, busbw_gbps
-
-    global _NV
-    nv.lib()
-    _NV = nv
-    nv._T0 = _T_START  # the communicator's phase lines count from this process's start too
-    ph("native library loaded")
 
     dtype = getattr(torch, args.dtype)
     esize = torch.tensor([], dtype=dtype).element_size()

@@ -41,6 +41,16 @@ def _diag(r, name):
     return "\n".join(["-- progress:"] + progress + ["-- errors:"] + errors[:25] + ["-- tail:", text[-1500:]])
 
 
+def _keep(r, name):
+    """Every bench run's whole output under gpurun_out/ (the per-rank phase timelines)."""
+    try:
+        os.makedirs(os.path.join(REPO, "gpurun_out", "bench_tests"), exist_ok=True)
+        with open(os.path.join(REPO, "gpurun_out", "bench_tests", f"{name}.log"), "w") as f:
+            f.write((r.stdout or "") + "\n" + (r.stderr or ""))
+    except OSError:
+        pass
+
+
 def test_bench_json_and_fallback_chain_two_ranks(cuda):
     env = dict(os.environ, FLEXAR_BENCH_SHARED_GPU="1", FLEXAR_BENCH_SHARED_RCCL="1", FLEXAR_BENCH_REJECT_FIRST="1",
                FLEXAR_NO_BUILD="1")
@@ -48,6 +58,7 @@ def test_bench_json_and_fallback_chain_two_ranks(cuda):
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(REPO, "bench.py"),
            "--gpus", "2", "--steps", "3", "--warmup", "1", "--size-mb", "16", "--no-calibrate", "--no-small"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110, cwd=REPO)
+    _keep(r, "fallback")
     assert r.returncode == 0, _diag(r, "fallback")
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
@@ -69,6 +80,7 @@ def _bench(extra_env, args, timeout=300):
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(REPO, "bench.py"),
            "--gpus", "2", "--steps", "3", "--warmup", "1", *args]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=REPO)
+    _keep(r, "sections_" + "_".join(sorted(extra_env)) if extra_env else "sections")
     assert r.returncode == 0, _diag(r, "sections")
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
