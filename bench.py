@@ -788,6 +788,9 @@ def main():
         "hbm_TBps_per_rank": hbm_tbps,  # HBM traffic of the timed schedule / step time (MI355X peak ~8 TB/s)
         "peer_traffic_per_rank": link_rate,  # program-cost link bytes / step time (N > 1)
         "rccl_busbw_GBps": rccl_busbw,
+        # the same-node bar: flexar's busbw over RCCL's on the same buffer, same ranks, same
+        # box (vs_baseline compares with the reference's CPU/MPICH number, which is context only)
+        "vs_rccl": round(busbw / rccl_busbw, 3) if rccl_busbw else None,
         "fallback": fallback,
         "tuner": tune_log or None,
         "cost_model": model,
