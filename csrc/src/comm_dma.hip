@@ -9,7 +9,9 @@ namespace flexar {
 int reduce_chain(char* dst, char* dst2, const char* const* srcs, int nsrc, uint64_t count, int dtype,
                         int op, float fs, hipStream_t st, int proto) {
   const size_t es = dtype_size(dtype);
-  int grid = (int)std::min<uint64_t>(1024, std::max<uint64_t>(1, count * es / (64 * 1024)));
+  // FLEXAR_REDUCE_GRID: workgroup cap of the standalone reduction (A/B; default 1024, one per 64 KiB below it)
+  static const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(env_u64("FLEXAR_REDUCE_GRID", 1024), 65535));
+  int grid = (int)std::min<uint64_t>(cap, std::max<uint64_t>(1, count * es / (64 * 1024)));
   int done = 0;
   while (done < nsrc) {
     SrcTable t;
@@ -28,7 +30,10 @@ int reduce_chain(char* dst, char* dst2, const char* const* srcs, int nsrc, uint6
     la.dst2 = last ? dst2 : nullptr;
     la.n = count;
     la.scale = last ? fs : 1.0f;
-    la.vec = vec_ok_for(al) ? 1 : 0;
+    // the standalone reduction takes the grid-interleaved form (device_exec.hpp reduce_interleaved);
+    // FLEXAR_REDUCE_SLICES=1 keeps per-workgroup slices (A/B)
+    static const bool slices = env_u64("FLEXAR_REDUCE_SLICES", 0) != 0;
+    la.vec = (vec_ok_for(al) ? 1 : 0) | (proto != PM_WT && !slices ? 2 : 0);
     la.grid = grid;
     la.stream = st;
     la.proto = proto;

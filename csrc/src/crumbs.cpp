@@ -159,13 +159,23 @@ void on_terminate() {
 
 }  // namespace
 
+bool crumbs_on() {
+  static const bool on = [] {
+    const char* e = getenv("FLEXAR_CRASH_REPORT");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+
 void crumb(const CrumbArgs& a) {
+  if (!crumbs_on()) return;  // FLEXAR_CRASH_REPORT=0: no ring, no report
   const uint64_t s = g_next.fetch_add(1, std::memory_order_relaxed);
   Crumb& c = g_ring[s & (kCrumbs - 1)];
   c.seq.store(0, std::memory_order_relaxed);
   std::atomic_signal_fence(std::memory_order_seq_cst);
   c.t_ns = now_ns();
-  c.tid = (uint32_t)syscall(SYS_gettid);
+  static thread_local const uint32_t tid = (uint32_t)syscall(SYS_gettid);  // once per thread: no syscall per launch
+  c.tid = tid;
   c.type = a.type;
   c.launch_kind = a.launch_kind;
   c.proto = a.proto;
@@ -254,8 +264,7 @@ void crash_report_write(const char* why) {
 void crash_report_install() {
   int expected = 0;
   if (!g_installed.compare_exchange_strong(expected, 1)) return;
-  const char* e = getenv("FLEXAR_CRASH_REPORT");
-  if (e && *e == '0') return;
+  if (!crumbs_on()) return;
   for (int sig : kSignals) {
     struct sigaction sa;
     memset(&sa, 0, sizeof(sa));

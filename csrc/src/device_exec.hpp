@@ -1645,11 +1645,73 @@ struct SrcTable {
   const char* p[kMaxSrc];
 };
 
+// Grid-interleaved form of the standalone reduction (reduce_kernel, vec bit 1): step i of workgroup b covers the
+// U x nt 16-B vectors at (i * grid + b) * U * nt of EVERY source, so at any moment the whole grid reads one
+// narrow window of each of the K sources (DRAM pages stay open for every workgroup) instead of K x grid
+// far-apart streams - the slice form's per-workgroup contiguous spans. Results are identical (the same
+// combine16 per element; only which workgroup computes an element changes).
+template <typename T, typename OP, int K>
+__device__ FX_INLINE void reduce_interleaved(const char* const (&s)[kMaxSrc], char* d0, char* d1, uint64_t n,
+                                             float scale) {
+  constexpr int E = 16 / sizeof(T);
+  constexpr int U = (K <= 2) ? 4 : ((K <= 4) ? 2 : FLEXAR_UNROLL_WIDE);
+  const bool sc = Elem<T>::is_float && scale != 1.0f;
+  const uint64_t nt = blockDim.x, nv = n / E, step = (uint64_t)U * nt;
+  for (uint64_t base = (uint64_t)blockIdx.x * step; base < nv; base += (uint64_t)gridDim.x * step) {
+    uint4 x[U][K];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t v = base + u * nt + threadIdx.x;
+#pragma unroll
+      for (int k = 0; k < K; ++k) x[u][k] = v < nv ? ld16(s[k] + v * 16) : uint4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t v = base + u * nt + threadIdx.x;
+      if (v >= nv) continue;
+      const uint4 y = combine16<T, OP, K>(x[u], scale, sc);
+      st16(d0 + v * 16, y);
+      if (d1) st16(d1 + v * 16, y);
+    }
+  }
+  // the last < E elements, by workgroup 0
+  if (blockIdx.x == 0)
+    for (uint64_t i = nv * E + threadIdx.x; i < n; i += nt) {
+      typename Elem<T>::acc acc = Elem<T>::load(ld_elem<PM_FENCE, T>(s[0], i));
+#pragma unroll
+      for (int k = 1; k < K; ++k) acc = OP::apply(acc, Elem<T>::load(ld_elem<PM_FENCE, T>(s[k], i)));
+      if (sc) acc = (typename Elem<T>::acc)(acc * (typename Elem<T>::acc)scale);
+      const T y = Elem<T>::store(acc);
+      st_elem<PM_FENCE, T>(d0, i, y);
+      if (d1) st_elem<PM_FENCE, T>(d1, i, y);
+    }
+}
+
 // PM_WT (copy-engine allreduce): sources written by peers' DMA are read system-coherently and the
 // result is written through, so a stream-ordered flag write after this kernel publishes it.
+// vec bit 0: 16-B vector accesses allowed; bit 1 (fence protocol only): the grid-interleaved form.
 template <typename T, typename OP, int PM>
 __global__ void __launch_bounds__(kExecThreads) reduce_kernel(SrcTable srcs, int nsrc, char* dst, char* dst2,
                                                               uint64_t n, float scale, int vec) {
+  if constexpr (PM != PM_WT && sizeof(T) < 16) {
+    if ((vec & 3) == 3) {
+      const char* s[kMaxSrc];
+#pragma unroll
+      for (int k = 0; k < kMaxSrc; ++k) s[k] = k < nsrc ? srcs.p[k] : nullptr;
+      switch (nsrc) {
+        case 1: reduce_interleaved<T, OP, 1>(s, dst, dst2, n, scale); break;
+        case 2: reduce_interleaved<T, OP, 2>(s, dst, dst2, n, scale); break;
+        case 3: reduce_interleaved<T, OP, 3>(s, dst, dst2, n, scale); break;
+        case 4: reduce_interleaved<T, OP, 4>(s, dst, dst2, n, scale); break;
+        case 5: reduce_interleaved<T, OP, 5>(s, dst, dst2, n, scale); break;
+        case 6: reduce_interleaved<T, OP, 6>(s, dst, dst2, n, scale); break;
+        case 7: reduce_interleaved<T, OP, 7>(s, dst, dst2, n, scale); break;
+        default: reduce_interleaved<T, OP, 8>(s, dst, dst2, n, scale); break;
+      }
+      return;
+    }
+  }
+  vec &= 1;
   const uint32_t quantum = sizeof(T) >= 16 ? 1u : (uint32_t)(16 / sizeof(T));
   uint64_t lo, hi;
   slice_range(n, blockIdx.x, gridDim.x, quantum, &lo, &hi);
