@@ -248,8 +248,12 @@ __device__ FX_INLINE void xfer_k(const char* const (&s)[kMaxSrc], char* const (&
                                  float scale, bool vec) {
   using A = typename Elem<T>::acc;
   constexpr int E = 16 / sizeof(T);
+// Groups in flight per lane for fan-in 5-8 transfers: 2 since round 5 (16 loads of 16 B per lane at fan-in 8).
+// Standalone reduction at fan-in 8 +1-3 % (profiles/r5_reduce/grid_unroll), executor schedules at 2-8 ranks in
+// one launch unchanged within noise (profiles/r5_reduce/executor_unroll), no occupancy change (fence executor
+// 145 -> 164 VGPRs, still 3 waves per SIMD); more remote loads in flight on the 8-GPU node's xGMI latency.
 #ifndef FLEXAR_UNROLL_WIDE
-#define FLEXAR_UNROLL_WIDE 1
+#define FLEXAR_UNROLL_WIDE 2
 #endif
   constexpr int U = (K <= 2) ? 4 : ((K <= 4) ? 2 : FLEXAR_UNROLL_WIDE);  // 16-B loads in flight per lane
   constexpr bool WT = PM == PM_WT;
