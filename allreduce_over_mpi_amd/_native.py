@@ -59,6 +59,7 @@ def _sig(lib):
         "flexar_comm_size": (i, [vp]),
         "flexar_comm_set_algo": (i, [vp, cp]),
         "flexar_comm_set_grid": (i, [vp, i, i]),
+        "flexar_comm_set_xfer_chunk": (i, [vp, u64]),
         "flexar_comm_set_tune_table": (i, [vp, cp]),
         "flexar_allreduce": (i, [vp, vp, vp, sz, i, i, vp]),
         "flexar_allreduce_ex": (i, [vp, vp, vp, sz, i, i, vp, cp, f]),

@@ -456,6 +456,10 @@ class Communicator:
     def set_grid(self, grid: int):
         nv.check(self._lib.flexar_comm_set_grid(self._h, int(grid), 0), "set_grid")
 
+    def set_xfer_chunk(self, elems: int):
+        """Executor work split of large spans (every rank the same): see LocalGroup.set_xfer_chunk."""
+        nv.check(self._lib.flexar_comm_set_xfer_chunk(self._h, int(elems)), "set_xfer_chunk")
+
     def set_tune_table(self, text: str):
         """Install a measured "nranks bytes spec" table (FLEXAR_TUNE_FILE format); "" = cost model."""
         nv.check(self._lib.flexar_comm_set_tune_table(self._h, text.encode()), "set_tune_table")
@@ -848,6 +852,12 @@ class LocalGroup:
     def set_grid(self, grid: int):
         for r in range(self.nranks):
             nv.check(self._lib.flexar_comm_set_grid(self._comms[r], int(grid), 0), "set_grid")
+
+    def set_xfer_chunk(self, elems: int):
+        """Executor work split of large spans: 0 = per-workgroup slices, else round-robin chunks of ``elems``
+        elements (a multiple of 8192; device_exec.hpp DevCtx::ichunk)."""
+        for r in range(self.nranks):
+            nv.check(self._lib.flexar_comm_set_xfer_chunk(self._comms[r], int(elems)), "set_xfer_chunk")
 
     def describe(self, count: int, dtype, rank: int = 0) -> str:
         b = ctypes.create_string_buffer(512)

@@ -119,6 +119,9 @@ int flexar_comm_size(flexar_comm_t comm);
  */
 int flexar_comm_set_algo(flexar_comm_t comm, const char* spec);
 int flexar_comm_set_grid(flexar_comm_t comm, int grid_blocks, int block_threads); /* 0 = auto */
+/* Executor work split of large spans: 0 = one contiguous slice per workgroup (default), else chunks of `elems`
+ * elements (a multiple of 8192) dealt round-robin to the workgroups. Every rank must set the same. */
+int flexar_comm_set_xfer_chunk(flexar_comm_t comm, uint64_t elems);
 /* Replace the communicator's measured tune table ("nranks bytes spec" lines, FLEXAR_TUNE_FILE format;
  * a row covers sizes >= bytes). NULL or "" clears it (back to the cost model). */
 int flexar_comm_set_tune_table(flexar_comm_t comm, const char* text);

@@ -215,7 +215,7 @@ inline const char* const* fingerprint_vars() {
   static const char* v[] = {"FLEXAR_ALGO",     "FT_TOPO",          "FLEXAR_CHUNK_BYTES", "FLEXAR_NCHANNELS",
                             "FLEXAR_MAX_GRID", "FLEXAR_MIN_BLOCK_BYTES", "FLEXAR_MODEL",
                             "FLEXAR_SELFTEST", "FLEXAR_ZC_AUTO", "FLEXAR_PARTIALS", "FLEXAR_CALIB",
-                            nullptr};
+                            "FLEXAR_EXEC_INTERLEAVE", nullptr};
   return v;
 }
 // FLEXAR_CALIB as the mode it selects: unset and "1" behave the same, "off" is "0", "2" is "force".

@@ -282,6 +282,7 @@ void fill_ctx(flexar_comm* c, DevProgram* dp, const void* in, void* out, DevCtx*
   x->stg_half_bytes = c->half_bytes;
   x->err = c->err_dev;
   x->progress = reinterpret_cast<uint64_t*>(c->err_dev) + 1;
+  x->ichunk = c->xfer_chunk;  // 0 = slices (FLEXAR_EXEC_INTERLEAVE, flexar_comm_set_xfer_chunk)
   x->timeout_ticks = c->timeout_ticks;
   x->vec_ok = vec_ok_for(((uintptr_t)in) | ((uintptr_t)out));
   x->fi_kind = c->fi_kind;

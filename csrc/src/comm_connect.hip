@@ -120,6 +120,7 @@ void init_defaults(flexar_comm* c) {
   c->have_tune = c->tune.load(getenv("FLEXAR_TUNE_FILE"));
   c->timeout_ticks = env_u64("FLEXAR_TIMEOUT_MS", 20000) * 100000ull;  // 100 MHz s_memrealtime
   c->zc_auto = env_u64("FLEXAR_ZC_AUTO", 1) != 0;
+  c->xfer_chunk = env_u64("FLEXAR_EXEC_INTERLEAVE", 0) ? kXferChunk : 0;
   c->max_grid = (int)env_u64("FLEXAR_MAX_GRID", 256);
   if (c->max_grid < 1) c->max_grid = 1;
   if (c->max_grid > (int)kMaxGridBlocks) c->max_grid = kMaxGridBlocks;
@@ -889,6 +890,20 @@ int flexar_comm_set_algo(flexar_comm_t c, const char* spec) {
   if (!parse_algo(spec ? spec : "auto", c->nranks, &s, &err)) { set_error(err); return FLEXAR_ERR_INVALID; }
   std::lock_guard<std::mutex> lk(c->mu);
   c->spec = s;
+  c->memo_gen++;
+  return 0;
+}
+
+// XFER work split: 0 = per-workgroup slices, else elements per round-robin chunk (a positive multiple of
+// kXferChunk). Every rank of a communicator must set the same (like the grid).
+int flexar_comm_set_xfer_chunk(flexar_comm_t c, uint64_t elems) {
+  if (!c) return FLEXAR_ERR_INVALID;
+  if (elems % kXferChunk) {
+    set_error("xfer chunk: 0 or a multiple of " + std::to_string(kXferChunk) + " elements");
+    return FLEXAR_ERR_INVALID;
+  }
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->xfer_chunk = elems;
   c->memo_gen++;
   return 0;
 }

@@ -185,6 +185,9 @@ struct flexar_comm {
   bool group_member = false;  // in-process group: peers' pointers are direct device pointers
   AlgoSpec spec;              // communicator default
   int grid_override = 0;
+  // XFER work split (DevCtx::ichunk): 0 = per-workgroup slices; else elements per round-robin chunk (a multiple
+  // of kXferChunk). FLEXAR_EXEC_INTERLEAVE=1 (in the settings fingerprint) or flexar_comm_set_xfer_chunk
+  uint64_t xfer_chunk = 0;
   int max_grid = 256;
   uint64_t min_block_bytes = 32 * 1024;
   uint64_t chunk_bytes = 0;  // FLEXAR_CHUNK_BYTES: cap on the bytes of one launch (0 = workspace-bound only)

@@ -61,7 +61,13 @@ struct DevCtx {
   // fault attribution (crumbs.hpp): host-mapped {started, finished} epoch words of this communicator;
   // workgroup 0 stores the epoch it starts and finishes (one system-scope store each; null = not recorded)
   uint64_t* progress;
+  // XFER work split (exec_body): 0 = every workgroup takes one contiguous slice of each span; otherwise spans of
+  // at least 4 x grid x ichunk elements go in ichunk-element chunks dealt round-robin to the workgroups (the
+  // whole grid then works in one narrow window of every operand, as reduce_interleaved); ichunk is a multiple
+  // of every slicing quantum and typed super-group (kXferChunk)
+  uint64_t ichunk;
 };
+constexpr uint64_t kXferChunk = 8192;  // elements: 32 KiB of fp32; a multiple of 512 x G for every typed layout
 constexpr uint32_t kAmaxParts = 256;    // == FLEXAR_AMAX_PARTIALS
 constexpr uint64_t kAmaxRegion = 256;   // bytes reserved per parity half for the amax granules
 
@@ -351,10 +357,7 @@ __device__ FX_INLINE char* io_base(const DevCtx& c, const Loc& l) {
 }
 
 template <typename T, typename OP, int PM>
-__device__ FX_INLINE void xfer_op(const DevCtx& c, const Op* o, uint32_t lb, uint32_t nb, uint32_t quantum,
-                                  uint64_t par) {
-  uint64_t lo, hi;
-  slice_range(o->len, lb, nb, quantum, &lo, &hi);
+__device__ FX_INLINE void xfer_op_range(const DevCtx& c, const Op* o, uint64_t lo, uint64_t hi, uint64_t par) {
   if (hi <= lo) return;
   const int ns = o->nsrc, nd = o->ndst;
   const char* s[kMaxSrc];
@@ -1270,10 +1273,8 @@ __device__ FX_INLINE bool xfer_mxb_k(int sp, const char* const (&s)[kMaxSrc], co
 // raise the whole kernel's register allocation - 256 VGPRs and scratch spills - which cost the 4-rank MX
 // executor 25 % (profiles/r4_mx/README.md); programs with fan-in <= 4 launch the narrow instantiation).
 template <typename T, typename W, int PM, int KMAX = kMaxSrc>
-__device__ FX_INLINE void xfer_op_typed(const DevCtx& c, const Op* o, uint32_t lb, uint32_t nb, uint32_t quantum,
-                                        uint64_t par, float pre, float post_inv) {
-  uint64_t lo, hi;
-  slice_range(o->len, lb, nb, quantum, &lo, &hi);
+__device__ FX_INLINE void xfer_op_typed_range(const DevCtx& c, const Op* o, uint64_t lo, uint64_t hi, uint64_t par,
+                                              float pre, float post_inv) {
   if (hi <= lo) return;
   constexpr bool FP8 = sizeof(W) == 1;
   const int ns = o->nsrc, nd = o->ndst;
@@ -1453,8 +1454,21 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
       bool bar = false;
       for (uint32_t k = 0; k < n; ++k) {
         const Op* q = c.ops + i + (n > 1 ? (k + lb) % n : 0);
-        if constexpr (TYPED) xfer_op_typed<T, WT_, PM, KMAX>(c, q, lb, nb, quantum, par, pre, post_inv);
-        else xfer_op<T, OP, PM>(c, q, lb, nb, quantum, par);
+        // the work split is a function of (len, grid) only, so the workgroup b of every rank that hands a span
+        // on and the one that takes it over cover the same elements
+        auto range = [&](uint64_t lo, uint64_t hi) {
+          if constexpr (TYPED) xfer_op_typed_range<T, WT_, PM, KMAX>(c, q, lo, hi, par, pre, post_inv);
+          else xfer_op_range<T, OP, PM>(c, q, lo, hi, par);
+        };
+        const uint64_t len = q->len;
+        if (c.ichunk && len >= 4ull * nb * c.ichunk) {
+          for (uint64_t lo = (uint64_t)lb * c.ichunk; lo < len; lo += (uint64_t)nb * c.ichunk)
+            range(lo, lo + c.ichunk < len ? lo + c.ichunk : len);
+        } else {
+          uint64_t lo, hi;
+          slice_range(len, lb, nb, quantum, &lo, &hi);
+          range(lo, hi);
+        }
         bar |= (q->flags & kXferBarrierAfter) != 0;
       }
       if (bar) __syncthreads();

@@ -601,3 +601,45 @@ def test_group_misaligned_views(cuda, groups, dtype, offsets):
                 for b in obufs:
                     assert not b[:oo].any() and not b[oo + size:].any(), (spec, size, oi, oo)
     grp.check()
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_group_chunked_work_split_exact(cuda, n):
+    """The executor's round-robin chunk split of large spans (set_xfer_chunk / FLEXAR_EXEC_INTERLEAVE,
+    device_exec.hpp DevCtx::ichunk): with a small grid every span of these buffers is chunked, a tail chunk is
+    partial, and every schedule family - staging, push / pull, rings, trees, write-through, typed partials, the
+    fp8 and MX wires - must give exactly what the slice split gives (same arithmetic per element)."""
+    from allreduce_over_mpi_amd.parallel import LocalGroup
+
+    grp = LocalGroup(n, workspace_bytes=256 << 20)
+    try:
+        size = 5 * 8192 * 16 * n + 12345  # spans of > 4 x grid x chunk elements, and a partial last chunk
+        g = torch.Generator(device=cuda).manual_seed(17 + n)
+        xs = [torch.randn(size, device=cuda, generator=g) for _ in range(n)]
+        xb = [x.to(torch.bfloat16) for x in xs]
+        specs = ["flat+pull", "flat+push", "ring", "flat+pull+wt", "flat+pull+mxe4m3"] + (["rhd+pull", "tree:2,4+push"]
+                                                                                         if n == 8 else [])
+        for spec in specs:
+            for data in (xs, xb):
+                outs = {}
+                for chunk in (0, 8192):
+                    grp.set_grid(16)
+                    grp.set_xfer_chunk(chunk)
+                    for _ in range(2):  # both staging parities
+                        outs[chunk] = grp.all_reduce([x.clone() for x in data], "sum", algo=spec)
+                    torch.cuda.synchronize()
+                for r in range(n):
+                    assert torch.equal(outs[0][r], outs[8192][r]), (spec, data[0].dtype, r)
+        # the global-scale fp8 wire (amax pass + one launch)
+        outs = {}
+        for chunk in (0, 8192):
+            grp.set_xfer_chunk(chunk)
+            outs[chunk] = grp.all_reduce_fp8([x.clone() for x in xs], op="avg")
+            torch.cuda.synchronize()
+        for r in range(n):
+            assert torch.equal(outs[0][r], outs[8192][r]), ("fp8", r)
+        grp.set_xfer_chunk(0)
+        grp.set_grid(0)
+        grp.check()
+    finally:
+        grp.close()
