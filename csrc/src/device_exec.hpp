@@ -632,6 +632,12 @@ enum : int { SP_T = 0, SP_TW = 1, SP_W = 2 };
 #define FLEXAR_TYPED_UU2_MAXV 4
 #endif
 constexpr int typed_uu(int v) { return v <= FLEXAR_TYPED_UU4_MAXV ? 4 : (v <= FLEXAR_TYPED_UU2_MAXV ? 2 : 1); }
+// Software pipelining of the typed lane-interleaved loop (xfer_mx): on when a batch holds at most
+// FLEXAR_TYPED_PIPE_MAXV 16-B vectors per lane (two batches are live; 0 = off). Build-time A/B knob.
+#ifndef FLEXAR_TYPED_PIPE_MAXV
+#define FLEXAR_TYPED_PIPE_MAXV 0
+#endif
+constexpr bool typed_pipe(int v) { return v <= FLEXAR_TYPED_PIPE_MAXV; }
 
 template <typename T, typename W, int K, int SP, int PM>
 __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (&d)[kMaxDst], int nd, uint32_t dm,
@@ -764,22 +770,17 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
     // `lim` elements from super-group sg: UI * span, or fewer for the last, partial super-group, whose lanes
     // past `lim` load zeros and drop their stores (the buffer descriptors' range check; lim is a multiple of
     // G, so every sub-chunk access is wholly inside or outside)
-    auto iter = [&](auto ucnt, uint64_t lim) {
+    // descriptors over UI super-groups from sg0 (<= UI * 16 KiB * 4 B: 32-bit offsets); the loads and the
+    // compute + stores are separate halves, so the pipelined loop below can issue one batch's loads before
+    // the previous batch's stores
+    auto load_it = [&](auto ucnt, uint64_t sg0, uint64_t lim, uint4 (&raw)[decltype(ucnt)::value][K][VM]) {
       constexpr int UI = decltype(ucnt)::value;
-      // descriptors over this iteration's UI super-groups (<= UI * 16 KiB * 4 B: 32-bit offsets)
-      __amdgpu_buffer_rsrc_t bs[K], bd[kMaxDst];
+      __amdgpu_buffer_rsrc_t bs[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const uint64_t es = isw(k) ? sizeof(W) : sizeof(T);
-        bs[k] = rsrc_of(s[k] + sg * span * es, lim * es);
+        bs[k] = rsrc_of(s[k] + sg0 * span * es, lim * es);
       }
-#pragma unroll
-      for (int dd = 0; dd < kMaxDst; ++dd) {
-        if (dd >= nd) continue;
-        const uint64_t es = (dm >> dd) & 1 ? sizeof(W) : sizeof(T);
-        bd[dd] = rsrc_of(d[dd] + sg * span * es, lim * es);
-      }
-      uint4 raw[UI][K][VM];
 #pragma unroll
       for (int u = 0; u < UI; ++u)
 #pragma unroll
@@ -790,6 +791,16 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
             if (isw(k)) ld_sub<SBW>(raw[u][k], j, bs[k], lw, e0 * (uint32_t)sizeof(W));
             else ld_sub<SBT>(raw[u][k], j, bs[k], lt, e0 * (uint32_t)sizeof(T));
           }
+    };
+    auto finish_it = [&](auto ucnt, uint64_t sg0, uint64_t lim, const uint4 (&raw)[decltype(ucnt)::value][K][VM]) {
+      constexpr int UI = decltype(ucnt)::value;
+      __amdgpu_buffer_rsrc_t bd[kMaxDst];
+#pragma unroll
+      for (int dd = 0; dd < kMaxDst; ++dd) {
+        if (dd >= nd) continue;
+        const uint64_t es = (dm >> dd) & 1 ? sizeof(W) : sizeof(T);
+        bd[dd] = rsrc_of(d[dd] + sg0 * span * es, lim * es);
+      }
 #pragma unroll
       for (int u = 0; u < UI; ++u) {
         float acc[G];
@@ -809,7 +820,37 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
         }
       }
     };
-    for (; sg + UU <= nsg; sg += UU) iter(std::integral_constant<int, UU>{}, (uint64_t)UU * span);
+    auto iter = [&](auto ucnt, uint64_t lim) {
+      uint4 raw[decltype(ucnt)::value][K][VM];
+      load_it(ucnt, sg, lim, raw);
+      finish_it(ucnt, sg, lim, raw);
+    };
+    using UUc = std::integral_constant<int, UU>;
+    if constexpr (typed_pipe(UU * K * VM)) {
+      // two batches in flight: batch i+1's loads are issued before batch i's converts and stores. On gfx9
+      // one counter (vmcnt) tracks loads and stores in issue order, so in the plain loop each batch's loads
+      // also wait out the previous batch's store acknowledgements; here they are older than those stores.
+      const uint64_t nmain = nsg - nsg % UU;
+      if (nmain) {
+        uint4 ra[UU][K][VM], rb[UU][K][VM];
+        const uint64_t lim = (uint64_t)UU * span;
+        load_it(UUc{}, 0, lim, ra);
+        for (;;) {
+          const bool more = sg + UU < nmain;
+          if (more) load_it(UUc{}, sg + UU, lim, rb);
+          finish_it(UUc{}, sg, lim, ra);
+          sg += UU;
+          if (!more) break;
+          const bool more2 = sg + UU < nmain;
+          if (more2) load_it(UUc{}, sg + UU, lim, ra);
+          finish_it(UUc{}, sg, lim, rb);
+          sg += UU;
+          if (!more2) break;
+        }
+      }
+    } else {
+      for (; sg + UU <= nsg; sg += UU) iter(UUc{}, (uint64_t)UU * span);
+    }
     if constexpr (UU > 1)
       for (; sg < nsg; ++sg) iter(std::integral_constant<int, 1>{}, span);
     if (sg * span < ng * G) iter(std::integral_constant<int, 1>{}, ng * G - sg * span);
@@ -1106,16 +1147,22 @@ __device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_
     const uint64_t nsg = vec ? n / span : 0;
     constexpr int SBT = SE * (int)sizeof(T), SBW = SE;
     const uint32_t lt = threadIdx.x * SBT, lw = threadIdx.x * SBW;
-    const uint32_t lb = threadIdx.x / LPB;  // the lane's block within a run's row of nt * SE elements
-    const bool lead = (threadIdx.x % LPB) == 0;
+    // Scale bytes, one per block: a wave's VM runs touch 32 of them per operand (BPW consecutive blocks per
+    // run, the runs nt * SE / 32 bytes apart). Lane l < 32 moves byte (run l / BPW, block l % BPW) with one
+    // 1-B access per operand and wave, and a lane takes run j's byte from lane j * BPW + (its block) by a
+    // cross-lane read - instead of VM 1-B accesses per lane and operand, each held in a register of its own
+    // (at fan-in 8 on fp32, 28 registers: the kernel spilled).
+    constexpr int BPW = 64 / LPB;
+    static_assert(BPW * VM == 32, "a wave's runs cover 32 blocks");
+    const uint32_t wl = threadIdx.x & 63;
+    const uint32_t mj = (wl & 31) / BPW, mb = (wl & 31) % BPW;  // the byte this lane moves: run mj, block mb
+    const uint32_t svo = (threadIdx.x >> 6) * BPW + mb + mj * (uint32_t)(nt * SE / kMxBlock);
+    const uint32_t lbw = wl / LPB;  // the lane's block within its wave's row of a run
     // the scale shadows cover the whole blocks only: the last partial block is the scalar tail's (mx_elem),
     // so a lane of the partial super-group never writes its scale
     const uint64_t nfull = n / kMxBlock;
-    __amdgpu_buffer_rsrc_t rss[K], rsd[kMaxDst];
-#pragma unroll
-    for (int k = 0; k < K; ++k) rss[k] = rsrc_of(isw(k) ? (const char*)ss[k] : nullptr, isw(k) ? nfull : 0);
-#pragma unroll
-    for (int dd = 0; dd < kMaxDst; ++dd) rsd[dd] = rsrc_of((const char*)sd[dd], sd[dd] ? nfull : 0);
+    // the scale descriptors are built where they are used, like the payload's: K + kMaxDst of them held over
+    // the loop (4 scalar registers each) overflowed the scalar file at fan-in 8 and spilled
     uint64_t sg = 0;
     // one iteration over UI super-groups; full super-groups beyond the last multiple of UU take the same
     // lane-interleaved layout one at a time (a slice of a few super-groups - DDP buckets, small pieces -
@@ -1135,30 +1182,43 @@ __device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_
         const uint64_t es = (dm >> dd) & 1 ? 1 : sizeof(T);
         bd[dd] = rsrc_of(d[dd] + sg * span * es, lim * es);
       }
-      // block of (u, j) = sboff(u, j) (uniform) + lb (per lane)
-      auto sboff = [&](int u, int j) -> uint32_t { return (uint32_t)(((sg + u) * span + j * nt * SE) / kMxBlock); };
+      // super-group u's first scale byte (uniform); a lane's byte of run j sits nt * SE / 32 * j + its block further
+      auto sboff = [&](int u) -> uint32_t { return (uint32_t)((sg + u) * span / kMxBlock); };
       uint4 raw[UI][K][VM];
-      uint32_t sb[UI][K][VM];
+      uint32_t sbw[UI][K];
 #pragma unroll
       for (int u = 0; u < UI; ++u)
 #pragma unroll
-        for (int k = 0; k < K; ++k)
+        for (int k = 0; k < K; ++k) {
 #pragma unroll
           for (int j = 0; j < VM; ++j) {
             const uint32_t e0 = (uint32_t)(u * span + j * nt * SE);  // uniform
-            if (isw(k)) {
-              ld_sub<SBW>(raw[u][k], j, bs[k], lw, e0);
-              sb[u][k][j] = __builtin_amdgcn_raw_buffer_load_b8(rss[k], lb, sboff(u, j), kAuxLd);
-            } else {
-              ld_sub<SBT>(raw[u][k], j, bs[k], lt, e0 * (uint32_t)sizeof(T));
-              sb[u][k][j] = 0;
-            }
+            if (isw(k)) ld_sub<SBW>(raw[u][k], j, bs[k], lw, e0);
+            else ld_sub<SBT>(raw[u][k], j, bs[k], lt, e0 * (uint32_t)sizeof(T));
           }
+          sbw[u][k] = isw(k) ? __builtin_amdgcn_raw_buffer_load_b8(rsrc_of((const char*)ss[k], nfull), svo, sboff(u), kAuxLd)
+                             : 0u;
+        }
 #pragma unroll
       for (int u = 0; u < UI; ++u) {
+        uint32_t sb[K][VM];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+          for (int j = 0; j < VM; ++j) sb[k][j] = isw(k) ? (uint32_t)__shfl((int)sbw[u][k], j * BPW + lbw, 64) : 0u;
         uint4 yq, yt[VM];
         uint32_t xb[VM];
-        mx_group<T, W, K, SP, RL>(raw[u], sb[u], scale, nd, dm, yq, xb, yt);
+        mx_group<T, W, K, SP, RL>(raw[u], sb, scale, nd, dm, yq, xb, yt);
+        // the wire destinations' scale bytes, gathered the same way: lane l < 32 stores run mj's byte of block
+        // mb, computed by that block's first lane
+        uint32_t xs = 0;
+        if (dm) {
+#pragma unroll
+          for (int j = 0; j < VM; ++j) {
+            const uint32_t t = (uint32_t)__shfl((int)xb[j], (int)(mb * LPB), 64);
+            xs = mj == (uint32_t)j ? t : xs;
+          }
+        }
 #pragma unroll
         for (int dd = 0; dd < kMaxDst; ++dd) {
           if (dd >= nd) continue;
@@ -1169,11 +1229,12 @@ __device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_
             if (wide) {
               const uint4 q1[1] = {yq};
               st_sub<SBW, NTS>(bd[dd], lw, e0, q1, j);
-              if (lead) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)xb[j], rsd[dd], lb, sboff(u, j), NTS ? 2 : 0);
             } else {
               st_sub<SBT, NTS>(bd[dd], lt, e0 * (uint32_t)sizeof(T), yt, j);
             }
           }
+          if (wide && wl < 32)
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)xs, rsrc_of((const char*)sd[dd], nfull), svo, sboff(u), NTS ? 2 : 0);
         }
       }
     };
@@ -1456,19 +1517,26 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
         const Op* q = c.ops + i + (n > 1 ? (k + lb) % n : 0);
         // the work split is a function of (len, grid) only, so the workgroup b of every rank that hands a span
         // on and the one that takes it over cover the same elements
-        auto range = [&](uint64_t lo, uint64_t hi) {
+        // one call site for both splits (slices: one pass over [lo, end); chunks: every nb-th chunk): with two,
+        // the compiler outlined the whole transfer into a called function (stack frame, captured state through
+        // flat pointers) and the slices ran up to 5 % slower
+        const uint64_t len = q->len;
+        uint64_t lo, end, step, chunk;
+        if (c.ichunk && len >= 4ull * nb * c.ichunk) {
+          lo = (uint64_t)lb * c.ichunk;
+          end = len;
+          chunk = c.ichunk;
+          step = (uint64_t)nb * c.ichunk;
+        } else {
+          slice_range(len, lb, nb, quantum, &lo, &end);
+          chunk = step = end - lo;  // a single pass (also when empty)
+        }
+        do {
+          const uint64_t hi = lo + chunk < end ? lo + chunk : end;
           if constexpr (TYPED) xfer_op_typed_range<T, WT_, PM, KMAX>(c, q, lo, hi, par, pre, post_inv);
           else xfer_op_range<T, OP, PM>(c, q, lo, hi, par);
-        };
-        const uint64_t len = q->len;
-        if (c.ichunk && len >= 4ull * nb * c.ichunk) {
-          for (uint64_t lo = (uint64_t)lb * c.ichunk; lo < len; lo += (uint64_t)nb * c.ichunk)
-            range(lo, lo + c.ichunk < len ? lo + c.ichunk : len);
-        } else {
-          uint64_t lo, hi;
-          slice_range(len, lb, nb, quantum, &lo, &hi);
-          range(lo, hi);
-        }
+          lo += step;
+        } while (lo < end);
         bar |= (q->flags & kXferBarrierAfter) != 0;
       }
       if (bar) __syncthreads();
