@@ -1147,22 +1147,16 @@ __device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_
     const uint64_t nsg = vec ? n / span : 0;
     constexpr int SBT = SE * (int)sizeof(T), SBW = SE;
     const uint32_t lt = threadIdx.x * SBT, lw = threadIdx.x * SBW;
-    // Scale bytes, one per block: a wave's VM runs touch 32 of them per operand (BPW consecutive blocks per
-    // run, the runs nt * SE / 32 bytes apart). Lane l < 32 moves byte (run l / BPW, block l % BPW) with one
-    // 1-B access per operand and wave, and a lane takes run j's byte from lane j * BPW + (its block) by a
-    // cross-lane read - instead of VM 1-B accesses per lane and operand, each held in a register of its own
-    // (at fan-in 8 on fp32, 28 registers: the kernel spilled).
-    constexpr int BPW = 64 / LPB;
-    static_assert(BPW * VM == 32, "a wave's runs cover 32 blocks");
-    const uint32_t wl = threadIdx.x & 63;
-    const uint32_t mj = (wl & 31) / BPW, mb = (wl & 31) % BPW;  // the byte this lane moves: run mj, block mb
-    const uint32_t svo = (threadIdx.x >> 6) * BPW + mb + mj * (uint32_t)(nt * SE / kMxBlock);
-    const uint32_t lbw = wl / LPB;  // the lane's block within its wave's row of a run
+    const uint32_t lb = threadIdx.x / LPB;  // the lane's block within a run's row of nt * SE elements
+    const bool lead = (threadIdx.x % LPB) == 0;
     // the scale shadows cover the whole blocks only: the last partial block is the scalar tail's (mx_elem),
     // so a lane of the partial super-group never writes its scale
     const uint64_t nfull = n / kMxBlock;
-    // the scale descriptors are built where they are used, like the payload's: K + kMaxDst of them held over
-    // the loop (4 scalar registers each) overflowed the scalar file at fan-in 8 and spilled
+    __amdgpu_buffer_rsrc_t rss[K], rsd[kMaxDst];
+#pragma unroll
+    for (int k = 0; k < K; ++k) rss[k] = rsrc_of(isw(k) ? (const char*)ss[k] : nullptr, isw(k) ? nfull : 0);
+#pragma unroll
+    for (int dd = 0; dd < kMaxDst; ++dd) rsd[dd] = rsrc_of((const char*)sd[dd], sd[dd] ? nfull : 0);
     uint64_t sg = 0;
     // one iteration over UI super-groups; full super-groups beyond the last multiple of UU take the same
     // lane-interleaved layout one at a time (a slice of a few super-groups - DDP buckets, small pieces -
@@ -1182,43 +1176,30 @@ __device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_
         const uint64_t es = (dm >> dd) & 1 ? 1 : sizeof(T);
         bd[dd] = rsrc_of(d[dd] + sg * span * es, lim * es);
       }
-      // super-group u's first scale byte (uniform); a lane's byte of run j sits nt * SE / 32 * j + its block further
-      auto sboff = [&](int u) -> uint32_t { return (uint32_t)((sg + u) * span / kMxBlock); };
+      // block of (u, j) = sboff(u, j) (uniform) + lb (per lane)
+      auto sboff = [&](int u, int j) -> uint32_t { return (uint32_t)(((sg + u) * span + j * nt * SE) / kMxBlock); };
       uint4 raw[UI][K][VM];
-      uint32_t sbw[UI][K];
+      uint32_t sb[UI][K][VM];
 #pragma unroll
       for (int u = 0; u < UI; ++u)
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
+        for (int k = 0; k < K; ++k)
 #pragma unroll
           for (int j = 0; j < VM; ++j) {
             const uint32_t e0 = (uint32_t)(u * span + j * nt * SE);  // uniform
-            if (isw(k)) ld_sub<SBW>(raw[u][k], j, bs[k], lw, e0);
-            else ld_sub<SBT>(raw[u][k], j, bs[k], lt, e0 * (uint32_t)sizeof(T));
+            if (isw(k)) {
+              ld_sub<SBW>(raw[u][k], j, bs[k], lw, e0);
+              sb[u][k][j] = __builtin_amdgcn_raw_buffer_load_b8(rss[k], lb, sboff(u, j), kAuxLd);
+            } else {
+              ld_sub<SBT>(raw[u][k], j, bs[k], lt, e0 * (uint32_t)sizeof(T));
+              sb[u][k][j] = 0;
+            }
           }
-          sbw[u][k] = isw(k) ? __builtin_amdgcn_raw_buffer_load_b8(rsrc_of((const char*)ss[k], nfull), svo, sboff(u), kAuxLd)
-                             : 0u;
-        }
 #pragma unroll
       for (int u = 0; u < UI; ++u) {
-        uint32_t sb[K][VM];
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-#pragma unroll
-          for (int j = 0; j < VM; ++j) sb[k][j] = isw(k) ? (uint32_t)__shfl((int)sbw[u][k], j * BPW + lbw, 64) : 0u;
         uint4 yq, yt[VM];
         uint32_t xb[VM];
-        mx_group<T, W, K, SP, RL>(raw[u], sb, scale, nd, dm, yq, xb, yt);
-        // the wire destinations' scale bytes, gathered the same way: lane l < 32 stores run mj's byte of block
-        // mb, computed by that block's first lane
-        uint32_t xs = 0;
-        if (dm) {
-#pragma unroll
-          for (int j = 0; j < VM; ++j) {
-            const uint32_t t = (uint32_t)__shfl((int)xb[j], (int)(mb * LPB), 64);
-            xs = mj == (uint32_t)j ? t : xs;
-          }
-        }
+        mx_group<T, W, K, SP, RL>(raw[u], sb[u], scale, nd, dm, yq, xb, yt);
 #pragma unroll
         for (int dd = 0; dd < kMaxDst; ++dd) {
           if (dd >= nd) continue;
@@ -1229,12 +1210,11 @@ __device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_
             if (wide) {
               const uint4 q1[1] = {yq};
               st_sub<SBW, NTS>(bd[dd], lw, e0, q1, j);
+              if (lead) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)xb[j], rsd[dd], lb, sboff(u, j), NTS ? 2 : 0);
             } else {
               st_sub<SBT, NTS>(bd[dd], lt, e0 * (uint32_t)sizeof(T), yt, j);
             }
           }
-          if (wide && wl < 32)
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)xs, rsrc_of((const char*)sd[dd], nfull), svo, sboff(u), NTS ? 2 : 0);
         }
       }
     };
