@@ -1081,7 +1081,8 @@ inline bool typed_pattern_ok(const Program& P, const Op& o) {
   const int K = o.nsrc;
   // MX wire: a wire-to-wire copy would have to carry the block scales too (the flat schedule has none)
   if (P.wire >= 4 && sm == all_s && dm) return false;
-  if (sm == all_s && dm == all_d) return true;  // wire type throughout
+  // wire type throughout: fp32 partials of any fan-in; an fp8 wire only copies (its kernels carry no fp8 sum)
+  if (sm == all_s && dm == all_d) return fp8 ? K == 1 : true;
   if (!fp8 && sm == 0 && dm == 0) return true;  // dtype throughout
   if (sm == 0) return fp8 ? K == 1 : K >= 2;
   if (sm == (all_s & ~1u)) return K >= 2 && (fp8 || K == 2);

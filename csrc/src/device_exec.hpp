@@ -328,18 +328,21 @@ __device__ FX_INLINE void xfer_k(const char* const (&s)[kMaxSrc], char* const (&
   }
 }
 
-template <typename T, typename OP, int PM>
-__device__ FX_INLINE void xfer_dispatch(int K, const char* const (&s)[kMaxSrc], char* const (&d)[kMaxDst], int nd,
+// KM caps the fan-in compiled in. The fp8-wire kernels use the untyped path for wire-to-wire copies only (K 1:
+// typed_pattern_ok admits no other all-wire op for them); compiling K 2-8 in as well had put the bf16 fp8-wire
+// fence kernel at 216 VGPRs (2 waves per SIMD) against 148 without them. Returns false for K > KM.
+template <typename T, typename OP, int PM, int KM = kMaxSrc>
+__device__ FX_INLINE bool xfer_dispatch(int K, const char* const (&s)[kMaxSrc], char* const (&d)[kMaxDst], int nd,
                                         uint64_t n, float scale, bool vec) {
   switch (K) {
-    case 1: xfer_k<T, OP, 1, PM>(s, d, nd, n, scale, vec); break;
-    case 2: xfer_k<T, OP, 2, PM>(s, d, nd, n, scale, vec); break;
-    case 3: xfer_k<T, OP, 3, PM>(s, d, nd, n, scale, vec); break;
-    case 4: xfer_k<T, OP, 4, PM>(s, d, nd, n, scale, vec); break;
-    case 5: xfer_k<T, OP, 5, PM>(s, d, nd, n, scale, vec); break;
-    case 6: xfer_k<T, OP, 6, PM>(s, d, nd, n, scale, vec); break;
-    case 7: xfer_k<T, OP, 7, PM>(s, d, nd, n, scale, vec); break;
-    default: xfer_k<T, OP, 8, PM>(s, d, nd, n, scale, vec); break;
+    case 1: xfer_k<T, OP, 1, PM>(s, d, nd, n, scale, vec); return true;
+    case 2: if constexpr (KM >= 2) { xfer_k<T, OP, 2, PM>(s, d, nd, n, scale, vec); return true; } return false;
+    case 3: if constexpr (KM >= 3) { xfer_k<T, OP, 3, PM>(s, d, nd, n, scale, vec); return true; } return false;
+    case 4: if constexpr (KM >= 4) { xfer_k<T, OP, 4, PM>(s, d, nd, n, scale, vec); return true; } return false;
+    case 5: if constexpr (KM >= 5) { xfer_k<T, OP, 5, PM>(s, d, nd, n, scale, vec); return true; } return false;
+    case 6: if constexpr (KM >= 6) { xfer_k<T, OP, 6, PM>(s, d, nd, n, scale, vec); return true; } return false;
+    case 7: if constexpr (KM >= 7) { xfer_k<T, OP, 7, PM>(s, d, nd, n, scale, vec); return true; } return false;
+    default: if constexpr (KM >= 8) { xfer_k<T, OP, 8, PM>(s, d, nd, n, scale, vec); return true; } return false;
   }
 }
 
@@ -1381,14 +1384,10 @@ __device__ FX_INLINE void xfer_op_typed_range(const DevCtx& c, const Op* o, uint
     (void)post_inv;
   } else {
     if (sm == all_s && dm == all_d) {  // wire type throughout (fp32 partial -> fp32 partial, fp8 copy)
-      xfer_dispatch<W, OpSum, PM>(ns, s, d, nd, n, o->scale, vec);
-      return;
-    }
-    if (!FP8 && sm == 0 && dm == 0) {  // dtype throughout (raw inputs, all-gather copies)
-      xfer_dispatch<T, OpSum, PM>(ns, s, d, nd, n, o->scale, vec);
-      return;
-    }
-    switch (ns) {
+      ok = xfer_dispatch<W, OpSum, PM, FP8 ? 1 : KMAX>(ns, s, d, nd, n, o->scale, vec);
+    } else if (!FP8 && sm == 0 && dm == 0) {  // dtype throughout (raw inputs, all-gather copies)
+      ok = xfer_dispatch<T, OpSum, PM, KMAX>(ns, s, d, nd, n, o->scale, vec);
+    } else switch (ns) {
       case 1: ok = xfer_mx_k<T, W, 1, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
       case 2: ok = xfer_mx_k<T, W, 2, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
       case 3: ok = xfer_mx_k<T, W, 3, PM>(sp, s, d, nd, dm, n, o->scale, pre, post_inv, vec); break;
@@ -1687,12 +1686,24 @@ __global__ void __launch_bounds__(kExecThreads) exec_kernel(DevCtx c) {
 }
 
 // Typed programs (Program::wire: fp32 partials or an fp8 wire), SUM/AVG only.
+// FLEXAR_TYPED_OCC3: the global-scale fp8 kernels of the narrow class (KMAX 4) ask the register allocator for 3
+// waves per SIMD (at most 168 VGPRs). The single-rank kernel fits without it (bf16 167, fp32 155); the in-process
+// group kernel needs 179 / 172 otherwise, and with it keeps a few prologue values in scratch.
+#ifndef FLEXAR_TYPED_OCC3
+#define FLEXAR_TYPED_OCC3 0
+#endif
+template <typename W, int KMAX>
+constexpr int typed_min_waves() {
+  return FLEXAR_TYPED_OCC3 && KMAX <= 4 && sizeof(W) == 1 && !IsMx<W>::value ? 3 : 1;
+}
 template <typename T, typename W, int PM, int KMAX = kMaxSrc>
-__global__ void __launch_bounds__(kExecThreads) exec_mx_kernel(DevCtx c) {
+__global__ void __launch_bounds__(kExecThreads) __attribute__((amdgpu_waves_per_eu(typed_min_waves<W, KMAX>())))
+exec_mx_kernel(DevCtx c) {
   exec_body<T, OpSum, PM, W, KMAX>(c, blockIdx.x, gridDim.x);
 }
 template <typename T, typename W, int PM, int KMAX = kMaxSrc>
-__global__ void __launch_bounds__(kExecThreads) exec_mx_group_kernel(const DevCtx* ctxs, uint32_t grid_per_rank) {
+__global__ void __launch_bounds__(kExecThreads) __attribute__((amdgpu_waves_per_eu(typed_min_waves<W, KMAX>())))
+exec_mx_group_kernel(const DevCtx* ctxs, uint32_t grid_per_rank) {
   const uint32_t r = blockIdx.x / grid_per_rank;
   exec_body<T, OpSum, PM, W, KMAX>(ctxs[r], blockIdx.x % grid_per_rank, grid_per_rank);
 }

@@ -138,3 +138,26 @@ def test_typed_program_dump_marks_wire_operands():
     assert "wire type fp32" in d and "STG~" in d
     d = nv.plan_dump("flat+pull+e4m3", 1, 4, 4096, "float32")
     assert "wire type e4m3" in d and "unit 1 B" in d
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 8])
+@pytest.mark.parametrize("spec", ["flat+pull+e4m3", "flat+push+e4m3", "flat+pull+e5m2", "flat+pull+mxe4m3",
+                                  "flat+push+mxe4m3"])
+def test_fp8_wire_programs_sum_no_wire_only_operands(n, spec):
+    """The fp8 / MX wire kernels carry the untyped path for wire-to-wire copies only (device_exec.hpp
+    xfer_dispatch KM; planner.hpp typed_pattern_ok admits no other all-wire op for an fp8 wire): every planned
+    fp8 program sums with the rank's own dtype value in the mix, and its widest fan-in is N (the kernel class)."""
+    import re
+
+    for rank in sorted({0, n - 1}):
+        d = nv.plan_dump(spec, rank, n, 1 << 16, "bfloat16")
+        widest = 0
+        for line in d.splitlines():
+            m = re.match(r"\s+XFER len=\d+ \[(.*)\] -> \[(.*)\]", line)
+            if not m:
+                continue
+            srcs, dsts = m.group(1).split(" + "), m.group(2).split(", ")
+            widest = max(widest, len(srcs))
+            if len(srcs) >= 2:
+                assert not all("~" in x for x in srcs + dsts), (spec, n, rank, line)
+        assert widest == n, (spec, n, rank, widest)
