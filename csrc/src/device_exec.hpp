@@ -217,9 +217,55 @@ __device__ FX_INLINE void st_elem(char* base, uint64_t i, T t) {
   }
 }
 
-template <typename T, typename OP, int K>
+template <typename S> struct IsFp8;
+template <typename S> __device__ FX_INLINE void fp8_word_decode(uint32_t w, float* x);
+template <typename S> __device__ FX_INLINE uint32_t fp8_word_encode(const float* x);
+
+// 4 fp8 values from fp32 with the element store's semantics (f32_to_e4m3 / _e5m2: NaN -> 0x7f, saturate to the
+// largest finite, RNE) at the packed converter's rate: clamp, pack with 2 converts, then put 0x7f in the bytes
+// whose input was a NaN (the clamp maps a NaN to a bound). Branch-free.
+template <typename T>
+__device__ FX_INLINE uint32_t fp8_store4(const float (&a)[4]) {
+  constexpr float M = IsFp8<T>::e4m3 ? 448.0f : 57344.0f;
+  float c[4];
+  uint32_t nan = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    c[j] = __builtin_fminf(__builtin_fmaxf(a[j], -M), M);
+    nan |= a[j] != a[j] ? 0xffu << (8 * j) : 0u;
+  }
+  return (fp8_word_encode<T>(c) & ~nan) | (0x7f7f7f7fu & nan);
+}
+
+// PACK = false keeps fp8 on the per-element converts: the write-through kernels (PM_WT) hold their register
+// budget with them (the packed form would take the copy-engine reduction from 2 workgroups per CU to 1).
+template <typename T, typename OP, int K, bool PACK = true>
 __device__ FX_INLINE uint4 combine16(const uint4 (&x)[K], float scale, bool sc) {
   if (K == 1 && !sc) return x[0];  // pure move: no decode/encode round trip (fp8/bf16 copies at HBM rate)
+  if constexpr (IsFp8<T>::value && PACK) {
+    // fp8, one 4-byte word at a time (few live registers): packed decode (2 converts per 4 elements instead of
+    // 4), fp32 accumulate in source order, post-scale, packed saturating encode (fp8_store4). Bit-identical to
+    // the per-element path below.
+    const float f = sc ? scale : 1.0f;
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float acc[4], t[4];
+      fp8_word_decode<T>((&x[0].x)[i], acc);
+#pragma unroll
+      for (int k = 1; k < K; ++k) {
+        fp8_word_decode<T>((&x[k].x)[i], t);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = OP::apply(acc[j], t[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = acc[j] * f;
+      w[i] = fp8_store4<T>(acc);
+    }
+    uint4 r;
+    __builtin_memcpy(&r, w, 16);
+    return r;
+  }
   using A = typename Elem<T>::acc;
   constexpr int E = 16 / sizeof(T);
   T v[E];
@@ -293,7 +339,7 @@ __device__ FX_INLINE void xfer_k(const char* const (&s)[kMaxSrc], char* const (&
       for (int k = 0; k < K; ++k) x[u][k] = ld(k, v + u * nt);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      uint4 y = combine16<T, OP, K>(x[u], scale, sc);
+      uint4 y = combine16<T, OP, K, PM != PM_WT>(x[u], scale, sc);
 #pragma unroll
       for (int dd = 0; dd < kMaxDst; ++dd)
         if (dd < nd) st(dd, v + u * nt, y);
@@ -303,7 +349,7 @@ __device__ FX_INLINE void xfer_k(const char* const (&s)[kMaxSrc], char* const (&
     uint4 x[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) x[k] = ld(k, v);
-    uint4 y = combine16<T, OP, K>(x, scale, sc);
+    uint4 y = combine16<T, OP, K, PM != PM_WT>(x, scale, sc);
 #pragma unroll
     for (int dd = 0; dd < kMaxDst; ++dd)
       if (dd < nd) st(dd, v, y);
@@ -1767,8 +1813,18 @@ __device__ FX_INLINE void reduce_interleaved(const char* const (&s)[kMaxSrc], ch
 // PM_WT (copy-engine allreduce): sources written by peers' DMA are read system-coherently and the
 // result is written through, so a stream-ordered flag write after this kernel publishes it.
 // vec bit 0: 16-B vector accesses allowed; bit 1 (fence protocol only): the grid-interleaved form.
+// The fp8 fence-protocol reduction asks for 4 waves per SIMD: two 512-thread workgroups per CU, at most 128
+// VGPRs (fp32 / bf16 fit that by themselves). The packed fp8 arithmetic would take 131 and keeps 20 B in
+// scratch with it. Measured (profiles/r5_fp8_packed): fp8 at fan-in 2 / 4 / 8 runs at 5.98 / 6.06 / 5.71 TB/s,
+// against 5.30 / 5.78 / 5.69 with per-element converts and 5.26 / 5.50 / 5.63 packed without it.
+// FLEXAR_REDUCE_OCC4=0 is the A/B build without it. Integer types and the write-through form (copy-engine path)
+// keep the default: held to 128 VGPRs they spill.
+#ifndef FLEXAR_REDUCE_OCC4
+#define FLEXAR_REDUCE_OCC4 1
+#endif
 template <typename T, typename OP, int PM>
-__global__ void __launch_bounds__(kExecThreads) reduce_kernel(SrcTable srcs, int nsrc, char* dst, char* dst2,
+__global__ void __launch_bounds__(kExecThreads)
+__attribute__((amdgpu_waves_per_eu(FLEXAR_REDUCE_OCC4 && PM != PM_WT && IsFp8<T>::value ? 4 : 1))) reduce_kernel(SrcTable srcs, int nsrc, char* dst, char* dst2,
                                                               uint64_t n, float scale, int vec) {
   if constexpr (PM != PM_WT && sizeof(T) < 16) {
     if ((vec & 3) == 3) {

@@ -52,6 +52,38 @@ def test_reduce_kernel_fp8_scaled(cuda, dtype):
     assert torch.equal(out.view(torch.uint8), want.view(torch.uint8))
 
 
+@pytest.mark.parametrize("dtype", [torch.float8_e4m3fn, torch.float8_e5m2])
+@pytest.mark.parametrize("nsrc", [2, 3, 8])
+def test_reduce_kernel_fp8_saturation_and_nan(cuda, dtype, nsrc):
+    """The packed fp8 store (device_exec.hpp fp8_store4) keeps the element store's semantics on every 16-B group
+    and on the scalar tail: sums beyond the largest finite saturate to it, infinities too (e5m2), and a NaN
+    anywhere in a column gives 0x7f. Finite results are the fp32 source-order sum rounded once (RNE)."""
+    from allreduce_over_mpi_amd.ops import reduce
+
+    big = 448.0 if dtype == torch.float8_e4m3fn else 57344.0
+    n = 4096 * 3 + 5  # vector groups plus a 5-element scalar tail
+    g = torch.Generator(device=cuda).manual_seed(11)
+    base = [torch.randn(n, device=cuda, generator=g) * 4 for _ in range(nsrc)]
+    for b in base:
+        b[::7] = big * 0.75           # columns 0, 7, 14, ...: every source 3/4 of the max -> saturating sums
+        b[3::7] = -big * 0.75
+    base[0][5::97] = float("nan")
+    base[-1][n - 2] = float("nan")    # in the tail
+    if dtype == torch.float8_e5m2:
+        base[1][11::101] = float("inf")
+        base[0][13::101] = float("-inf")
+    srcs = [b.to(dtype) for b in base]
+    out = reduce(srcs, "sum")
+    torch.cuda.synchronize()
+    acc = _seq_ref(srcs)
+    nan = torch.isnan(acc)
+    want = acc.clamp(-big, big).to(dtype).view(torch.uint8)
+    got = out.view(torch.uint8)
+    assert torch.equal(got[~nan], want[~nan])
+    assert bool((got[nan] == 0x7F).all()), got[nan].unique()
+    assert int(nan.sum()) > 0 and int((acc.abs() > big).sum()) > 0
+
+
 @pytest.mark.parametrize("op", ["sum", "max", "min", "band", "bor", "bxor", "prod"])
 def test_reduce_kernel_int(cuda, op):
     from allreduce_over_mpi_amd.ops import reduce
