@@ -237,8 +237,10 @@ __device__ FX_INLINE uint32_t fp8_store4(const float (&a)[4]) {
   return (fp8_word_encode<T>(c) & ~nan) | (0x7f7f7f7fu & nan);
 }
 
-// PACK = false keeps fp8 on the per-element converts: the write-through kernels (PM_WT) hold their register
-// budget with them (the packed form would take the copy-engine reduction from 2 workgroups per CU to 1).
+// PACK = false keeps fp8 on the per-element converts. The executor's transfers (xfer_k) use it: packed, the fp8
+// flat executor measured 2 % slower (364 against 356 us, 4 ranks x 100 MiB, profiles/r5_fp8_packed/verify), and
+// the write-through kernels would lose their second workgroup per CU. The grid-interleaved standalone reduction
+// packs (reduce_interleaved).
 template <typename T, typename OP, int K, bool PACK = true>
 __device__ FX_INLINE uint4 combine16(const uint4 (&x)[K], float scale, bool sc) {
   if (K == 1 && !sc) return x[0];  // pure move: no decode/encode round trip (fp8/bf16 copies at HBM rate)
@@ -339,7 +341,7 @@ __device__ FX_INLINE void xfer_k(const char* const (&s)[kMaxSrc], char* const (&
       for (int k = 0; k < K; ++k) x[u][k] = ld(k, v + u * nt);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      uint4 y = combine16<T, OP, K, PM != PM_WT>(x[u], scale, sc);
+      uint4 y = combine16<T, OP, K, false>(x[u], scale, sc);
 #pragma unroll
       for (int dd = 0; dd < kMaxDst; ++dd)
         if (dd < nd) st(dd, v + u * nt, y);
@@ -349,7 +351,7 @@ __device__ FX_INLINE void xfer_k(const char* const (&s)[kMaxSrc], char* const (&
     uint4 x[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) x[k] = ld(k, v);
-    uint4 y = combine16<T, OP, K, PM != PM_WT>(x, scale, sc);
+    uint4 y = combine16<T, OP, K, false>(x, scale, sc);
 #pragma unroll
     for (int dd = 0; dd < kMaxDst; ++dd)
       if (dd < nd) st(dd, v, y);
