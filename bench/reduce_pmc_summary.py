@@ -61,12 +61,15 @@ def main(root):
             row["lds_bank_conflict_cycles"] = s.get("SQ_LDS_BANK_CONFLICT", 0)
             out.append(row)
     times = trace_times(root)
-    # kernel_bench order: dtype-major, fan-in 2 then 8; each case 3 warm-up + 5 timed calls
+    # per dtype (by kernel name), kernel_bench's order: fan-in 2 then 8, each case 3 warm-up + 5 timed calls
+    token = {"float32": "reduce_kernel<float", "bfloat16": "bf16_t", "float8_e4m3fn": "fp8e4m3_t"}
     per = 8
-    i = 0
+    seen = defaultdict(int)
     for row in out:
-        ts = [t for _, t in times[i:i + per]]
-        i += per
+        mine = [t for n, t in times if token[row["dtype"]] in n]
+        i = seen[row["dtype"]]
+        seen[row["dtype"]] += per
+        ts = mine[i:i + per]
         if ts:
             us = sorted(ts)[len(ts) // 2]
             row["kernel_us_median"] = round(us, 1)
