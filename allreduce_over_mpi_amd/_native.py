@@ -32,6 +32,10 @@ class FlexarError(RuntimeError):
         self.rc = rc
 
 
+# int (*agree)(void* ctx) of flexar_comm_destroy_agreed
+AGREE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
+
+
 def _sig(lib):
     c = ctypes
     vp, sz, i, f, d, cp = c.c_void_p, c.c_size_t, c.c_int, c.c_float, c.c_double, c.c_char_p
@@ -46,6 +50,10 @@ def _sig(lib):
         "flexar_comm_connect": (i, [vp, vp]),
         "flexar_comm_destroy": (i, [vp]),
         "flexar_comm_destroy_local": (i, [vp]),
+        "flexar_comm_destroy_agreed": (i, [vp, AGREE_FN, vp]),
+        "flexar_comm_last_spec": (i, [vp, cp, sz]),
+        "flexar_parked_bytes": (u64, []),
+        "flexar_comm_set_zc_auto": (i, [vp, i]),
         "flexar_comm_resync": (i, [vp]),
         "flexar_comm_host_agree": (i, [vp, c.c_uint64, i, c.POINTER(c.c_uint64)]),
         "flexar_comm_host_page_check": (i, [vp, c.POINTER(i)]),

@@ -30,7 +30,8 @@ def default_candidates(world: int, nbytes: int, esize: int = 4) -> list[str]:
     """The schedules worth measuring for ``nbytes`` on ``world`` ranks (bench.py, tools/flexar_tune.py and
     ``autotune`` share this list): latency protocols for small buffers, every flat-stage protocol, rings
     on 1, 2 and 4 arc-disjoint channels and on N - 1 (the full mesh: ``ring:7`` at N = 8), RHD, the
-    two-stage FlexTree factorizations and the copy engines. The direction-balanced flat ("+bidir") joins the
+    two-stage FlexTree factorizations (each also on N - 1 link-balanced channels: ``rhd:7``, ``tree:4,2:7``)
+    and the copy engines. The direction-balanced flat ("+bidir") joins the
     flat protocols: on xGMI its reduce-scatter reads and its all-gather writes share the links' two
     directions. For 16/8-bit elements (``esize`` < 4) every multi-hop schedule is measured twice: with fp32
     partials (the default typed staging, one rounding) and rounded per hop ("+rw", 16-bit partials on the
@@ -48,8 +49,12 @@ def default_candidates(world: int, nbytes: int, esize: int = 4) -> list[str]:
         c.append(f"ring:{full}")
     if world > 2 and (world & (world - 1)) == 0:
         c.append("rhd+pull")
+        if world >= 4:  # N - 1 link-balanced channels: every stage on every link (planner.hpp build_tree_channels)
+            c.append(f"rhd:{world - 1}+pull")
     if world >= 8 and world % 4 == 0:
         c += [f"tree:4,{world // 4}+pull", f"tree:{world // 4},4+pull"]
+        if world <= 16:
+            c += [f"tree:4,{world // 4}:{world - 1}+pull", f"tree:{world // 4},4:{world - 1}+pull"]
     if nbytes >= (1 << 20):
         c.append("dma")
     if esize < 4:  # the single-rounding trade-off, measured: per-hop rounded forms of the multi-hop schedules

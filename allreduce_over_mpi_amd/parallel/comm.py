@@ -227,7 +227,8 @@ class Communicator:
             return
         nv.check(self._lib.flexar_comm_host_page_drop(self._h), "host_page_drop")
         self.host_page_note = ("host page not shared (no mark from rank(s) "
-                               f"{[i for i, r in enumerate(rows) if r != b'1']}): teardown falls back to deferred frees")
+                               f"{[i for i, r in enumerate(rows) if r != b'1']}): close() agrees over the bootstrap "
+                               "exchange instead (a close without it keeps this rank's workspace allocated)")
         if self.rank == 0:
             nv.log_warn(self.host_page_note)
 
@@ -457,8 +458,16 @@ class Communicator:
         nv.check(self._lib.flexar_comm_set_grid(self._h, int(grid), 0), "set_grid")
 
     def set_xfer_chunk(self, elems: int):
-        """Executor work split of large spans (every rank the same): see LocalGroup.set_xfer_chunk."""
-        nv.check(self._lib.flexar_comm_set_xfer_chunk(self._h, int(elems)), "set_xfer_chunk")
+        """Executor work split of large spans: see LocalGroup.set_xfer_chunk. Collective: producer and consumer
+        workgroups must split a span the same way on every rank, so the ranks exchange the value first and
+        a mismatch raises on every rank, leaving the setting unchanged (a silent mismatch would
+        misassign elements or hang)."""
+        elems = int(elems)
+        if self.world_size > 1 and self._exchange is not None:
+            rows = [r.decode() for r in self._exchange(str(elems).encode())]
+            if len(set(rows)) != 1:
+                raise self._agreed(nv.FlexarError(1, f"set_xfer_chunk: ranks disagree ({rows})"))
+        nv.check(self._lib.flexar_comm_set_xfer_chunk(self._h, elems), "set_xfer_chunk")
 
     def set_tune_table(self, text: str):
         """Install a measured "nranks bytes spec" table (FLEXAR_TUNE_FILE format); "" = cost model."""
@@ -757,12 +766,39 @@ class Communicator:
         frees (flexar_comm_destroy). ``collective=False`` (garbage collection) skips the agreements and
         leaves this rank's exported buffers allocated until the process exits."""
         if getattr(self, "_h", None) is not None and self._h.value:
+            agree_fn = self._teardown_agreement() if collective else None
             self._hi = 0
             h, self._h = self._h, ctypes.c_void_p()
             self._regs = {}
-            rc = (self._lib.flexar_comm_destroy if collective else self._lib.flexar_comm_destroy_local)(h)
+            if not collective:
+                rc = self._lib.flexar_comm_destroy_local(h)
+            elif agree_fn is not None:
+                rc = self._lib.flexar_comm_destroy_agreed(h, agree_fn, None)
+            else:
+                rc = self._lib.flexar_comm_destroy(h)
             if rc and collective:
                 nv.log_warn(f"rank {self.rank}: close: {nv.last_error()}")
+
+    def _teardown_agreement(self):
+        """The two teardown agreements over the bootstrap exchange, for a communicator whose ranks found at
+        connect that they share no host page (one container per rank, a private /dev/shm: every rank dropped it
+        together, _verify_host_page). The library calls the returned barrier where the page's agreements would
+        be, so the workspace is freed rather than parked. None otherwise: with the page the library
+        agrees by itself, and a page dropped later by one rank's timed-out agreement is not an agreed state (its
+        peers would not join an exchange), so that close parks and says so."""
+        if self.world_size == 1 or self._exchange is None or not self.host_page_note:
+            return None
+        exchange = self._exchange
+
+        def barrier(_ctx):
+            try:
+                exchange(b"")
+                return 1
+            except Exception:  # noqa: BLE001 - a failed agreement parks the workspace (reported by the library)
+                return 0
+
+        self._agree_cb = nv.AGREE_FN(barrier)  # kept alive for the duration of the destroy call
+        return self._agree_cb
 
     def __del__(self):
         try:

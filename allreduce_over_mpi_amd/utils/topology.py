@@ -30,7 +30,7 @@ def legacy_best(nranks: int, chunk: float = 100.0):
     """The reference cost model's argmin over ordered factorizations: (widths, cost)."""
     best = None
     for p in nv.enumerate_plans(nranks):
-        if not p.startswith("tree:"):
+        if not p.startswith("tree:") or p.count(":") > 1:  # a channelled copy has the same widths
             continue
         w = [int(x) for x in p[5:].split("+")[0].split(",")]
         c = nv.legacy_cost(w, nranks, chunk)

@@ -787,10 +787,7 @@ def main():
         "aggregate_busbw_GBps": round(busbw * world, 2),
         "hbm_TBps_per_rank": hbm_tbps,  # HBM traffic of the timed schedule / step time (MI355X peak ~8 TB/s)
         "peer_traffic_per_rank": link_rate,  # program-cost link bytes / step time (N > 1)
-        "rccl_busbw_GBps": rccl_busbw,
-        # the same-node bar: flexar's busbw over RCCL's on the same buffer, same ranks, same
-        # box (vs_baseline compares with the reference's CPU/MPICH number, which is context only)
-        "vs_rccl": round(busbw / rccl_busbw, 3) if rccl_busbw else None,
+        **rccl_fields(busbw, rccl_busbw, shared_rccl),
         "fallback": fallback,
         "tuner": tune_log or None,
         "cost_model": model,
@@ -819,6 +816,16 @@ def main():
     comm.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def rccl_fields(busbw, rccl_busbw, shared_rccl):
+    """The same-node bar: flexar's busbw over RCCL's on the same buffer, same ranks, same box
+    (vs_baseline compares with the reference's CPU/MPICH number, which is context only). In the shared-GPU
+    rehearsal RCCL runs over loopback sockets, so a ratio against it means nothing on xGMI:
+    the figure moves to rccl_busbw_GBps_loopback and vs_rccl is null."""
+    if shared_rccl:
+        return {"rccl_busbw_GBps": None, "rccl_busbw_GBps_loopback": rccl_busbw, "vs_rccl": None}
+    return {"rccl_busbw_GBps": rccl_busbw, "vs_rccl": round(busbw / rccl_busbw, 3) if rccl_busbw else None}
 
 
 def _x4(lo, hi):
@@ -1002,7 +1009,8 @@ def run_reduce_kernel(dev, mib=256.0, fanins=(2, 4, 8), dtypes=("float32", "bflo
 
 def run_config3(comm, world, rank, dev, dist, timed_fn, max_vec, host_ref, args):
     """BASELINE config #3: bf16, 1 GiB per rank. RHD (tree 2,..,2) with fp32 partials ("+f32": one rounding)
-    and rounded per hop ("+rw": the reference's ring semantics, bf16 partials on the links), and the
+    and rounded per hop ("+rw": the reference's ring semantics, bf16 partials on the links), single-channel and
+    with N - 1 link-balanced channels ("rhd:7" at N = 8), and the
     selector's own choice, each checked against the fp32 sum of the same bf16 inputs, next to RCCL bf16."""
     import torch
 
@@ -1021,7 +1029,10 @@ def run_config3(comm, world, rank, dev, dist, timed_fn, max_vec, host_ref, args)
     ref_max = float(ref.abs().max().item()) + 1e-6
     out = {"what": f"bf16 {args.config3_mb:g} MiB per rank", "bytes": n * 2, "variants": {}}
     pow2 = world > 1 and not world & (world - 1)
-    variants = (["rhd+pull+f32", "rhd+pull+rw"] if pow2 else []) + ["auto"]
+    # single-channel RHD drives one xGMI link per stage; rhd:C (C = N - 1 link-balanced channels, planner.hpp
+    # build_tree_channels) spreads every stage over all of them
+    variants = (["rhd+pull+f32", "rhd+pull+rw"] if pow2 else []) + \
+               ([f"rhd:{world - 1}+pull+f32", f"rhd:{world - 1}+pull+rw"] if pow2 and world >= 4 else []) + ["auto"]
     for spec in variants:
         a = None if spec == "auto" else spec
         failed, err = 0.0, None

@@ -279,8 +279,8 @@ int main(int argc, char** argv) {
         } else {  // bf16/fp16/fp8 or AVG have no MPI handle: call the flexar C API directly
           if (!device) die("this dtype/op needs --mem device");
           static flexar_comm_t dc = flexar::mpi::device_comm(MPI_COMM_WORLD);
-          if (flexar::mpi::zc_requested() && nranks > 1)  // refused everywhere -> staging schedule
-            (void)flexar::mpi::ensure_registered(dc, MPI_COMM_WORLD, buf, n * es);
+          if (nranks > 1)  // registration / zero-copy agreement, as MPI_Allreduce_FT does (mpi_mod.hpp zc_prepare)
+            (void)flexar::mpi::zc_prepare(MPI_COMM_WORLD, buf, buf, n * es);
           rc = flexar_allreduce(dc, buf, buf, n, dt, op, nullptr);
         }
       } else if (a.comm == "mpi") {
@@ -339,6 +339,12 @@ int main(int argc, char** argv) {
       hres.resize(n * es);
       if (device) (void)hipMemcpy(hres.data(), buf, n * es, hipMemcpyDeviceToHost);
       else memcpy(hres.data(), buf, n * es);
+    }
+    if (a.comm == "flexar" && device && rank == 0) {  // the schedule the last call ran (zero copy or staging)
+      char spec[256] = {0};
+      if (flexar::mpi::dev_holder(MPI_COMM_WORLD) &&
+          flexar_comm_last_spec(flexar::mpi::dev_holder(MPI_COMM_WORLD)->c, spec, sizeof(spec)) == 0 && spec[0])
+        fprintf(stderr, "schedule n=%zu: %s\n", n, spec);
     }
     if (a.sweep_max && rank == 0) {
       double bytes = (double)n * es;

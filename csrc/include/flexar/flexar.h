@@ -91,6 +91,14 @@ int flexar_comm_connect(flexar_comm_t comm, const void* all_handles);
  * that every rank has unmapped, then frees. A peer that does not arrive within FLEXAR_TIMEOUT_MS leaves
  * this rank's exported buffers allocated and returns FLEXAR_ERR_TIMEOUT (the communicator is gone). */
 int flexar_comm_destroy(flexar_comm_t comm);
+/* The same teardown when the host page is gone (flexar_comm_host_page_drop, or a host agreement timed out):
+ * `agree(ctx)` is called twice, where the page's two agreements would be (all calls finished; all peers
+ * unmapped), and must return 1 only once every rank has called it (e.g. a barrier over the caller's
+ * bootstrap). With the page present it is not called. Without either agreement the exported buffers stay
+ * allocated and the call returns non-zero (FLEXAR_ERR_STATE) with a named error. */
+int flexar_comm_destroy_agreed(flexar_comm_t comm, int (*agree)(void*), void* ctx);
+/* Bytes of exported buffers this process keeps allocated because a teardown could not agree (diagnostic). */
+uint64_t flexar_parked_bytes(void);
 /* Non-collective teardown (garbage collection): no agreement; exported buffers stay allocated. */
 int flexar_comm_destroy_local(flexar_comm_t comm);
 /* Collective host-side agreement (shared-memory page of a connected communicator): *out = the maximum
@@ -109,8 +117,10 @@ int flexar_comm_size(flexar_comm_t comm);
  *   "auto"                 cost-model selection (default)
  *   "ring" | "ring:C"      ring (C channels over link-disjoint Hamiltonian cycles)
  *   "flat"                 one-stage tree = direct reduce-scatter + all-gather (FT_TOPO unset)
- *   "rhd"                  tree 2,2,...,2 (recursive halving / doubling)
- *   "tree:a,b,c"           mixed-radix FlexTree with the given stage widths
+ *   "rhd" | "rhd:C"        tree 2,2,...,2 (recursive halving / doubling), optionally on C channels
+ *   "tree:a,b,c" | "tree:a,b,c:C"  mixed-radix FlexTree with the given stage widths; ":C" runs it on C
+ *                          link-balanced channels (disjoint slices, relabelled ranks: every stage covers the
+ *                          xGMI links evenly, "rhd:7" at N = 8 drives all 7 links in every stage)
  *   "oneshot"              every rank reduces the full buffer (small messages)
  *   "ft"                   honour FT_TOPO exactly like the reference (any 1 = ring)
  * Optional suffixes: "+pull" (all-gather pulls from owners) / "+push" (owners push), "+nts" (streaming
@@ -236,6 +246,11 @@ uint64_t flexar_comm_model_hash(flexar_comm_t comm);
 int flexar_comm_stats(flexar_comm_t comm, char* buf, size_t buflen);
 /* Describe the algorithm the communicator would run for (count, dtype). */
 int flexar_comm_describe(flexar_comm_t comm, size_t count, int dtype, char* buf, size_t buflen);
+/* The schedule the last allreduce on this communicator ran (after the zero-copy decision), "" before any. */
+int flexar_comm_last_spec(flexar_comm_t comm, char* buf, size_t buflen);
+/* Whether automatic choices may switch to zero copy on registered buffers (FLEXAR_ZC_AUTO at creation).
+ * Every rank must set the same value before a call; the MPI layer sets it per call from an agreement. */
+int flexar_comm_set_zc_auto(flexar_comm_t comm, int on);
 
 /* ---- in-process group: nranks ranks on ONE device in ONE process ---------------
  * Every rank's workgroups run in a single launch (rank = blockIdx / grid), so the

@@ -428,6 +428,7 @@ inline HostComm* host_comm(MPI_Comm comm) {
 // device communicator's teardown agrees with its peers by itself (flexar_comm_destroy, host_barrier.hpp).
 struct DevHolder {
   flexar_comm_t c = nullptr;
+  bool zc_closed = false;  // a registration was refused (on every rank): no further attempts
   ~DevHolder() {
     if (c) flexar_comm_destroy(c);
   }
@@ -444,11 +445,14 @@ inline int dev_keyval() {
   return kv;
 }
 extern "C" int flexar_current_device(void);
-inline flexar_comm_t device_comm(MPI_Comm comm) {
+inline DevHolder* dev_holder(MPI_Comm comm) {
   int flag = 0;
   void* v = nullptr;
   MPI_Comm_get_attr(comm, dev_keyval(), &v, &flag);
-  if (flag) return static_cast<DevHolder*>(v)->c;
+  return flag ? static_cast<DevHolder*>(v) : nullptr;
+}
+inline flexar_comm_t device_comm(MPI_Comm comm) {
+  if (DevHolder* h = dev_holder(comm)) return h->c;
   int rank, size;
   MPI_Comm_rank(comm, &rank);
   MPI_Comm_size(comm, &size);
@@ -538,14 +542,36 @@ inline flexar_comm_t device_comm(MPI_Comm comm) {
 inline int allreduce(const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype datatype, MPI_Op mop,
                      MPI_Comm comm);
 
-// FLEXAR_ALGO=flat+zc with device buffers: the zero-copy schedule reads the peers' buffers directly, so
-// the call's buffer must be registered on every rank. Registration is collective and cached per range;
-// a range is (re-)registered when any rank lacks it or its allocation changed since (freed and its
-// address reused: flexar_reg_find < 0), and the new registration replaces the stale one on every rank.
-inline bool zc_requested() {
-  static const bool zc = getenv("FLEXAR_ALGO") && strstr(getenv("FLEXAR_ALGO"), "+zc") != nullptr;
-  return zc;
+// Zero copy through the MPI entry points. The zero-copy schedules read / write the peers'
+// buffers directly, so a call's buffers must be registered on every rank (collective, cached per range).
+//  * FORCE (FLEXAR_ALGO names "+zc"): every device call registers its buffers first (ensure_registered);
+//  * AUTO (default: FLEXAR_ALGO unset or "auto", FLEXAR_MPI_ZC unset or 1): device calls of at least
+//    FLEXAR_MPI_ZC_MIN_BYTES (1 MiB) take part in one agreement per call (a 2-int MPI_Allreduce MIN): "both
+//    buffers registered and fresh on every rank" runs the cost model's choice with zero copy allowed (the
+//    flat schedule becomes "+zc+push", zc_policy.hpp); otherwise, while registrations are below
+//    FLEXAR_MPI_ZC_MAX_REGS (64) and none was refused, the buffers are registered collectively (a stale
+//    registration - freed, address reused - is replaced) and the call runs zero copy; else it runs staging
+//    with zero copy disallowed on every rank (flexar_comm_set_zc_auto), so a registration that is fresh on
+//    one rank and stale on another can never split the ranks between two schedules. The c10d backend's
+//    probe window (parallel/backend.py) closes after idle agreements because it sits on DDP's issue path;
+//    an MPI call already synchronises the device, and only the per-call agreement catches a freed and
+//    reused address, so here it stays;
+//  * OFF: FLEXAR_ALGO set to a spec without "+zc" (the user chose the schedule), FLEXAR_MPI_ZC=0 or
+//    FLEXAR_ZC_AUTO=0.
+// Reference entry point: allreduce_over_mpi/mpi_mod.hpp:1167-1221 (MPI_Allreduce_FT), driven by
+// benchmark.cpp:147-159.
+enum class ZcMode { OFF = 0, AUTO = 1, FORCE = 2 };
+inline ZcMode zc_mode_of(const char* algo, const char* mpi_zc, const char* zc_auto = nullptr) {
+  if (algo && strstr(algo, "+zc")) return ZcMode::FORCE;
+  if ((mpi_zc && !strcmp(mpi_zc, "0")) || (zc_auto && !strcmp(zc_auto, "0"))) return ZcMode::OFF;
+  if (algo && *algo && strcmp(algo, "auto") != 0) return ZcMode::OFF;
+  return ZcMode::AUTO;
 }
+inline ZcMode zc_mode() {
+  static const ZcMode m = zc_mode_of(getenv("FLEXAR_ALGO"), getenv("FLEXAR_MPI_ZC"), getenv("FLEXAR_ZC_AUTO"));
+  return m;
+}
+inline bool zc_requested() { return zc_mode() == ZcMode::FORCE; }
 inline int ensure_registered(flexar_comm_t c, MPI_Comm comm, const void* p, size_t bytes) {
   int mine = flexar_reg_find(c, p, bytes) > 0 ? 1 : 0, all = 0;
   MPI_Allreduce(&mine, &all, 1, MPI_INT, MPI_MIN, comm);
@@ -564,6 +590,50 @@ inline int ensure_registered(flexar_comm_t c, MPI_Comm comm, const void* p, size
   if (!ok) fprintf(stderr, "[flexar] register: %s\n", flexar_last_error());
   MPI_Allreduce(&ok, &all_ok, 1, MPI_INT, MPI_MIN, comm);
   return all_ok ? MPI_SUCCESS : MPI_ERR_OTHER;
+}
+
+// Registration / zero-copy decision for one device call on `comm` (see zc_mode). Collective over `comm` for
+// FORCE and for AUTO calls of at least the minimum size (every rank passes the same count); returns true
+// when the call may run zero copy.
+inline bool zc_prepare(MPI_Comm comm, const void* in, const void* out, size_t bytes) {
+  const ZcMode m = zc_mode();
+  DevHolder* d = dev_holder(comm);
+  if (!d) return false;
+  flexar_comm_t c = d->c;
+  if (m == ZcMode::OFF) return false;
+  if (m == ZcMode::FORCE) {
+    // a registration refused on any rank (all agree) leaves the buffers unregistered: the call then runs
+    // the staging schedule (comm.hip falls back from a default "+zc" spec for unregistered buffers)
+    int e = ensure_registered(c, comm, in, bytes);
+    if (e == MPI_SUCCESS && in != out) e = ensure_registered(c, comm, out, bytes);
+    return e == MPI_SUCCESS;
+  }
+  static const uint64_t min_bytes = [] {
+    const char* e = getenv("FLEXAR_MPI_ZC_MIN_BYTES");
+    return e && *e ? strtoull(e, nullptr, 10) : (1ull << 20);
+  }();
+  static const int max_regs = [] {
+    const char* e = getenv("FLEXAR_MPI_ZC_MAX_REGS");
+    return e && *e ? atoi(e) : 64;
+  }();
+  if (bytes < min_bytes) {  // the same on every rank: no agreement, never zero copy
+    flexar_comm_set_zc_auto(c, 0);
+    return false;
+  }
+  auto fresh = [&](const void* p) { return flexar_reg_find(c, p, bytes) > 0; };
+  const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
+  int v[2] = {fresh(in) && (in == out || fresh(out)) ? 1 : 0,
+              aligned && !d->zc_closed && flexar_reg_count(c) + 2 <= max_regs ? 1 : 0};
+  MPI_Allreduce(MPI_IN_PLACE, v, 2, MPI_INT, MPI_MIN, comm);
+  bool use = v[0] != 0;
+  if (!use && v[1]) {
+    int e = ensure_registered(c, comm, in, bytes);  // agreed result on every rank
+    if (e == MPI_SUCCESS && in != out) e = ensure_registered(c, comm, out, bytes);
+    if (e == MPI_SUCCESS) use = true;
+    else d->zc_closed = true;
+  }
+  flexar_comm_set_zc_auto(c, use ? 1 : 0);
+  return use;
 }
 
 // Device buffers spanning nodes: intra-node reduce-scatter over xGMI (flexar), inter-node allreduce
@@ -633,13 +703,7 @@ inline int allreduce(const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
       return hierarchical_device_allreduce(*hc, in, recvbuf, count, datatype, mop, dt, op);
     if (hc->nodes == 1 || size <= 1) {  // one node: xGMI/IPC GPU engine
       flexar_comm_t c = device_comm(comm);
-      if (zc_requested() && size > 1) {
-        // a registration refused on any rank (all agree) leaves the buffers unregistered: the call then runs
-        // the staging schedule (comm.hip falls back from a default "+zc" spec for unregistered buffers)
-        int e = ensure_registered(c, comm, in, count * es);
-        if (e == MPI_SUCCESS && in != recvbuf) e = ensure_registered(c, comm, recvbuf, count * es);
-        (void)e;
-      }
+      if (size > 1) zc_prepare(comm, in, recvbuf, count * es);
       int rc = flexar_allreduce(c, in, recvbuf, count, dt, op, nullptr);
       // MPI semantics: recvbuf holds the result when the call returns (a NIC, MPI_Send or another stream
       // may read it next), and a device watchdog timeout is this call's error, not the next one's

@@ -129,7 +129,17 @@ class Planner {
         if (w < 2) { if (err) *err = "tree width < 2"; return false; }
       // typed staging: fp32 partials need the fused forms (no partial sum passes through OUT); fp8 wire
       // pulls (one quantised copy of each result instead of a re-quantised multicast)
-      build_tree_lonely(spec.widths, (uint32_t)prod, spec.ag == AgMode::PULL || wire >= 2, spec.fuse || wire == 1);
+      const bool pull = spec.ag == AgMode::PULL || wire >= 2, fuse = spec.fuse || wire == 1;
+      if (spec.channels > 1) {
+        if (prod != (long)N) {
+          if (err) *err = "tree channels (tree:...:C, rhd:C) need widths whose product is the world size";
+          return false;
+        }
+        build_tree_channels(spec.widths, std::min(spec.channels, max_tree_channels((int)spec.widths.size())), pull,
+                            fuse);
+      } else {
+        build_tree_lonely(spec.widths, (uint32_t)prod, pull, fuse);
+      }
       if (r >= (uint32_t)prod) {
         // A lonely rank allocates only its fold slots, the tree ranks much more. Every rank sizes its
         // pieces (and the MPI engine its shared window) from its own stg_elems, so all ranks must report
@@ -585,9 +595,35 @@ class Planner {
     finish_channel();
   }
 
-  void build_tree(const std::vector<int>& widths, const uint32_t N, uint16_t first, bool pull, bool fuse) {
+  // Link-balanced multi-channel tree ("rhd:C", "tree:a,b:C"): channel c runs the tree on its own aligned
+  // slice of the buffer, in logical ranks relabelled by tree_channel_labels (topology.hpp), with its own
+  // staging and its own flag slots. Same blocks, same fan-ins, same hand-off count as the one-channel tree;
+  // in every stage the C channels' groups cover the xGMI links evenly instead of loading w_s - 1 of them.
+  void build_tree_channels(const std::vector<int>& widths, int C, bool pull, bool fuse) {
     const uint32_t S = (uint32_t)widths.size();
-    uint64_t split = round_up((count + N - 1) / N);
+    const auto& labels = tree_channel_labels((int)N, widths, C);
+    const uint64_t per = round_up((count + C - 1) / C);
+    for (int c = 0; c < C; ++c) {
+      const uint64_t c_off = std::min<uint64_t>(count, (uint64_t)c * per);
+      const uint64_t c_cnt = std::min<uint64_t>(count - c_off, per);
+      build_tree(widths, N, BUF_IN, pull, fuse, &labels[c], c_off, c_cnt, (uint32_t)c * 2 * S);
+      finish_channel();
+    }
+  }
+
+  // One tree over ranks [0, N) (N = the tree ranks' count when lonely ranks fold in). `phys` relabels it:
+  // the schedule is built in logical ranks and logical rank l is physical rank (*phys)[l] (null = identity).
+  // [c_off, c_off + c_cnt) is the slice of the buffer it reduces, slot0 its first flag slot.
+  void build_tree(const std::vector<int>& widths, const uint32_t N, uint16_t first, bool pull, bool fuse,
+                  const std::vector<uint32_t>* phys = nullptr, uint64_t c_off = 0, uint64_t c_cnt = ~0ull,
+                  uint32_t slot0 = 0) {
+    const uint32_t S = (uint32_t)widths.size();
+    const uint64_t cnt = c_cnt == ~0ull ? count : c_cnt;
+    uint64_t split = round_up((cnt + N - 1) / N);
+    std::vector<uint32_t> lab(N), lg(std::max<uint32_t>(N, this->N));
+    for (uint32_t l = 0; l < N; ++l) lab[l] = phys ? (*phys)[l] : l;
+    for (uint32_t l = 0; l < N; ++l) lg[lab[l]] = l;
+    const uint32_t lr = lg[r];  // this rank's logical rank
     std::vector<Stage> st(S);
     uint32_t g = 1;
     for (uint32_t s = 0; s < S; ++s) {
@@ -595,12 +631,12 @@ class Planner {
       x.w = widths[s];
       x.g = g;
       x.G = g * x.w;
-      x.base = r / x.G * x.G + r % g;
-      x.myj = (r / g) % x.w;
-      for (uint32_t j = 0; j < x.w; ++j) x.members.push_back(x.base + j * g);
+      x.base = lr / x.G * x.G + lr % g;
+      x.myj = (lr / g) % x.w;
+      for (uint32_t j = 0; j < x.w; ++j) x.members.push_back(lab[x.base + j * g]);  // physical ranks
       g = x.G;
     }
-    auto digit = [&](uint32_t rank, uint32_t s) { return (rank / st[s].g) % st[s].w; };
+    auto digit = [&](uint32_t l, uint32_t s) { return (l / st[s].g) % st[s].w; };  // of a logical index
     // Digit-reversed block placement: block k, with mixed-radix digits d_s = digit(k, s),
     // lives at physical block pos(k) = sum_s d_s * N / G_s (the stage-0 digit most significant). The blocks
     // a stage-s member sends one peer (k == p mod G_s: digits 0..s fixed) are then ONE contiguous span of
@@ -611,16 +647,17 @@ class Planner {
     std::vector<uint32_t> pos(N, 0);
     for (uint32_t k = 0; k < N; ++k)
       for (uint32_t s = 0; s < S; ++s) pos[k] += digit(k, s) * (N / st[s].G);
-    auto boff = [&](uint32_t k) { return (uint64_t)pos[k] * split; };
+    auto rel = [&](uint32_t k) { return (uint64_t)pos[k] * split; };  // offset of block k in the slice
+    auto boff = [&](uint32_t k) { return c_off + rel(k); };
     auto blen = [&](uint32_t k) -> uint64_t {
-      uint64_t s = boff(k);
-      return s >= count ? 0 : std::min(split, count - s);
+      uint64_t s = rel(k);
+      return s >= cnt ? 0 : std::min(split, cnt - s);
     };
     auto sidx = [&](uint32_t s, uint32_t k) { return (uint64_t)(pos[k] % (N / st[s].G)); };
-    // blocks of member p at stage s: k == p (mod G_s), in buffer order
+    // blocks of (physical) member p at stage s: k == logical(p) (mod G_s), in buffer order
     auto blocks_of = [&](uint32_t p, uint32_t s) {
       std::vector<uint32_t> b;
-      for (uint32_t k = p % st[s].G; k < N; k += st[s].G) b.push_back(k);
+      for (uint32_t k = lg[p] % st[s].G; k < N; k += st[s].G) b.push_back(k);
       std::sort(b.begin(), b.end(), [&](uint32_t a, uint32_t c) { return pos[a] < pos[c]; });
       return b;
     };
@@ -651,9 +688,9 @@ class Planner {
     auto ag_off = [&](uint32_t s, uint32_t j, uint32_t k) {
       return ag_base[s] + ((uint64_t)j * (N / st[s].G) + sidx(s, k)) * split;
     };
-    auto pub_off = [&](uint32_t k) { return pub_base + boff(k); };
-    // rank in stage-s group of `r` that owns block k after stage s
-    auto owner_at = [&](uint32_t k, uint32_t s) { return st[s].base + digit(k, s) * st[s].g; };
+    auto pub_off = [&](uint32_t k) { return pub_base + rel(k); };
+    // (physical) rank in stage-s group of `r` that owns block k after stage s
+    auto owner_at = [&](uint32_t k, uint32_t s) { return lab[st[s].base + digit(k, s) * st[s].g]; };
 
     // ---------------- reduce-scatter
     for (uint32_t s = 0; s < S; ++s) {
@@ -663,8 +700,8 @@ class Planner {
         for (uint32_t p : x.others())
           for (uint32_t k : blocks_of(p, s)) xfer(blen(k), {own_at(s, k, first)}, {rs_loc(s, p, x.myj, k)}, 1.0f);
       }
-      signal(x.others(), s);
-      wait(x.others(), s);
+      signal(x.others(), slot0 + s);
+      wait(x.others(), slot0 + s);
       bool last = (s + 1 == S);
       for (uint32_t k : blocks_of(r, s)) {
         std::vector<Loc> srcs{own_at(s, k, first)};
@@ -695,7 +732,7 @@ class Planner {
     for (int si = (int)S - 1; si >= 0; --si) {
       uint32_t s = (uint32_t)si;
       const Stage& x = st[s];
-      uint32_t slot = S + s;
+      uint32_t slot = slot0 + S + s;
       if (pull) {
         signal(x.others(), slot);  // my pub holds blocks_of(r, s)
         wait(x.others(), slot);
@@ -716,7 +753,7 @@ class Planner {
         signal(x.others(), slot);
         wait(x.others(), slot);
         for (uint32_t p : x.others()) {
-          uint32_t j = digit(p, s);
+          uint32_t j = digit(lg[p], s);
           for (uint32_t k : blocks_of(p, s)) {
             std::vector<Loc> dsts{loc(BUF_OUT, r, boff(k))};
             if (fuse)  // forward to every member of every lower AG stage right away

@@ -35,7 +35,7 @@ enum class AgMode { AUTO, PUSH, PULL };
 struct AlgoSpec {
   AlgoKind kind = AlgoKind::AUTO;
   std::vector<int> widths;  // TREE stage widths, product == nranks
-  int channels = 1;         // RING: number of arc-disjoint rings
+  int channels = 1;         // RING: arc-disjoint rings; TREE: link-balanced relabelled copies (tree_channel_labels)
   AgMode ag = AgMode::AUTO; // TREE: all-gather direction
   bool fuse = true;         // fuse reduce->forward (tree RS / AG multicast)
   bool nts = false;         // executor stores with the streaming (nontemporal) policy
@@ -75,6 +75,7 @@ struct AlgoSpec {
       case AlgoKind::TREE:
         ss << "tree:";
         for (size_t i = 0; i < widths.size(); ++i) ss << (i ? "," : "") << widths[i];
+        if (channels > 1) ss << ":" << channels;
         break;
     }
     if (kind == AlgoKind::TREE && ag == AgMode::PULL) ss << "+pull";
@@ -244,14 +245,30 @@ inline bool parse_algo(const std::string& raw, int nranks, AlgoSpec* spec, std::
     return true;
   }
   if (head == "flat" || head == "twoshot") { spec->kind = AlgoKind::TREE; spec->widths = {nranks}; return true; }
+  // trailing ":C" of a tree spec: C link-balanced channels ("rhd:7", "tree:4,2:7")
+  auto tree_channels = [&](const std::string& a) -> bool {
+    if (a.empty()) return true;
+    std::vector<int> v;
+    if (!parse_int_list(a, &v, err) || v.size() != 1) {
+      if (err && err->empty()) *err = "tree channel count ':C' expects one integer";
+      return false;
+    }
+    spec->channels = v[0];
+    return true;
+  };
   if (head == "rhd") {
     if (nranks < 2 || (nranks & (nranks - 1))) { if (err) *err = "rhd needs a power-of-two world size"; return false; }
     spec->kind = AlgoKind::TREE;
     for (int n = nranks; n > 1; n >>= 1) spec->widths.push_back(2);
-    return true;
+    return tree_channels(arg);
   }
   if (head == "tree") {
     std::vector<int> w;
+    const size_t cc = arg.find(':');
+    if (cc != std::string::npos) {
+      if (!tree_channels(arg.substr(cc + 1))) return false;
+      arg = arg.substr(0, cc);
+    }
     if (!parse_int_list(arg, &w, err)) return false;
     long prod = 1;
     for (int x : w) {
@@ -387,8 +404,114 @@ inline std::vector<int> ring_order(int nranks, int channel, int C = 1) {
   return ord;
 }
 
+// ---- link-balanced channels for multi-stage trees ("rhd:C", "tree:a,b:C") --------------------------------
+// A FlexTree stage puts a rank in a group of w_s members (reference Send_Ops / Recv_Ops,
+// mpi_mod.hpp:147-214), so stage s of one tree drives w_s - 1 of a GPU's N - 1 xGMI links and RHD drives one.
+// C channels run the same tree on disjoint slices of the buffer, each over a relabelled rank set: channel c
+// runs the tree in LOGICAL ranks and labels[c][l] is the physical rank playing logical rank l. The relabellings
+// are chosen so that, stage by stage, the channels' groups cover the links evenly.
+//  * N = 2^k, every width a power of two: ranks are vectors of GF(2)^k and a stage's group is a coset of the
+//    subspace spanned by its logical bits. Channel c maps logical bit b to the field element g^(c+b) of GF(2^k),
+//    g a primitive element (a Singer cycle): {g^c, .., g^(c+k-1)} is a basis, so every channel is a valid tree,
+//    and over C = N - 1 channels the stage subspaces run through one full orbit of the cycle, which covers every
+//    nonzero element equally often. RHD at N = 8: stage s of channel c pairs r with r ^ g^(c+s) - in every stage
+//    the 7 channels use 7 distinct partners, i.e. every link. tree:4,2 / tree:2,4: the 7 planes of GF(2)^3.
+//    Channel 0 is the identity (the single-channel tree's labels).
+//  * any other (N, widths): a deterministic greedy search - channel 0 the identity, each next channel the best
+//    of a fixed pseudo-random candidate set by (sum over stages of the busiest link's load, then the sum of
+//    squared loads). Every rank computes the same labels.
+inline int exact_log2(int n) {
+  int k = 0;
+  while ((1 << k) < n) ++k;
+  return (1 << k) == n ? k : -1;
+}
+inline std::vector<std::vector<uint32_t>> tree_channel_labels_compute(int n, const std::vector<int>& widths, int C) {
+  std::vector<std::vector<uint32_t>> out;
+  const int k = exact_log2(n);
+  bool pow2 = k >= 1 && k <= 4;
+  for (int w : widths) pow2 = pow2 && exact_log2(w) >= 1;
+  if (pow2) {
+    static const uint32_t prim[5] = {0, 0x3, 0x7, 0xB, 0x13};  // x+1, x^2+x+1, x^3+x+1, x^4+x+1
+    std::vector<uint32_t> pw((size_t)std::max(1, n - 1));
+    pw[0] = 1;
+    for (size_t i = 1; i < pw.size(); ++i) {
+      uint32_t x = pw[i - 1] << 1;
+      if (x & (uint32_t)n) x ^= prim[k];
+      pw[i] = x;
+    }
+    for (int c = 0; c < C; ++c) {
+      std::vector<uint32_t> lab(n, 0);
+      for (int l = 0; l < n; ++l)
+        for (int b = 0; b < k; ++b)
+          if (l >> b & 1) lab[l] ^= pw[(size_t)(c + b) % pw.size()];
+      out.push_back(lab);
+    }
+    return out;
+  }
+  // greedy: loads[s][a * n + b] = channels whose stage-s groups contain the pair (a, b)
+  const size_t S = widths.size();
+  std::vector<std::vector<int>> load(S, std::vector<int>((size_t)n * n, 0));
+  auto groups = [&](const std::vector<uint32_t>& lab, size_t s, const std::function<void(uint32_t, uint32_t)>& fn) {
+    int g = 1;
+    for (size_t t = 0; t < s; ++t) g *= widths[t];
+    for (int base = 0; base < n; ++base) {
+      if ((base / g) % widths[s]) continue;  // one pass per group: its digit-0 member
+      for (int i = 0; i < widths[s]; ++i)
+        for (int j = i + 1; j < widths[s]; ++j) {
+          uint32_t a = lab[base + i * g], b = lab[base + j * g];
+          fn(std::min(a, b), std::max(a, b));
+        }
+    }
+  };
+  uint64_t seed = 0x9E3779B97F4A7C15ull ^ ((uint64_t)n << 32);
+  for (int w : widths) seed = seed * 1000003ull + (uint64_t)w;
+  auto next = [&]() {  // splitmix64: the same sequence on every rank and platform
+    uint64_t z = (seed += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  };
+  for (int c = 0; c < C; ++c) {
+    std::vector<uint32_t> best(n);
+    for (int l = 0; l < n; ++l) best[l] = (uint32_t)l;
+    if (c > 0) {
+      double best_score = 1e300;
+      std::vector<uint32_t> cand(n);
+      for (int trial = 0; trial < 256; ++trial) {
+        for (int l = 0; l < n; ++l) cand[l] = (uint32_t)l;
+        for (int i = n - 1; i > 0; --i) std::swap(cand[i], cand[next() % (uint64_t)(i + 1)]);
+        double mx_sum = 0, sq = 0;
+        for (size_t s = 0; s < S; ++s) {
+          int mx = 0;
+          std::vector<int> tmp = load[s];
+          groups(cand, s, [&](uint32_t a, uint32_t b) { ++tmp[(size_t)a * n + b]; });
+          for (int v : tmp) mx = std::max(mx, v), sq += (double)v * v;
+          mx_sum += mx;
+        }
+        const double score = mx_sum * 1e6 + sq;
+        if (score < best_score) best_score = score, best = cand;
+      }
+    }
+    for (size_t s = 0; s < S; ++s) groups(best, s, [&](uint32_t a, uint32_t b) { ++load[s][(size_t)a * n + b]; });
+    out.push_back(best);
+  }
+  return out;
+}
+inline const std::vector<std::vector<uint32_t>>& tree_channel_labels(int n, const std::vector<int>& widths, int C) {
+  static std::mutex mu;
+  static std::map<std::vector<int>, std::vector<std::vector<uint32_t>>> memo;
+  std::vector<int> key{n, C};
+  key.insert(key.end(), widths.begin(), widths.end());
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = memo.find(key);
+  if (it == memo.end()) it = memo.emplace(key, tree_channel_labels_compute(n, widths, C)).first;
+  return it->second;
+}
+// channels a tree of S stages may run: two flag slots per stage and channel
+inline int max_tree_channels(int S) { return std::max(1, (int)kProgSlots / std::max(1, 2 * S)); }
+
 // Candidate plans for the selector: ring (1..C channels), every ordered factorization as a tree,
-// and the one-shot.
+// the multi-stage trees again with N - 1 link-balanced channels, and the one-shot.
 inline std::vector<AlgoSpec> enumerate_plans(int nranks) {
   std::vector<AlgoSpec> out;
   if (nranks <= 1) return out;
@@ -402,6 +525,13 @@ inline std::vector<AlgoSpec> enumerate_plans(int nranks) {
   for (auto& w : ordered_factorizations(nranks, 4096)) {
     AlgoSpec t; t.kind = AlgoKind::TREE; t.widths = w; out.push_back(t);
   }
+  if (nranks >= 4 && nranks <= (int)kMaxRanks)
+    for (auto& w : ordered_factorizations(nranks, 4096)) {
+      if (w.size() < 2) continue;
+      AlgoSpec t; t.kind = AlgoKind::TREE; t.widths = w;
+      t.channels = std::min(nranks - 1, max_tree_channels((int)w.size()));
+      out.push_back(t);
+    }
   // prime N: trees over N - 1 ranks plus one lonely rank (reference ChooseWidth.h, "+1" structures)
   if (nranks > 3 && is_prime(nranks))
     for (auto& w : ordered_factorizations(nranks - 1, 4096)) {

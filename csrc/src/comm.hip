@@ -281,7 +281,8 @@ void fill_ctx(flexar_comm* c, DevProgram* dp, const void* in, void* out, DevCtx*
   x->epochs = c->epochs;
   x->stg_half_bytes = c->half_bytes;
   x->err = c->err_dev;
-  x->progress = reinterpret_cast<uint64_t*>(c->err_dev) + 1;
+  // launch progress words for the crash report: two system-scope stores per launch, only when the report is on
+  x->progress = crumbs_on() ? reinterpret_cast<uint64_t*>(c->err_dev) + 1 : nullptr;
   x->ichunk = c->xfer_chunk;  // 0 = slices (FLEXAR_EXEC_INTERLEAVE, flexar_comm_set_xfer_chunk)
   x->timeout_ticks = c->timeout_ticks;
   x->vec_ok = vec_ok_for(((uintptr_t)in) | ((uintptr_t)out));
@@ -482,6 +483,23 @@ int flexar_comm_describe(flexar_comm_t c, size_t count, int dtype, char* buf, si
   return 0;
 }
 
+int flexar_comm_last_spec(flexar_comm_t c, char* buf, size_t buflen) {
+  if (!c || !buf || !buflen) return FLEXAR_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  snprintf(buf, buflen, "%s", c->have_last_spec ? c->last_spec.str().c_str() : "");
+  return 0;
+}
+
+int flexar_comm_set_zc_auto(flexar_comm_t c, int on) {
+  if (!c) return FLEXAR_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->zc_auto != (on != 0)) {
+    c->zc_auto = on != 0;
+    c->memo_gen++;  // a remembered call may hold the other decision
+  }
+  return 0;
+}
+
 int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count, int dtype, int op,
                         void* stream, const char* algo, float scale) {
   int rc = validate_call(c, dtype, op, scale);
@@ -535,6 +553,8 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     if (d > 0) hit = hit && m.s.zc;
     if (d < 0) hit = hit && !m.s.zc;
   }
+  c->last_spec = s;
+  c->have_last_spec = true;
   auto remember = [&](uint64_t piece, DevProgram* dp, int grid) {
     if (hit) return;
     m.gen = c->memo_gen;

@@ -710,7 +710,10 @@ static void grave_keep(int device, void* p, uint64_t bytes, int rank) {
 // unmapped before anything is freed - no rank can then allocate, export or map new memory while a peer
 // still holds a mapping of this communicator's. A peer that does not arrive within FLEXAR_TIMEOUT_MS
 // (or a local destroy) leaves this rank's exported buffers parked (grave_keep) instead of freed.
-static int destroy_impl(flexar_comm* c, bool agree) {
+// Without the host page (a private /dev/shm per rank, or a host agreement that timed out and dropped it) the
+// caller may supply the two agreements itself (`ext`, flexar_comm_destroy_agreed: e.g. a barrier over its
+// bootstrap exchange), so the workspace is still freed instead of parked.
+static int destroy_impl(flexar_comm* c, bool agree, int (*ext)(void*) = nullptr, void* ext_ctx = nullptr) {
   crumb_phase("comm_destroy", agree ? "collective" : "local", c->rank, c->nranks);
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
@@ -718,11 +721,17 @@ static int destroy_impl(flexar_comm* c, bool agree) {
   int rc = 0;
   bool agreed = false;
   std::string why;
+  const bool use_ext = agree && !c->hb && ext != nullptr;
   if (c->hb && agree) {
     int late = -1;
     agreed = c->hb->arrive_and_wait(timeout_ms, &late);
     if (!agreed) why = "rank " + std::to_string(late) + " did not reach the teardown within " +
                        std::to_string(timeout_ms) + " ms";
+  } else if (use_ext) {
+    agreed = ext(ext_ctx) != 0;
+    if (!agreed) why = "the caller's agreement before teardown failed";
+  } else if (agree) {
+    why = "no teardown agreement (the host page was dropped and the caller gave no agreement of its own)";
   }
   // teardown keeps going past failures; FLEXAR_LOG_LEVEL=info names them
   auto ipc_close = [&](void* p, const char* what, int r) {
@@ -763,11 +772,14 @@ static int destroy_impl(flexar_comm* c, bool agree) {
   if (c->st_buf) (void)hipFree(c->st_buf);
   if (c->cal_dev) (void)hipFree(c->cal_dev);
   if (c->st_bad) (void)hipHostFree(c->st_bad);
-  if (agreed) {
+  if (agreed && c->hb) {
     int late = -1;
     agreed = c->hb->arrive_and_wait(timeout_ms, &late);  // every rank has unmapped this rank's buffers
     if (!agreed) why = "rank " + std::to_string(late) + " did not finish unmapping within " +
                        std::to_string(timeout_ms) + " ms";
+  } else if (agreed && use_ext) {
+    agreed = ext(ext_ctx) != 0;
+    if (!agreed) why = "the caller's agreement after unmapping failed";
   }
   // peers may map stg / flags only once this rank has exported them, and only through a connect that
   // joined the agreement (hb); without an agreement they stay parked
@@ -778,10 +790,11 @@ static int destroy_impl(flexar_comm* c, bool agree) {
   } else {
     grave_keep(c->device, c->stg, c->ws_bytes, c->rank);
     grave_keep(c->device, c->flags, kFlagWords * sizeof(uint64_t), c->rank);
-    if (agree && c->hb) {
-      set_error("destroy: " + why + "; this rank's workspace stays allocated until the process exits");
+    if (agree) {  // a collective close that parks memory says so
+      set_error("destroy: " + why + "; this rank's workspace (" + std::to_string(c->ws_bytes) +
+                " bytes) stays allocated until the process exits");
       logf(LOG_WARN, c->rank, "destroy: %s; keeping this rank's exported workspace allocated", why.c_str());
-      rc = FLEXAR_ERR_TIMEOUT;
+      rc = c->hb || use_ext ? FLEXAR_ERR_TIMEOUT : FLEXAR_ERR_STATE;
     }
   }
   if (c->hb) c->hb->unlink();  // every rank joined long before (connect): the name is no longer needed
@@ -801,6 +814,13 @@ static int destroy_impl(flexar_comm* c, bool agree) {
 extern "C" {
 
 int flexar_comm_destroy(flexar_comm_t c) { return c ? destroy_impl(c, true) : 0; }
+int flexar_comm_destroy_agreed(flexar_comm_t c, int (*agree)(void*), void* ctx) {
+  return c ? destroy_impl(c, true, agree, ctx) : 0;
+}
+uint64_t flexar_parked_bytes(void) {
+  std::lock_guard<std::mutex> lk(g_grave_mu);
+  return g_grave_bytes;
+}
 
 // Host-side agreement of this communicator's ranks (collective: every rank, same order): the maximum
 // (op 0) or the bitwise OR (op 1) of one 64-bit value over the ranks, through the teardown page
@@ -839,7 +859,8 @@ int flexar_comm_host_page_check(flexar_comm_t c, int* shared) {
     return 0;
   }
   logf(LOG_WARN, c->rank, "host page not shared: rank %d's mark is missing from %s (a private /dev/shm?): teardown "
-       "falls back to deferred frees and host agreements to the bootstrap", missing, c->hb->name().c_str());
+       "needs the caller's agreement (flexar_comm_destroy_agreed; otherwise the workspace stays allocated) and "
+       "host agreements go to the bootstrap", missing, c->hb->name().c_str());
   c->hb->unlink();
   c->hb.reset();
   c->hb_shared = 0;

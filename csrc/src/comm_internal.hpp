@@ -285,6 +285,8 @@ struct flexar_comm {
   int next_reg = 1;
   std::map<std::string, std::pair<char*, int>> ipc_maps;  // (peer, handle) -> mapped base, references
   bool zc_auto = true;  // FLEXAR_ZC_AUTO=0: automatic choices never switch to zero copy
+  AlgoSpec last_spec;     // the schedule the last allreduce ran (after the zero-copy decision)
+  bool have_last_spec = false;
   int* st_buf = nullptr;        // self-test buffers (device)
   uint32_t* st_bad = nullptr;   // self-test mismatch counter (host-mapped)
   uint32_t* st_bad_dev = nullptr;

@@ -157,6 +157,43 @@ void on_terminate() {
   std::abort();
 }
 
+// A per-thread alternate signal stack: the handlers are installed with SA_ONSTACK, and a
+// SIGSEGV from a stack overflow cannot run on the stack that overflowed. The installing thread gets one in
+// crash_report_install and every thread that records a breadcrumb (every thread that launches flexar work)
+// lazily in crumb(); a thread that already has one (Python's faulthandler, a sanitizer) keeps it. Freed at
+// thread exit. 64 KiB: the report needs a few hundred bytes of frames plus its 512-byte line buffer.
+struct AltStack {
+  void* mem = nullptr;
+  ~AltStack() {
+    if (!mem) return;
+    stack_t cur;
+    if (sigaltstack(nullptr, &cur) == 0 && cur.ss_sp == mem) {
+      stack_t off;
+      memset(&off, 0, sizeof(off));
+      off.ss_flags = SS_DISABLE;
+      sigaltstack(&off, nullptr);
+    }
+    free(mem);
+  }
+};
+void ensure_altstack() {
+  static thread_local bool done = false;
+  static thread_local AltStack mine;
+  if (done) return;
+  done = true;
+  stack_t cur;
+  if (sigaltstack(nullptr, &cur) == 0 && !(cur.ss_flags & SS_DISABLE)) return;  // the thread has one already
+  constexpr size_t kAltStackBytes = 64 * 1024;
+  void* m = malloc(kAltStackBytes);
+  if (!m) return;
+  stack_t ss;
+  memset(&ss, 0, sizeof(ss));
+  ss.ss_sp = m;
+  ss.ss_size = kAltStackBytes;
+  if (sigaltstack(&ss, nullptr) == 0) mine.mem = m;
+  else free(m);
+}
+
 }  // namespace
 
 bool crumbs_on() {
@@ -169,6 +206,7 @@ bool crumbs_on() {
 
 void crumb(const CrumbArgs& a) {
   if (!crumbs_on()) return;  // FLEXAR_CRASH_REPORT=0: no ring, no report
+  if (g_installed.load(std::memory_order_relaxed)) ensure_altstack();
   const uint64_t s = g_next.fetch_add(1, std::memory_order_relaxed);
   Crumb& c = g_ring[s & (kCrumbs - 1)];
   c.seq.store(0, std::memory_order_relaxed);
@@ -205,15 +243,20 @@ void crumb_phase(const char* what, const char* label, int rank, int nranks) {
   crumb(a);
 }
 
+// A slot is claimed with a sentinel first (a concurrent registration cannot claim it too), then filled, then
+// published with a release store - the report (which skips the sentinel) never pairs one communicator's
+// progress words with another's rank / device.
+static const volatile uint64_t kClaimed[2] = {0, 0};
 int crumb_register_comm(int rank, int nranks, int device, const volatile uint64_t* progress) {
   for (int i = 0; i < kMaxLiveComms; ++i) {
     const volatile uint64_t* expected = nullptr;
-    if (g_live[i].progress.load(std::memory_order_relaxed) == nullptr) {
-      g_live[i].rank = rank;
-      g_live[i].nranks = nranks;
-      g_live[i].device = device;
-      if (g_live[i].progress.compare_exchange_strong(expected, progress)) return i;
-    }
+    if (g_live[i].progress.load(std::memory_order_relaxed) != nullptr) continue;
+    if (!g_live[i].progress.compare_exchange_strong(expected, kClaimed, std::memory_order_acquire)) continue;
+    g_live[i].rank = rank;
+    g_live[i].nranks = nranks;
+    g_live[i].device = device;
+    g_live[i].progress.store(progress, std::memory_order_release);
+    return i;
   }
   return -1;
 }
@@ -229,7 +272,7 @@ void crash_report_write(const char* why) {
   // device progress of every live communicator (host-mapped words written by executor workgroup 0)
   for (int i = 0; i < kMaxLiveComms; ++i) {
     const volatile uint64_t* p = g_live[i].progress.load(std::memory_order_acquire);
-    if (!p) continue;
+    if (!p || p == kClaimed) continue;
     o.s("[flexar crash report]   communicator rank ").i(g_live[i].rank).s("/").i(g_live[i].nranks).s(" device ")
         .i(g_live[i].device).s(": executor workgroup 0 started epoch ").u(p[0]).s(", finished epoch ").u(p[1])
         .s("\n");
@@ -265,6 +308,7 @@ void crash_report_install() {
   int expected = 0;
   if (!g_installed.compare_exchange_strong(expected, 1)) return;
   if (!crumbs_on()) return;
+  ensure_altstack();
   for (int sig : kSignals) {
     struct sigaction sa;
     memset(&sa, 0, sizeof(sa));
@@ -307,8 +351,16 @@ void flexar_crash_report_install(void) { flexar::crash_report_install(); }
 void flexar_crash_report_dump(const char* why) { flexar::crash_report_write(why ? why : "explicit dump"); }
 
 // Tests only: end the process the way an uncaught C++ exception (kind 0: std::terminate) or abort() (1) does.
+// kind 2: a stack overflow by unbounded recursion (the SIGSEGV then arrives on an exhausted stack).
+static int overflow_stack(volatile int depth) {
+  volatile char pad[4096];
+  pad[0] = (char)depth;
+  pad[sizeof(pad) - 1] = (char)(depth >> 8);
+  return overflow_stack(depth + 1) + pad[0] + pad[sizeof(pad) - 1];  // not a tail call
+}
 void flexar_test_fatal(int kind) {
   if (kind == 0) std::terminate();
+  if (kind == 2) (void)overflow_stack(0);
   std::abort();
 }
 

@@ -44,6 +44,8 @@ void crumb_phase(const char* what, const char* label, int rank = -1, int nranks 
 int crumb_register_comm(int rank, int nranks, int device, const volatile uint64_t* progress);
 void crumb_unregister_comm(int slot);
 
+// FLEXAR_CRASH_REPORT unset or non-zero: breadcrumbs, launch progress words and the report are on.
+bool crumbs_on();
 // Installs the fatal-signal and terminate handlers once per process (FLEXAR_CRASH_REPORT=0: never).
 void crash_report_install();
 // Writes the report to fd 2 now (tests, explicit dumps); `why` is printed in the header.

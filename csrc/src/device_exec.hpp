@@ -1740,17 +1740,33 @@ __global__ void __launch_bounds__(kExecThreads) exec_kernel(DevCtx c) {
 #ifndef FLEXAR_TYPED_OCC3
 #define FLEXAR_TYPED_OCC3 0
 #endif
+// FLEXAR_TYPED_THREADS (build knob): workgroup size of the typed kernels. At 512 threads (8 waves,
+// 2 per SIMD) a second workgroup shares a CU only at <= 128 VGPRs, and the typed kernels use 155-230; at 256 (4 waves,
+// 1 per SIMD) two fit at <= 256 VGPRs and three at <= 168. The launch multiplies the grid by the workgroups per CU
+// it targets (typed_grid_mul: 3 for the narrow fan-in class, 2 otherwise; flags and epochs are per workgroup,
+// kMaxGridBlocks caps it, co-residency holds by the same factor); every rank runs the same build.
+#ifndef FLEXAR_TYPED_THREADS
+#define FLEXAR_TYPED_THREADS 512
+#endif
+constexpr int kTypedThreads = FLEXAR_TYPED_THREADS;
+static_assert(kTypedThreads == 256 || kTypedThreads == 512, "FLEXAR_TYPED_THREADS: 256 or 512");
+template <int KMAX>
+constexpr int typed_grid_mul() {
+  return kTypedThreads == 256 ? (KMAX <= 4 ? 3 : 2) : 1;
+}
 template <typename W, int KMAX>
 constexpr int typed_min_waves() {
+  // 256-thread workgroups: three per CU for the narrow fan-in class (<= 168 VGPRs), two otherwise (<= 256)
+  if (kTypedThreads == 256) return KMAX <= 4 ? 3 : 2;
   return FLEXAR_TYPED_OCC3 && KMAX <= 4 && sizeof(W) == 1 && !IsMx<W>::value ? 3 : 1;
 }
 template <typename T, typename W, int PM, int KMAX = kMaxSrc>
-__global__ void __launch_bounds__(kExecThreads) __attribute__((amdgpu_waves_per_eu(typed_min_waves<W, KMAX>())))
+__global__ void __launch_bounds__(kTypedThreads) __attribute__((amdgpu_waves_per_eu(typed_min_waves<W, KMAX>())))
 exec_mx_kernel(DevCtx c) {
   exec_body<T, OpSum, PM, W, KMAX>(c, blockIdx.x, gridDim.x);
 }
 template <typename T, typename W, int PM, int KMAX = kMaxSrc>
-__global__ void __launch_bounds__(kExecThreads) __attribute__((amdgpu_waves_per_eu(typed_min_waves<W, KMAX>())))
+__global__ void __launch_bounds__(kTypedThreads) __attribute__((amdgpu_waves_per_eu(typed_min_waves<W, KMAX>())))
 exec_mx_group_kernel(const DevCtx* ctxs, uint32_t grid_per_rank) {
   const uint32_t r = blockIdx.x / grid_per_rank;
   exec_body<T, OpSum, PM, W, KMAX>(ctxs[r], blockIdx.x % grid_per_rank, grid_per_rank);

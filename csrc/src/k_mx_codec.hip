@@ -126,6 +126,18 @@ __global__ void __launch_bounds__(kMxcThreads) mx_pack16_kernel(const T* __restr
         }
         __builtin_memcpy(&q[i], &r, 4);
       }
+      // NaN inputs: the scaled converts write the NaN byte with the sign set whatever the input's sign; the element
+      // store (and ops.quant.mx_quantize) keep the sign: 0x7f | sign. Only blocks holding a NaN take this branch.
+      if (am > 0x7f800000u) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const uint32_t b = mxc_f32_bits<T>(w, e);
+          if ((b & 0x7fffffffu) > 0x7f800000u) {
+            const uint32_t sh = 8 * (e & 3);
+            q[e / 4] = (q[e / 4] & ~(0xffu << sh)) | ((0x7fu | ((b >> 24) & 0x80u)) << sh);
+          }
+        }
+      }
       if (e0 < nwhole) {
         if constexpr (E == 4) {
           *(uint32_t*)(msg + e0) = q[0];  // 4 B per lane, 256 B contiguous across the wave

@@ -1,6 +1,7 @@
 // Instantiation helper included by each k_<dtype>.hip.
 #pragma once
 
+#include <atomic>
 #include <string>
 
 #include "internal.hpp"
@@ -9,9 +10,9 @@
 namespace flexar {
 
 template <typename K>
-inline int query_kernel(K kern, const LaunchArgs& a) {
+inline int query_kernel(K kern, const LaunchArgs& a, int threads = kExecThreads) {
   int occ = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kExecThreads, 0) != hipSuccess) {
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, threads, 0) != hipSuccess) {
     (void)hipGetLastError();
     set_error("occupancy query failed");
     return FLEXAR_ERR_HIP;
@@ -119,25 +120,58 @@ inline int launch_int(int op, const LaunchArgs& a) {
 
 namespace flexar {
 
+// Workgroups of `kern` (at `threads`) the current device keeps resident at once, cached per kernel and device.
+template <typename K>
+inline int resident_blocks(K kern, int threads, std::atomic<int>* cache) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) { (void)hipGetLastError(); return 0; }
+  int v = cache[dev].load(std::memory_order_relaxed);
+  if (v > 0) return v;
+  int occ = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, threads, 0) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  v = occ * cus;
+  cache[dev].store(v, std::memory_order_relaxed);
+  return v;
+}
+
 // Typed-program executor launch (exec_mx_kernel<T, W, PM, KMAX>); "+nts" runs the fence protocol.
 template <typename T, typename W, int KMAX>
 inline int launch_typed_k(const LaunchArgs& a) {
   const bool wt = a.proto == PM_WT;
   if (a.kind != LAUNCH_QUERY) clear_stale_error();
+  // FLEXAR_TYPED_THREADS = 256: 2-3 times the workgroups of half the size (a multiple of the channel count still),
+  // never more than the device keeps resident (every workgroup waits on its peers' workgroup of the same index)
+  int g = a.grid;
+  if (typed_grid_mul<KMAX>() > 1 && a.kind != LAUNCH_QUERY) {
+    static std::atomic<int> res_cache[2][2][16];  // [group][wt][device]
+    const int ranks = a.kind == LAUNCH_GROUP ? a.nranks : 1;
+    const int res = a.kind == LAUNCH_GROUP
+                        ? resident_blocks(wt ? exec_mx_group_kernel<T, W, PM_WT, KMAX> : exec_mx_group_kernel<T, W, PM_FENCE, KMAX>,
+                                          kTypedThreads, res_cache[0][wt])
+                        : resident_blocks(wt ? exec_mx_kernel<T, W, PM_WT, KMAX> : exec_mx_kernel<T, W, PM_FENCE, KMAX>,
+                                          kTypedThreads, res_cache[1][wt]);
+    for (int m = typed_grid_mul<KMAX>(); m > 1; --m)
+      if (a.grid * m <= (int)kMaxGridBlocks && a.grid * m * ranks <= res) { g = a.grid * m; break; }
+  }
   switch (a.kind) {
     case LAUNCH_QUERY:
-      return query_kernel(wt ? exec_mx_kernel<T, W, PM_WT, KMAX> : exec_mx_kernel<T, W, PM_FENCE, KMAX>, a);
+      return query_kernel(wt ? exec_mx_kernel<T, W, PM_WT, KMAX> : exec_mx_kernel<T, W, PM_FENCE, KMAX>, a,
+                          kTypedThreads);
     case LAUNCH_EXEC:
-      if (wt) hipLaunchKernelGGL((exec_mx_kernel<T, W, PM_WT, KMAX>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
-      else hipLaunchKernelGGL((exec_mx_kernel<T, W, PM_FENCE, KMAX>), dim3(a.grid), dim3(kExecThreads), 0, a.stream, a.ctx);
+      if (wt) hipLaunchKernelGGL((exec_mx_kernel<T, W, PM_WT, KMAX>), dim3(g), dim3(kTypedThreads), 0, a.stream, a.ctx);
+      else hipLaunchKernelGGL((exec_mx_kernel<T, W, PM_FENCE, KMAX>), dim3(g), dim3(kTypedThreads), 0, a.stream, a.ctx);
       break;
     case LAUNCH_GROUP:
       if (wt)
-        hipLaunchKernelGGL((exec_mx_group_kernel<T, W, PM_WT, KMAX>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
-                           a.stream, a.d_ctxs, (uint32_t)a.grid);
+        hipLaunchKernelGGL((exec_mx_group_kernel<T, W, PM_WT, KMAX>), dim3(g * a.nranks), dim3(kTypedThreads), 0,
+                           a.stream, a.d_ctxs, (uint32_t)g);
       else
-        hipLaunchKernelGGL((exec_mx_group_kernel<T, W, PM_FENCE, KMAX>), dim3(a.grid * a.nranks), dim3(kExecThreads), 0,
-                           a.stream, a.d_ctxs, (uint32_t)a.grid);
+        hipLaunchKernelGGL((exec_mx_group_kernel<T, W, PM_FENCE, KMAX>), dim3(g * a.nranks), dim3(kTypedThreads), 0,
+                           a.stream, a.d_ctxs, (uint32_t)g);
       break;
     default:
       return FLEXAR_ERR_INVALID;

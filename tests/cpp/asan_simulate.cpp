@@ -16,10 +16,13 @@ int main() {
   int fails = 0, runs = 0;
   std::mt19937 rng(7);
   for (int n : {2, 3, 4, 5, 6, 7, 8, 12}) {
-    std::vector<std::string> specs = {"flat", "ring", "ring:2", "oneshot", "flat+push", "flat+nofuse"};
-    for (auto& p : flexar::enumerate_plans(n))
-      if (p.kind == flexar::AlgoKind::TREE) specs.push_back(p.str() + "+push"), specs.push_back(p.str() + "+pull");
-    for (auto& spec : specs) {
+    std::vector<std::pair<std::string, int>> specs = {{"flat", 1}, {"ring", 1}, {"ring:2", 2}, {"oneshot", 1},
+                                                      {"flat+push", 1}, {"flat+nofuse", 1}};
+    for (auto& p : flexar::enumerate_plans(n))  // trees, multi-channel ones included ("tree:2,2,2:7")
+      if (p.kind == flexar::AlgoKind::TREE)
+        specs.push_back({p.str() + "+push", p.channels}), specs.push_back({p.str() + "+pull", p.channels});
+    for (auto& sc : specs) {
+      const std::string& spec = sc.first;
       for (size_t count : {1ul, 7ul, 1000ul, 4099ul}) {
         std::vector<std::vector<float>> in(n, std::vector<float>(count)), out(n, std::vector<float>(count));
         std::vector<double> ref(count, 0.0);
@@ -31,7 +34,7 @@ int main() {
         std::vector<const void*> ip(n);
         std::vector<void*> op(n);
         for (int r = 0; r < n; ++r) ip[r] = in[r].data(), op[r] = out[r].data();
-        int grid = spec.rfind("ring:2", 0) == 0 ? 4 : 3;
+        int grid = sc.second > 1 ? 2 * sc.second : 3;  // whole channels
         int rc = flexar_simulate(spec.c_str(), n, count, FLEXAR_FLOAT32, FLEXAR_SUM, ip.data(), op.data(), grid, 2, 0,
                                  1.0f);
         ++runs;

@@ -57,6 +57,20 @@ int main(int argc, char** argv) {
   MPI_Comm_rank(MPI_COMM_WORLD, &g_rank);
   MPI_Comm_size(MPI_COMM_WORLD, &size);
   bool quick = argc > 1 && !strcmp(argv[1], "--quick");
+  {  // zero-copy policy of the MPI entry points (mpi_mod.hpp zc_mode_of): registration by default for device
+     // buffers, never when the user named a spec without "+zc", always when it names "+zc"
+    using flexar::mpi::ZcMode;
+    using flexar::mpi::zc_mode_of;
+    const bool ok = zc_mode_of(nullptr, nullptr) == ZcMode::AUTO && zc_mode_of("auto", nullptr) == ZcMode::AUTO &&
+                    zc_mode_of("", "1") == ZcMode::AUTO && zc_mode_of("flat", nullptr) == ZcMode::OFF &&
+                    zc_mode_of("rhd:7+pull", nullptr) == ZcMode::OFF && zc_mode_of(nullptr, "0") == ZcMode::OFF &&
+                    zc_mode_of(nullptr, nullptr, "0") == ZcMode::OFF && zc_mode_of("flat+zc", "0") == ZcMode::FORCE &&
+                    zc_mode_of("flat+zc+push", nullptr) == ZcMode::FORCE;
+    if (!ok) {
+      ++g_fail;
+      fprintf(stderr, "rank %d: zc_mode_of policy mismatch\n", g_rank);
+    }
+  }
   std::vector<std::string> algos = {"flat", "ring", "oneshot", "ring:2"};
   for (auto& p : flexar::enumerate_plans(size))
     if (p.kind == flexar::AlgoKind::TREE) algos.push_back(p.str());

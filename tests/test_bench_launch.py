@@ -161,3 +161,13 @@ def test_selftest_retry_policy_per_gpu_vs_shared():
     env = {}
     bench.configure_env(8, 3, 3, env)
     assert "FLEXAR_SELFTEST_RETRY" not in env
+
+
+def test_rehearsal_does_not_report_a_same_node_ratio():
+    """with RCCL over loopback sockets (the shared-GPU rehearsal) vs_rccl is null and the RCCL
+    figure is labelled loopback; on one GPU per rank both fields are the same-node bar."""
+    f = bench.rccl_fields(450.0, 2.25, shared_rccl=True)
+    assert f == {"rccl_busbw_GBps": None, "rccl_busbw_GBps_loopback": 2.25, "vs_rccl": None}
+    f = bench.rccl_fields(300.0, 250.0, shared_rccl=False)
+    assert f == {"rccl_busbw_GBps": 250.0, "vs_rccl": 1.2}
+    assert bench.rccl_fields(300.0, None, shared_rccl=False)["vs_rccl"] is None

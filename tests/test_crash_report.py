@@ -6,7 +6,8 @@ counterpart is glog's InstallFailureSignalHandler (allreduce_over_mpi/benchmark.
 process records a phase, attempts a reduction-kernel launch (no GPU on this host: the launch itself fails,
 after its breadcrumb), records another phase and then dies by SIGABRT, SIGSEGV or std::terminate; its
 stderr must carry the report with the launch and the last phase, and the process must still die by the
-original signal (the handler chains).
+original signal (the handler chains). A stack overflow too: the handler runs on a
+per-thread alternate signal stack, so the report still comes out of a thread whose own stack is exhausted.
 """
 import os
 import signal
@@ -32,6 +33,8 @@ CHILD = textwrap.dedent("""
         os.abort()
     elif how == "segv":
         ctypes.string_at(0)
+    elif how == "overflow":
+        l.flexar_test_fatal(2)  # unbounded native recursion: the SIGSEGV arrives on an exhausted stack
     else:
         l.flexar_test_fatal(0)
 """)
@@ -45,7 +48,8 @@ def _run(how, env_extra=None):
                           text=True, timeout=180)
 
 
-@pytest.mark.parametrize("how,sig", [("abort", signal.SIGABRT), ("segv", signal.SIGSEGV), ("terminate", signal.SIGABRT)])
+@pytest.mark.parametrize("how,sig", [("abort", signal.SIGABRT), ("segv", signal.SIGSEGV), ("terminate", signal.SIGABRT),
+                                     ("overflow", signal.SIGSEGV)])
 def test_fatal_report_names_the_last_launch(how, sig):
     r = _run(how)
     assert r.returncode == -sig, (r.returncode, r.stderr[-2000:])

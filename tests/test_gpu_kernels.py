@@ -186,6 +186,32 @@ def test_group_allreduce_all_algorithms_f32(cuda, groups, n):
     grp.check()
 
 
+@pytest.mark.parametrize("n,spec", [(4, "rhd:3+pull"), (4, "rhd:3+push"), (8, "rhd:7+pull"), (8, "rhd:7+push"),
+                                    (8, "rhd:7+pull+nts"), (8, "rhd:7+pull+wt"), (8, "tree:4,2:7+pull"),
+                                    (8, "tree:2,4:7+push+nofuse"), (8, "rhd:3+pull")])
+def test_group_channelled_trees_bit_exact(cuda, groups, n, spec):
+    """Link-balanced multi-channel trees (planner.hpp build_tree_channels): integer-valued fp32 inputs make every
+    partial sum exact, so the device result must EQUAL the fp64 reference - out of place and in place, over
+    three consecutive calls (both staging parities), sizes with uneven channel and block tails."""
+    grp = groups[n]
+    for size in (1, 7, 4099, 65539, (3 << 20) + 17):
+        g = torch.Generator(device=cuda).manual_seed(size * 7 + n)
+        xs = [torch.randint(-1000, 1000, (size,), device=cuda, generator=g).float() for _ in range(n)]
+        ref = torch.stack([x.double() for x in xs]).sum(0)
+        for in_place in (False, True):
+            ins = [x.clone() for x in xs]
+            outs = None if in_place else [torch.empty_like(x) for x in xs]
+            for call in range(3):
+                if in_place:
+                    for i, x in zip(ins, xs):
+                        i.copy_(x)
+                res = grp.all_reduce(ins, "sum", outs=outs, algo=spec)
+                torch.cuda.synchronize()
+                for r, o in enumerate(res):
+                    assert torch.equal(o.double(), ref), f"{spec} size={size} rank={r} in_place={in_place} call={call}"
+    grp.check()
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.int32, torch.float64])
 def test_group_allreduce_dtypes(cuda, groups, dtype):
     n = 8
@@ -222,7 +248,8 @@ def _ulps(a: torch.Tensor, b: torch.Tensor) -> int:
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float8_e4m3fn])
-@pytest.mark.parametrize("spec", ["ring", "ring:4", "ring:7", "rhd", "tree:2,4", "tree:4,2+push", "tree:2,2,2+pull"])
+@pytest.mark.parametrize("spec", ["ring", "ring:4", "ring:7", "rhd", "tree:2,4", "tree:4,2+push", "tree:2,2,2+pull",
+                                  "rhd:7+pull", "tree:4,2:7+push"])
 def test_group_typed_fp32_partials(cuda, groups, dtype, spec):
     """Multi-hop schedules of 16/8-bit inputs keep partial sums in fp32 staging (exec_mx_kernel with fp32
     wire operands): the device result is within 1 ulp of the exact sum rounded once, i.e. flat's result,

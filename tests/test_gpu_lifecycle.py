@@ -89,9 +89,12 @@ def _worker(rank, world, port, mode, q):
             if rank == world - 1:
                 comm.close(collective=False)  # never reaches the agreement
             else:
+                from allreduce_over_mpi_amd import _native as nv
+
                 t0 = time.monotonic()
                 comm.close()
                 out["close_s"] = time.monotonic() - t0
+                out["parked"] = int(nv.lib().flexar_parked_bytes())
             dist.barrier()
         elif mode == "private":
             comm = Communicator(workspace_bytes=64 << 20)
@@ -100,8 +103,15 @@ def _worker(rank, world, port, mode, q):
             out["err"] = _exact(comm, rank, world, 1 << 18)
             comm.check()
             t0 = time.monotonic()
-            comm.close()  # no page: no agreement to wait out; the exported buffers are parked
+            comm.close()  # no page: the two teardown agreements run over the bootstrap exchange
             out["close_s"] = time.monotonic() - t0
+            for _ in range(2):  # and again: nothing is ever parked
+                c2 = Communicator(workspace_bytes=64 << 20)
+                out["err"] = max(out["err"], _exact(c2, rank, world, 1 << 16))
+                c2.close()
+            from allreduce_over_mpi_amd import _native as nv
+
+            out["parked"] = int(nv.lib().flexar_parked_bytes())
         elif mode in ("hiperr", "retry"):
             comm = Communicator(workspace_bytes=64 << 20)
             out["failed"] = list(comm.selftest_failed)
@@ -160,6 +170,7 @@ def test_close_with_an_absent_peer_times_out_named(cuda):
     out, _ = _run(2, "absent")
     assert out[0]["err"] == 0.0 and out[1]["err"] == 0.0
     assert 1.5 < out[0]["close_s"] < 15.0, out[0]
+    assert out[0]["parked"] >= 64 << 20, out[0]  # the timed-out close parks (and says so: a warning)
 
 
 def test_private_host_page_is_detected_at_connect(cuda):
@@ -172,6 +183,7 @@ def test_private_host_page_is_detected_at_connect(cuda):
         assert o["page"][0] is False and o["page"][1] is False, (r, o)
         assert o["err"] == 0.0, (r, o)
         assert o["close_s"] < 4.0, (r, o)
+        assert o["parked"] == 0, (r, o)  # the workspace is freed, not parked for the process's life
     assert "host page not shared" in (out[0]["page"][2] or ""), out[0]
 
 

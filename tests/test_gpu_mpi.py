@@ -48,6 +48,34 @@ def test_mpi_zero_copy_sweep_reregisters(tools):
     assert r.returncode == 0 and "check n=65539: ok" in r.stdout, r.stdout[-3000:]
 
 
+def test_mpi_zero_copy_by_default(tools):
+    """with no FLEXAR_ALGO, MPI_Allreduce_FT on device buffers of at least 1 MiB registers them
+    collectively (mpi_mod.hpp zc_prepare) and the cost model's flat choice runs zero copy ("+zc+push"); below
+    1 MiB, or with FLEXAR_MPI_ZC=0, or with a named spec, it runs staging. Results exact every time."""
+    r = _mpirun(2, [tools["flexar_bench"], "--mem", "device", "--size", "4M", "--repeat", "5", "--check"])
+    assert r.returncode == 0 and "check n=4194304: ok" in r.stdout, r.stdout[-3000:]
+    sched = [ln for ln in r.stdout.splitlines() if ln.startswith("schedule n=4194304")]
+    assert sched and "+zc" in sched[-1], r.stdout[-3000:]
+    r = _mpirun(2, [tools["flexar_bench"], "--mem", "device", "--size", "4099", "--repeat", "3", "--check"])
+    assert r.returncode == 0 and "check n=4099: ok" in r.stdout and "+zc" not in r.stdout, r.stdout[-3000:]
+    for env, args in (({"FLEXAR_MPI_ZC": "0"}, []), ({}, ["--algo", "flat+pull"])):
+        r = _mpirun(2, [tools["flexar_bench"], "--mem", "device", "--size", "4M", "--repeat", "3", "--check"] + args,
+                    env=env)
+        sched = [ln for ln in r.stdout.splitlines() if ln.startswith("schedule n=4194304")]
+        assert r.returncode == 0 and sched and "+zc" not in sched[-1], (env, args, r.stdout[-3000:])
+
+
+def test_mpi_zero_copy_default_fresh_buffers(tools):
+    """The default registration with a fresh hipMalloc per sweep size (often a freed buffer's address): the
+    per-call agreement catches stale registrations and re-registers; every size exact; bf16 too."""
+    r = _mpirun(2, [tools["flexar_bench"], "--mem", "device", "--sweep", "256K:16M", "--repeat", "3", "--check"])
+    assert r.returncode == 0 and r.stdout.count(": ok") >= 7, r.stdout[-3000:]
+    # --sweep takes bytes: 2 MiB .. 16 MiB run zero copy (1 MiB and below: the selector picks LL)
+    assert sum("+zc" in ln for ln in r.stdout.splitlines() if ln.startswith("schedule")) >= 4, r.stdout[-3000:]
+    r = _mpirun(2, [tools["flexar_bench"], "--mem", "device", "--dtype", "bfloat16", "--size", "2M", "--check"])
+    assert r.returncode == 0 and "check n=2097152: ok" in r.stdout, r.stdout[-3000:]
+
+
 def test_mpi_device_buffers_host_staging(tools):
     """Ranks on 'different nodes' (virtual nodes of 1 rank): whole buffer staged through host p2p."""
     r = _mpirun(2, [tools["flexar_bench"], "--mem", "device", "--size", "65537", "--repeat", "3", "--check"],

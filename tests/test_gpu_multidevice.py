@@ -56,9 +56,10 @@ def _specs(world):
     if full > max(4, chans):
         specs.append(f"ring:{full}")
     if world == 4:
-        specs += ["tree:2,2+push", "tree:2,2+pull", "tree:2,2+push+wt", "rhd+rccl"]
+        specs += ["tree:2,2+push", "tree:2,2+pull", "tree:2,2+push+wt", "rhd+rccl", "rhd:3+pull", "rhd:3+push"]
     if world == 8:
-        specs += ["tree:2,4+push", "tree:2,4+pull", "tree:4,2+push", "tree:4,2+pull", "rhd", "rhd+rccl"]
+        specs += ["tree:2,4+push", "tree:2,4+pull", "tree:4,2+push", "tree:4,2+pull", "rhd", "rhd+rccl",
+                  "rhd:7+pull", "rhd:7+push", "tree:4,2:7+pull", "tree:2,4:7+push+nts"]
     if world in (3, 6):
         specs += [f"tree:{a},{b}+pull" for a, b in ((2, world // 2),) if a * b == world]
     assert all(nv.model_cost_us(s.replace("+rccl", ""), world, 1e6) > 0 for s in specs)
@@ -68,7 +69,7 @@ def _specs(world):
 def _typed_specs(world):
     out = ["ring+f32", "ring+rw"]
     if world >= 4 and not world & (world - 1):
-        out += ["rhd+pull+f32", "rhd+pull+rw"]
+        out += ["rhd+pull+f32", "rhd+pull+rw", f"rhd:{world - 1}+pull+f32", f"rhd:{world - 1}+pull+rw"]
     if world == 8:
         out += ["tree:4,2+pull+f32", "tree:4,2+pull+rw"]
     return out

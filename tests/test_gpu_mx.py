@@ -166,3 +166,31 @@ def test_mx_codec_matches_reference(cuda, wire, dtype):
         buf[3:3 + 3 * mb] = msgs.reshape(-1)
         got = mx_unpack_sum(buf[3:3 + 3 * mb].view(3, mb), n, wire).cpu()  # base 3 B past an allocation
         assert torch.equal(got, want_sum), n
+
+
+@pytest.mark.parametrize("wire", ["e4m3", "e5m2"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_mx_codec_non_finite_matches_reference(cuda, wire, dtype):
+    """the pack's scaled converts (v_cvt_scalef32_pk_*) against ops.quant.mx_quantize on blocks holding
+    +Inf, -Inf and NaN - whole blocks and the partial tail block - byte for byte (values and scale bytes), and
+    unpack_sum against mx_dequantize of the same bytes (NaN positions compared as NaN)."""
+    from allreduce_over_mpi_amd.ops.quant import mx_dequantize, mx_pack, mx_quantize, mx_unpack_sum
+
+    for n in (96, 100, 4096 + 17):
+        x = torch.randn(n, generator=torch.Generator().manual_seed(n)) * 3.0
+        x[5] = float("inf")              # block 0: +Inf among finite values
+        x[40] = float("-inf")            # block 1: -Inf
+        x[70] = float("nan")             # block 2: NaN
+        x[n - 2] = float("nan")          # the tail block (n = 100, 4113) or the last whole one
+        x[n - 1] = float("inf")
+        x = x.to(dtype)
+        msg = mx_pack(x.cuda(), wire).cpu()
+        q, sb = mx_quantize(x.float(), wire)
+        want = torch.cat([q.view(torch.uint8), sb.to(torch.uint8)])
+        diff = (msg != want).nonzero().flatten().tolist()
+        assert not diff, (n, [(i, int(msg[i]), int(want[i])) for i in diff[:8]])
+        got = mx_unpack_sum(msg.cuda().unsqueeze(0), n, wire).cpu()
+        ref = mx_dequantize(q, sb, n)
+        assert torch.equal(torch.isnan(got), torch.isnan(ref)), n
+        fin = ~torch.isnan(ref)
+        assert torch.equal(got[fin], ref[fin]), n

@@ -30,7 +30,7 @@ def _trees(n):
 
 @pytest.mark.parametrize("n", [2, 4, 6, 8, 12, 16])
 def test_every_tree_moves_the_bandwidth_optimal_bytes(n):
-    S = n * 4096 * 4  # divisible into aligned blocks: no tail rounding
+    S = n * (n - 1) * 4096 * 4  # divisible into aligned channel slices and blocks: no tail rounding
     for spec in _trees(n):
         widths = [int(w) for w in spec.split(":")[1].split(",")]
         prod = 1

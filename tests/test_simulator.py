@@ -21,6 +21,14 @@ def topologies(n):
     return sorted(set(out))
 
 
+def channels_of(spec):
+    """C of "ring:C" / "tree:a,b:C" / "rhd:C" (1 otherwise)."""
+    head = spec.split("+")[0]
+    if head.startswith("ring:") or head.startswith("rhd:"):
+        return int(head.split(":")[1])
+    return int(head.split(":")[2]) if head.startswith("tree:") and head.count(":") == 2 else 1
+
+
 def ref_sum(ins):
     return np.sum(np.stack(ins).astype(np.float64), 0)
 
@@ -29,7 +37,7 @@ def ref_sum(ins):
 def test_all_topologies_f32(nv, n):
     rng = np.random.default_rng(n)
     for spec in topologies(n):
-        chans = int(spec.split(":")[1].split("+")[0]) if spec.startswith("ring:") else 1
+        chans = channels_of(spec)
         for size in SIZES:
             ins = [rng.standard_normal(size).astype(np.float32) for _ in range(n)]
             for in_place in (False, True):

@@ -52,8 +52,10 @@ def test_enumerate_plans(nv):
     p8 = nv.enumerate_plans(8)
     assert "tree:8" in p8 and "tree:2,2,2" in p8 and "tree:2,4" in p8 and "tree:4,2" in p8
     assert "ring" in p8 and "ring:4" in p8 and "oneshot" in p8 and "ll" in p8
-    trees = [p for p in p8 if p.startswith("tree:")]
+    trees = [p for p in p8 if p.startswith("tree:") and p.count(":") == 1]
     assert len(trees) == nv.count_factorizations(8)
+    # every multi-stage tree again on N - 1 link-balanced channels (planner.hpp build_tree_channels)
+    assert sorted(p for p in p8 if p.count(":") == 2) == ["tree:2,2,2:7", "tree:2,4:7", "tree:4,2:7"]
     p7 = nv.enumerate_plans(7)  # prime: flat tree + rings
     assert "tree:7" in p7 and "ring:6" in p7
     assert nv.enumerate_plans(1) == []
@@ -135,9 +137,13 @@ def test_plans_move_bandwidth_optimal_bytes(nv, n):
     count = 16384 * n  # large enough that 16-element block rounding stays < 1 % (ring:7 splits 7 ways)
     specs = [p for p in nv.enumerate_plans(n) if p.startswith(("tree:", "ring"))]
     specs = [s for s in specs if not s.startswith("tree:") or
-             __import__("math").prod(int(w) for w in s[5:].split(",")) == n]  # lonely trees fold extra data
+             __import__("math").prod(int(w) for w in s[5:].split(":")[0].split(",")) == n]  # lonely trees fold extra data
     specs += [s + "+push" for s in specs if s.startswith("tree:")] + ["flat", "oneshot", "flat+bidir"]
     for spec in specs:
+        if spec.split("+")[0].count(":") == 2:  # N - 1 channels: slices of whole aligned blocks
+            count = n * (n - 1) * 4096
+        else:
+            count = 16384 * n
         want = (n - 1) * count if spec == "oneshot" else 2 * (n - 1) * count / n
         for r in range(n):
             got = _remote_elems(nv.plan_dump(spec, r, n, count), r)
