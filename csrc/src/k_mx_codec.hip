@@ -163,7 +163,15 @@ __global__ void __launch_bounds__(64) mx_pack_tail_kernel(const T* __restrict__ 
 #pragma unroll
   for (int o = kMxBlock / 2; o > 0; o >>= 1) am = max(am, (uint32_t)__shfl_xor((int)am, o));
   const uint32_t xr = mx_scale_byte(am, E4);
-  if (i < n) msg[i] = Elem<W>::store(v / mx_scale_value(xr)).bits;
+  if (i < n) {
+    // non-finite values as ops.quant.mx_quantize (torch's fp8 casts) and the whole-block converts give them:
+    // NaN -> 0x7f | sign, Inf -> the type's Inf (e5m2 0x7c) or NaN (e4m3 has no Inf) | sign; the element store
+    // would saturate Inf to the largest finite value
+    const uint32_t b = __float_as_uint(v), sg = (b >> 24) & 0x80u;
+    if ((b & 0x7fffffffu) > 0x7f800000u) msg[i] = (uint8_t)(0x7fu | sg);
+    else if ((b & 0x7fffffffu) == 0x7f800000u) msg[i] = (uint8_t)((E4 ? 0x7fu : 0x7cu) | sg);
+    else msg[i] = Elem<W>::store(v / mx_scale_value(xr)).bits;
+  }
   if (threadIdx.x == 0) msg[n + i0 / kMxBlock] = (uint8_t)xr;
 }
 
