@@ -27,6 +27,8 @@ def main():
     dt = getattr(torch, dtype)
     count = (mib << 20) // dt.itemsize
     grp = LocalGroup(n, workspace_bytes=6 * (mib << 20) + (64 << 20))
+    if os.environ.get("TEP_GRID"):  # workgroups per rank (a multiple of the program's channel count)
+        grp.set_grid(int(os.environ["TEP_GRID"]))
     g = torch.Generator(device="cuda").manual_seed(1)
     xs = [torch.randn(count, device="cuda", generator=g).to(dt) for _ in range(n)]
     ys = [torch.empty_like(x) for x in xs]
