@@ -38,6 +38,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <set>
 #include <vector>
 
 #include "flexar/cost_model.hpp"
@@ -428,7 +429,10 @@ inline HostComm* host_comm(MPI_Comm comm) {
 // device communicator's teardown agrees with its peers by itself (flexar_comm_destroy, host_barrier.hpp).
 struct DevHolder {
   flexar_comm_t c = nullptr;
-  bool zc_closed = false;  // a registration was refused (on every rank): no further attempts
+  // zero copy through the MPI entry points (zc_prepare): buffers whose registration was refused on some rank
+  // (e.g. an allocation above FLEXAR_REG_MAX_ALLOC) are not tried again; past 64 refusals nothing is
+  std::set<std::pair<uintptr_t, size_t>> zc_refused;
+  bool zc_closed = false;
   ~DevHolder() {
     if (c) flexar_comm_destroy(c);
   }
@@ -549,8 +553,9 @@ inline int allreduce(const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
 //    FLEXAR_MPI_ZC_MIN_BYTES (1 MiB) take part in one agreement per call (a 2-int MPI_Allreduce MIN): "both
 //    buffers registered and fresh on every rank" runs the cost model's choice with zero copy allowed (the
 //    flat schedule becomes "+zc+push", zc_policy.hpp); otherwise, while registrations are below
-//    FLEXAR_MPI_ZC_MAX_REGS (64) and none was refused, the buffers are registered collectively (a stale
-//    registration - freed, address reused - is replaced) and the call runs zero copy; else it runs staging
+//    FLEXAR_MPI_ZC_MAX_REGS (64) and this buffer's registration was not refused before, the buffers are
+//    registered collectively (a stale registration - freed, address reused - is replaced) and the call runs
+//    zero copy; else it runs staging
 //    with zero copy disallowed on every rank (flexar_comm_set_zc_auto), so a registration that is fresh on
 //    one rank and stale on another can never split the ranks between two schedules. The c10d backend's
 //    probe window (parallel/backend.py) closes after idle agreements because it sits on DDP's issue path;
@@ -622,15 +627,21 @@ inline bool zc_prepare(MPI_Comm comm, const void* in, const void* out, size_t by
   }
   auto fresh = [&](const void* p) { return flexar_reg_find(c, p, bytes) > 0; };
   const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
+  const bool refused = d->zc_refused.count({(uintptr_t)in, bytes}) || d->zc_refused.count({(uintptr_t)out, bytes});
   int v[2] = {fresh(in) && (in == out || fresh(out)) ? 1 : 0,
-              aligned && !d->zc_closed && flexar_reg_count(c) + 2 <= max_regs ? 1 : 0};
+              aligned && !refused && !d->zc_closed && flexar_reg_count(c) + 2 <= max_regs ? 1 : 0};
   MPI_Allreduce(MPI_IN_PLACE, v, 2, MPI_INT, MPI_MIN, comm);
   bool use = v[0] != 0;
   if (!use && v[1]) {
     int e = ensure_registered(c, comm, in, bytes);  // agreed result on every rank
     if (e == MPI_SUCCESS && in != out) e = ensure_registered(c, comm, out, bytes);
-    if (e == MPI_SUCCESS) use = true;
-    else d->zc_closed = true;
+    if (e == MPI_SUCCESS) {
+      use = true;
+    } else {  // refused on some rank (agreed): remember this buffer, give up after many
+      d->zc_refused.insert({(uintptr_t)in, bytes});
+      d->zc_refused.insert({(uintptr_t)out, bytes});
+      if (d->zc_refused.size() > 64) d->zc_closed = true;
+    }
   }
   flexar_comm_set_zc_auto(c, use ? 1 : 0);
   return use;

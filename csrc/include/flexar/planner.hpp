@@ -88,6 +88,9 @@ class Planner {
       if (count) xfer(count, {loc(BUF_IN, r, 0)}, {loc(BUF_OUT, r, 0)}, scale);
       finish_channel();
       P->desc = "copy";
+    } else if ((spec.zc || spec.bidir) && spec.channels > 1) {
+      if (err) *err = "channels (:C) apply to the staging trees and rings, not to " + spec.str();
+      return false;
     } else if (spec.zc) {
       if (wire || spec.msg || !(spec.kind == AlgoKind::TREE && spec.widths.size() == 1 && spec.widths[0] == (int)N)) {
         if (err) *err = "zero-copy (+zc) runs the flat schedule over IPC-registered buffers (no wire type, no +rccl)";

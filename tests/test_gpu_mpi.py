@@ -76,6 +76,18 @@ def test_mpi_zero_copy_default_fresh_buffers(tools):
     assert r.returncode == 0 and "check n=2097152: ok" in r.stdout, r.stdout[-3000:]
 
 
+def test_mpi_zero_copy_refused_registration(tools):
+    """A buffer whose registration is refused (its allocation above FLEXAR_REG_MAX_ALLOC, here 4 MiB) runs staging,
+    exactly, and is not retried; buffers that fit keep running zero copy."""
+    r = _mpirun(2, [tools["flexar_bench"], "--mem", "device", "--sweep", "2M:16M", "--repeat", "3", "--check"],
+                env={"FLEXAR_REG_MAX_ALLOC": str(4 << 20)})
+    assert r.returncode == 0 and r.stdout.count(": ok") >= 4, r.stdout[-3000:]
+    sched = {int(ln.split("=")[1].split(":")[0]): ln.split(": ")[1] for ln in r.stdout.splitlines()
+             if ln.startswith("schedule n=")}
+    assert "+zc" in sched[(2 << 20) // 4] or "+zc" in sched[(4 << 20) // 4], sched
+    assert "+zc" not in sched[(8 << 20) // 4] and "+zc" not in sched[(16 << 20) // 4], sched
+
+
 def test_mpi_device_buffers_host_staging(tools):
     """Ranks on 'different nodes' (virtual nodes of 1 rank): whole buffer staged through host p2p."""
     r = _mpirun(2, [tools["flexar_bench"], "--mem", "device", "--size", "65537", "--repeat", "3", "--check"],

@@ -137,6 +137,9 @@ def test_parse_and_errors(nv):
         nv.simulate("tree:2,2:3", [np.zeros(64, np.int32)] * 5)  # lonely ranks: no channels
     with pytest.raises(nv.FlexarError):
         nv.simulate("rhd:x", [np.zeros(64, np.int32)] * 4)
+    for bad in ("tree:4:3+zc", "tree:4:3+bidir"):  # the direct exchanges have no stages to relabel
+        with pytest.raises(nv.FlexarError):
+            nv.simulate(bad, [np.zeros(64, np.int32)] * 4, grid=6)
 
 
 def test_message_transport_runs_channelled_trees(nv):
