@@ -157,3 +157,31 @@ def test_selector_prices_channelled_trees(nv):
         for p in nv.enumerate_plans(n):
             if p.startswith("tree:") and p.count(":") == 2:
                 assert nv.model_cost_us(p + "+pull", n, 64 << 20) < 1e20, (n, p)
+
+
+def test_random_trees_and_channels_exact(nv):
+    """Property check over random world sizes, factorizations, channel counts, sizes and all-gather forms: every
+    channelled tree the planner accepts sums exactly on every rank (simulator of the device protocol)."""
+    from hypothesis import given, settings, strategies as st
+
+    import math
+
+    facts = {n: [p for p in nv.enumerate_plans(n) if p.startswith("tree:") and "," in p and p.count(":") == 1
+                 and math.prod(int(w) for w in p[5:].split(",")) == n]  # lonely-rank trees take no channels
+             for n in range(4, 17)}
+    facts = {n: v for n, v in facts.items() if v}
+
+    @settings(max_examples=60, deadline=None, derandomize=True)
+    @given(st.sampled_from(sorted(facts)), st.integers(0, 10 ** 6), st.integers(2, 20), st.integers(1, 6000),
+           st.sampled_from(["", "+push", "+pull", "+push+nofuse"]))
+    def check(n, pick, C, size, mod):
+        base = facts[n][pick % len(facts[n])]
+        spec = f"{base}:{C}{mod}"
+        ins = [np.random.default_rng(size + r).integers(-99, 99, size).astype(np.int32) for r in range(n)]
+        want = np.sum(np.stack(ins), 0)
+        stages = base.count(",") + 1
+        grid = 2 * min(C, 126 // (2 * stages))  # the planner caps C at the flag-slot budget (2 per stage)
+        for r, o in enumerate(nv.simulate(spec, ins, grid=grid, ncalls=2)):
+            np.testing.assert_array_equal(o, want, err_msg=f"{spec} n={n} size={size} r={r}")
+
+    check()
