@@ -248,7 +248,9 @@ def phase(what: str, rank: int = -1, nranks: int = 0, echo: bool = None):
 
         now = time.time()
         stamp = time.strftime("%H:%M:%S", time.localtime(now)) + f".{int(now * 1000) % 1000:03d}"
-        print(f"[phase r{rank} {stamp} +{time.monotonic() - _T0:.3f}s] {what}", file=sys.stderr, flush=True)
+        # one write(2) per line: ranks sharing a launcher's stderr must not split each other's lines
+        sys.stderr.flush()
+        os.write(2, f"[phase r{rank} {stamp} +{time.monotonic() - _T0:.3f}s] {what}\n".encode())
 
 
 def last_error() -> str:

@@ -71,9 +71,20 @@ DROP_AT = {"cost_model_fit": 0.5, "config4_tail": 0.65, "grid_sweep": 0.75}
 COMPANION_AT = 0.85  # config3 / config4 head / config5 / small messages
 
 
+def write_line(fd: int, text: str):
+    """One whole line with ONE write(2) where the OS allows (a pipe takes up to PIPE_BUF = 4 KiB atomically): every
+    rank of a torchrun job shares the launcher's stdout / stderr, and print() issues the text and its newline as two
+    writes, so another rank's line could land between them - or inside rank 0's JSON line."""
+    (sys.stdout if fd == 1 else sys.stderr).flush()
+    data = (text + "\n").encode()
+    while data:
+        n = os.write(fd, data)
+        data = data[n:]
+
+
 def log(rank, *a):
     if rank == 0:
-        print("[bench]", *a, file=sys.stderr, flush=True)
+        write_line(2, " ".join(["[bench]"] + [str(x) for x in a]))
 
 
 _NV = None  # the native module once imported (phase breadcrumbs)
@@ -85,7 +96,7 @@ def phase(rank, what):
     started, on stderr; also a native breadcrumb that the crash report prints."""
     now = time.time()
     stamp = time.strftime("%H:%M:%S", time.localtime(now)) + f".{int(now * 1000) % 1000:03d}"
-    print(f"[phase r{rank} {stamp} +{time.monotonic() - _T_START:.3f}s] bench: {what}", file=sys.stderr, flush=True)
+    write_line(2, f"[phase r{rank} {stamp} +{time.monotonic() - _T_START:.3f}s] bench: {what}")
     if _NV is not None:
         _NV.crumb("phase", "bench: " + what, rank)
 
@@ -254,7 +265,7 @@ def main():
                     help="skip the 64 KiB..64 MiB mini-sweep of the tuner's candidates vs RCCL and the cost-model fit")
     ap.add_argument("--no-configs", action="store_true", help="skip the BASELINE config #3/#4/#5 companion sections")
     ap.add_argument("--config3-mb", type=float, default=1024.0, help="config #3 buffer MiB (bf16)")
-    ap.add_argument("--config4-max", default="1G", help="config #4 sweep top size")
+    ap.add_argument("--config4-max", default="4G", help="config #4 sweep top size (BASELINE: 4 KB -> 4 GB)")
     ap.add_argument("--config5-mb", type=float, default=256.0, help="config #5 buffer MiB (fp32 in, e4m3 wire)")
     ap.add_argument("--transport", default="rccl", choices=["rccl", "auto", "ipc"],
                     help="Communicator transport at N > 1 (rccl: IPC + the '+rccl' message transport candidates)")
@@ -810,8 +821,14 @@ def main():
     out["dropped"] = budget.dropped or None
     out["budget_s"] = budget.seconds
     out["bench_wall_s"] = round(budget.elapsed(), 1)
+    # the result line alone on the shared stdout: every rank's earlier output is out before it (barrier), no rank
+    # writes while it goes out (barrier after), and it leaves in whole writes starting on a fresh line
+    if world > 1:
+        dist.barrier()
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        write_line(1, json.dumps(out))
+    if world > 1:
+        dist.barrier()
     ph("teardown")
     comm.close()
     if world > 1:
