@@ -68,7 +68,8 @@ struct ProgramCost {
   double hbm_write = 0;
 };
 
-inline ProgramCost program_cost(const Program& P, uint32_t rank, int links) {
+inline ProgramCost program_cost(const Program& P, uint32_t rank, int links,
+                                std::vector<std::map<uint32_t, double>>* phases_out = nullptr) {
   ProgramCost c;
   c.stg_bytes = (double)P.stg_bytes();
   const double L = links < 1 ? 1.0 : (double)links;
@@ -108,6 +109,7 @@ inline ProgramCost program_cost(const Program& P, uint32_t rank, int links) {
     for (const auto& kv : ph) mx = std::max(mx, kv.second), tot += kv.second;
     c.link_time_bytes += std::max(mx, tot / L);
   }
+  if (phases_out) *phases_out = std::move(phases);
   return c;
 }
 

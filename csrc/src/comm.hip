@@ -493,10 +493,7 @@ int flexar_comm_last_spec(flexar_comm_t c, char* buf, size_t buflen) {
 int flexar_comm_set_zc_auto(flexar_comm_t c, int on) {
   if (!c) return FLEXAR_ERR_INVALID;
   std::lock_guard<std::mutex> lk(c->mu);
-  if (c->zc_auto != (on != 0)) {
-    c->zc_auto = on != 0;
-    c->memo_gen++;  // a remembered call may hold the other decision
-  }
+  c->zc_auto = on != 0;  // remembered calls carry the policy they were decided under (CallMemo::zc_auto)
   return 0;
 }
 
@@ -518,7 +515,7 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
   const char* akey = algo ? algo : "";
   flexar_comm::CallMemo& m = c->memo[((uint64_t)count * 0x9E3779B97F4A7C15ull + (uint64_t)dtype * 31u + (uint64_t)op) >> 60];
   bool hit = m.gen == c->memo_gen && m.count == count && m.dtype == dtype && m.op == op && m.fsb == fsb &&
-             m.algo == akey;
+             m.zc_auto == c->zc_auto && m.algo == akey;
   AlgoSpec s;
   if (hit) {
     s = m.s;
@@ -567,6 +564,7 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     m.piece = piece;
     m.dp = dp;
     m.grid = grid;
+    m.zc_auto = c->zc_auto;
   };
   if (s.msg) {
     remember(0, nullptr, 0);

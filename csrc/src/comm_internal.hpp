@@ -240,6 +240,7 @@ struct flexar_comm {
     uint64_t piece = 0;
     DevProgram* dp = nullptr;  // program of a one-piece call
     int grid = 0;
+    bool zc_auto = true;  // the zero-copy policy the decision was made under (flexar_comm_set_zc_auto)
   };
   CallMemo memo[16];
   uint64_t memo_gen = 1;

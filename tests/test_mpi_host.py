@@ -73,3 +73,19 @@ def test_plan_tool(tools):
     assert "2*4-1" in r.stdout and "2*3+1" in r.stdout
     r = _run([tools["flexar_plan"], "sweep", "20"])
     assert r.stdout.splitlines()[0] == "N,structures,microseconds" and len(r.stdout.splitlines()) == 21
+
+
+def test_plan_tool_link_table(tools):
+    """flexar_plan links: per phase, the bytes rank 0 moves with each peer. rhd:7 at N = 8 drives all 7 links in every
+    phase with equal bytes; single-channel rhd drives one."""
+    def table(spec):
+        r = _run([tools["flexar_plan"], "links", spec, "8", str(64 << 20)])
+        assert r.returncode == 0, r.stdout
+        rows = [ln.split() for ln in r.stdout.splitlines()[2:]]
+        return [[float(v) for v in row[2:]] for row in rows]
+    seven = [row for row in table("rhd:7+pull") if any(row)]  # (the pull form has one phase of local work only)
+    assert len(seven) == 6
+    for row in seven:
+        assert all(v > 0 for v in row) and max(row) - min(row) <= 0.01 * max(row), row
+    one = [row for row in table("rhd+pull") if any(row)]
+    assert len(one) == 6 and all(sum(v > 0 for v in row) == 1 for row in one), one

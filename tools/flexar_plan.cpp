@@ -13,6 +13,8 @@
 //   flexar_plan select N BYTES       the runtime's choice
 //   flexar_plan cost SPEC N BYTES [ESIZE]  what the compiled programs cost (hand-offs, link / HBM bytes)
 //                                    and the model's time, per rank
+//   flexar_plan links SPEC N BYTES [RANK]  bytes this rank moves to / from each peer in each phase (between
+//                                    hand-offs, all channels together): which xGMI links a schedule drives
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -33,7 +35,7 @@ static std::string star(const std::vector<int>& w) {
 
 static int usage() {
   fprintf(stderr,
-          "usage: flexar_plan model N [bytes] | choose N | sweep [NMAX] | dump SPEC N RANK [COUNT] | select N BYTES |"
+          "usage: flexar_plan model N [bytes] | choose N | sweep [NMAX] | dump SPEC N RANK [COUNT] | select N BYTES | links SPEC N BYTES [RANK] |"
           " cost SPEC N BYTES [ESIZE]\n");
   return 2;
 }
@@ -117,6 +119,38 @@ int main(int argc, char** argv) {
       const ProgramCost c = program_cost(P, (uint32_t)r, m.links);
       printf("%-6d %10.0f %16.0f %18.0f %16.0f %16.0f\n", r, c.handoffs, c.link_bytes, c.link_time_bytes, c.hbm_read,
              c.hbm_write);
+    }
+    return 0;
+  }
+  if (cmd == "links" && argc >= 5) {
+    AlgoSpec s;
+    std::string err;
+    const int n = atoi(argv[3]);
+    const double bytes = atof(argv[4]);
+    const uint32_t r = argc > 5 ? (uint32_t)atoi(argv[5]) : 0;
+    if (!parse_algo(argv[2], n, &s, &err)) { fprintf(stderr, "%s\n", err.c_str()); return 1; }
+    if (s.kind == AlgoKind::AUTO) s = select_plan(m, n, bytes);
+    if (s.kind == AlgoKind::TREE && s.ag == AgMode::AUTO) s.ag = AgMode::PULL;
+    if (s.kind == AlgoKind::LL || s.kind == AlgoKind::DMA || (int)r >= n) return usage();
+    Program P;
+    Planner pl(n, r, (uint64_t)(bytes / 4), 4, 1.0f);
+    if (!pl.build(s, &P, &err)) { fprintf(stderr, "%s\n", err.c_str()); return 1; }
+    std::vector<std::map<uint32_t, double>> ph;
+    const ProgramCost c = program_cost(P, r, m.links, &ph);
+    printf("%s on %d ranks, rank %u, %.0f bytes (fp32): %zu phases, busiest-link bytes %.0f\n", s.str().c_str(), n, r,
+           bytes, ph.size(), c.link_time_bytes);
+    printf("%-6s %6s", "phase", "links");
+    for (int p = 0; p < n; ++p)
+      if ((uint32_t)p != r) printf(" %12s", ("peer " + std::to_string(p)).c_str());
+    printf("\n");
+    for (size_t i = 0; i < ph.size(); ++i) {
+      printf("%-6zu %6zu", i, ph[i].size());
+      for (int p = 0; p < n; ++p) {
+        if ((uint32_t)p == r) continue;
+        auto it = ph[i].find((uint32_t)p);
+        printf(" %12.0f", it == ph[i].end() ? 0.0 : it->second);
+      }
+      printf("\n");
     }
     return 0;
   }
