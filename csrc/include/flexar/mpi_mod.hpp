@@ -181,6 +181,7 @@ struct HostComm {
   size_t shard_cap = 0;
   std::unique_ptr<Pool> pool;
   XgmiModel model = XgmiModel::from_env();
+  std::map<double, AlgoSpec> auto_choice;  // the selector's pick per call size ("auto": priced once, not per call)
   int threads = 1;
 
   ~HostComm() {
@@ -268,7 +269,14 @@ inline int resolve_algo(HostComm& h, double bytes, AlgoSpec* s) {
     fprintf(stderr, "[flexar] %s\n", err.c_str());
     return 1;
   }
-  if (s->kind == AlgoKind::AUTO) *s = select_plan(h.model, h.size, bytes);
+  if (s->kind == AlgoKind::AUTO) {
+    auto it = h.auto_choice.find(bytes);
+    if (it == h.auto_choice.end()) {
+      if (h.auto_choice.size() > 4096) h.auto_choice.clear();
+      it = h.auto_choice.emplace(bytes, select_plan(h.model, h.size, bytes)).first;
+    }
+    *s = it->second;
+  }
   if (s->kind == AlgoKind::LL) s->kind = AlgoKind::ONESHOT;  // LL granules are a device protocol
   if (s->kind == AlgoKind::DMA) s->kind = AlgoKind::TREE, s->widths = {h.size};  // copy engines: device only
   if (s->kind == AlgoKind::TREE && (!h.shared || s->ag == AgMode::AUTO)) s->ag = AgMode::PUSH;
