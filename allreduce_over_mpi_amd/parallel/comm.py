@@ -485,6 +485,13 @@ class Communicator:
         nv.check(self._lib.flexar_comm_describe(self._h, int(count), nv.dtype_code(dtype), b, 512), "describe")
         return b.value.decode()
 
+    def last_spec(self) -> str:
+        """The schedule the last allreduce on this communicator ran, after the zero-copy decision (``describe``
+        gives the plan before it: registered buffers may turn the flat choice into ``+zc+push``); "" before any."""
+        b = ctypes.create_string_buffer(256)
+        nv.check(self._lib.flexar_comm_last_spec(self._h, b, 256), "last_spec")
+        return b.value.decode()
+
     def check(self):
         nv.check(self._lib.flexar_comm_check(self._h), "comm_check")
 

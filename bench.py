@@ -532,6 +532,7 @@ def main():
         f1, _ = check("auto")
         f1 = max_over_ranks(f1)
         t1 = timed("auto", 5) if f1 == 0.0 else None
+        model["registered_choice"] = comm.last_spec() if hasattr(comm, "last_spec") else None  # after the zc decision
         model["registered_measured_us"] = round(t1 * 1e6, 1) if t1 else None
         model["registered_busbw_GBps"] = round(busbw_gbps(nbytes, t1, world), 2) if t1 else None
         model["registered_correct"] = f1 == 0.0

@@ -103,6 +103,8 @@ def test_bench_baseline_config_sections(cuda):
     assert c5["correct"] is True and c5["max_rel_err"] < 0.13 and c5["rccl_fp32_avg_busbw_GBps"] > 0, c5
     assert out["dropped"] is None and out["bench_wall_s"] > 0 and out["budget_s"] == 400
     assert out["readiness"]["calibration"]["source"] in ("measured", "cache"), out["readiness"]
+    if out["zero_copy"]["registered"]:  # the automatic choice on registered buffers, as it ran (last_spec)
+        assert "+zc" in (out["cost_model"].get("registered_choice") or ""), out["cost_model"]
 
 
 def test_bench_budget_drops_in_order(cuda):
