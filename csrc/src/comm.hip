@@ -59,7 +59,12 @@ int resolve_spec(flexar_comm* c, const char* algo, double bytes, AlgoSpec* out, 
       std::string err;
       if (!parse_algo(t, c->nranks, &s, &err)) { set_error("tune table: " + err); return FLEXAR_ERR_INVALID; }
     } else {
-      s = select_plan(c->model, c->nranks, bytes, nullptr, k);
+      std::lock_guard<std::mutex> lk(c->sel_mu);
+      if (c->sel_gen != c->memo_gen || c->sel_memo.size() > 1024) c->sel_memo.clear(), c->sel_gen = c->memo_gen;
+      const auto key = std::make_tuple(bytes, k.esize, (k.narrow_sum ? 1 : 0) | (k.wire_ok ? 2 : 0));
+      auto it = c->sel_memo.find(key);
+      if (it == c->sel_memo.end()) it = c->sel_memo.emplace(key, select_plan(c->model, c->nranks, bytes, nullptr, k)).first;
+      s = it->second;
     }
   }
   // an fp8 wire in the communicator's default spec (FLEXAR_ALGO / FT_TOPO) applies to the calls it can carry:

@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <tuple>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -244,6 +245,11 @@ struct flexar_comm {
   };
   CallMemo memo[16];
   uint64_t memo_gen = 1;
+  // the selector's choice per (bytes, element size, call kind) under the current model (memo_gen): pricing every
+  // candidate program costs tens of us, and the 16-slot call memo above can miss when many sizes alternate
+  std::mutex sel_mu;
+  uint64_t sel_gen = 0;
+  std::map<std::tuple<double, uint32_t, int>, AlgoSpec> sel_memo;
   // readiness (readiness.hpp): protocol families that failed the connect-time self-test, per-peer
   // link classes from the topology probe, residency of the executor kernel
   uint32_t disabled = 0;
