@@ -272,6 +272,8 @@ def main():
     ap.add_argument("--no-reduce-kernel", action="store_true",
                     help="N = 1: skip the fan-in 2/4/8 reduction-kernel section (reduce_kernel)")
     ap.add_argument("--reduce-kernel-mb", type=float, default=256.0, help="reduce_kernel: MiB per source")
+    ap.add_argument("--no-group-executor", action="store_true",
+                    help="N = 1: skip the 8-ranks-in-one-launch executor section (group_executor)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -819,6 +821,8 @@ def main():
                        "through the flexar executor kernel and is not comparable with busbw")
         if not args.no_reduce_kernel:  # outside the timed region; the headline `value` is unchanged
             out["reduce_kernel"] = run_reduce_kernel(dev, args.reduce_kernel_mb)
+        if not args.no_group_executor:
+            out["group_executor"] = run_group_executor(dev)
     out["dropped"] = budget.dropped or None
     out["budget_s"] = budget.seconds
     out["bench_wall_s"] = round(budget.elapsed(), 1)
@@ -970,6 +974,59 @@ def readiness_record(comm, creations=()):
                           "note": getattr(comm, "host_page_note", None)},
             "calibration": getattr(comm, "calibration", None),
             "creations": list(creations) or None}
+
+
+def run_group_executor(dev, ranks=8, mib=64, iters=5,
+                       specs=("flat+pull", "rhd+pull", "rhd:7+pull", "tree:4,2:7+pull", "ring:7", "flat+zc+push")):
+    """N = 1 companion section: the complete multi-rank device protocol (flags, epochs, both staging parities)
+    with `ranks` ranks in ONE launch on this GPU (LocalGroup), fp32 `mib` MiB per rank, for the schedule
+    families of the 8-GPU node - the link-balanced channelled trees among them (`rhd:7`, `tree:4,2:7`). Inputs are
+    integers, so every partial sum is exact: `exact` compares every element of every rank's result with the
+    sum. The "links" are this GPU's HBM, so the figure is the executor's effective HBM rate (program-cost bytes
+    over time), not an xGMI bandwidth."""
+    import torch
+
+    from allreduce_over_mpi_amd import _native as nv
+    from allreduce_over_mpi_amd.parallel import LocalGroup
+
+    t0 = time.perf_counter()
+    count = (mib << 20) // 4
+    grp = LocalGroup(ranks, workspace_bytes=4 * (mib << 20))
+    rows = []
+    try:
+        pat = torch.remainder(torch.arange(count, device=dev, dtype=torch.int32), 251)
+        xs = [(pat + r).float() for r in range(ranks)]
+        want = (pat * ranks + ranks * (ranks - 1) // 2).float()
+        del pat
+        ys = [torch.empty_like(x) for x in xs]
+        for spec in specs:
+            row = {"spec": spec}
+            try:
+                for _ in range(2):  # both staging parities (the in-process "+zc" addresses the ranks' buffers directly)
+                    grp.all_reduce(xs, "sum", outs=ys, algo=spec)
+                torch.cuda.synchronize()
+                row["exact"] = all(torch.equal(y, want) for y in ys)
+                st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                st.record()
+                for _ in range(iters):
+                    grp.all_reduce(xs, "sum", outs=ys, algo=spec)
+                en.record()
+                torch.cuda.synchronize()
+                us = st.elapsed_time(en) * 1e3 / iters
+                costs = [nv.program_cost(spec, r, ranks, count, "float32", links=1) for r in range(ranks)]
+                hbm = sum(c["hbm_read"] + c["hbm_write"] for c in costs)
+                row.update(us=round(us, 1), eff_hbm_TBps=round(hbm / (us * 1e-6) / 1e12, 3))
+                grp.check()
+            except nv.FlexarError as e:
+                row["error"] = str(e)
+            rows.append(row)
+        del xs, ys, want
+    finally:
+        grp.close()
+        torch.cuda.empty_cache()
+    return {"what": f"{ranks} ranks x {mib} MiB fp32 in one launch on one GPU (LocalGroup): the multi-rank protocol "
+                    "and schedules of the 8-GPU node, shared HBM instead of xGMI", "rows": rows,
+            "wall_s": round(time.perf_counter() - t0, 2)}
 
 
 def run_reduce_kernel(dev, mib=256.0, fanins=(2, 4, 8), dtypes=("float32", "bfloat16", "float8_e4m3fn"), iters=10):

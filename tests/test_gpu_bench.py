@@ -133,3 +133,22 @@ def test_bench_json_names_a_recovered_selftest_family(cuda):
     assert rd["creations"][0]["selftest_recovered"] == ["fence"], rd
     assert rd["host_page"]["joined"] is True and rd["host_page"]["verified_shared"] is True, rd
     assert out["value"] > 0
+
+
+def test_bench_n1_line_carries_the_group_executor_section(cuda):
+    """The driver's N = 1 line (no launcher): besides the headline it carries the 8-ranks-in-one-launch executor
+    section, every schedule family of the 8-GPU node (the link-balanced channelled trees among them) exact on
+    integer data, with a time and an effective HBM rate."""
+    env = dict(os.environ, FLEXAR_NO_BUILD="1")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "3", "--warmup", "1",
+                        "--no-reduce-kernel"], env=env, capture_output=True, text=True, timeout=240, cwd=REPO)
+    _keep(r, "n1_group_executor")
+    assert r.returncode == 0, _diag(r, "n1_group_executor")
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 1 and out["value"] == 0.0
+    rows = {row["spec"]: row for row in out["group_executor"]["rows"]}
+    assert {"rhd+pull", "rhd:7+pull", "tree:4,2:7+pull", "flat+pull"} <= set(rows), rows
+    for spec, row in rows.items():
+        assert row.get("exact") is True and row["us"] > 0 and 0 < row["eff_hbm_TBps"] < 10, (spec, row)
