@@ -287,7 +287,9 @@ void fill_ctx(flexar_comm* c, DevProgram* dp, const void* in, void* out, DevCtx*
   x->stg_half_bytes = c->half_bytes;
   x->err = c->err_dev;
   // launch progress words for the crash report: two system-scope stores per launch, only when the report is on
-  x->progress = crumbs_on() ? reinterpret_cast<uint64_t*>(c->err_dev) + 1 : nullptr;
+  // (FLEXAR_PROGRESS=0 keeps the host breadcrumbs and drops the device stores)
+  static const bool progress_on = crumbs_on() && !(getenv("FLEXAR_PROGRESS") && *getenv("FLEXAR_PROGRESS") == '0');
+  x->progress = progress_on ? reinterpret_cast<uint64_t*>(c->err_dev) + 1 : nullptr;
   x->ichunk = c->xfer_chunk;  // 0 = slices (FLEXAR_EXEC_INTERLEAVE, flexar_comm_set_xfer_chunk)
   x->timeout_ticks = c->timeout_ticks;
   x->vec_ok = vec_ok_for(((uintptr_t)in) | ((uintptr_t)out));
