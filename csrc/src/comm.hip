@@ -263,7 +263,7 @@ int choose_grid(flexar_comm* c, uint64_t bytes, uint32_t nchan) {
   return g;
 }
 
-void fill_ctx(flexar_comm* c, DevProgram* dp, const void* in, void* out, DevCtx* x) {
+void fill_ctx(flexar_comm* c, DevProgram* dp, const void* in, void* out, DevCtx* x, uint64_t bytes) {
   memset(x, 0, sizeof(*x));
   if (dp) {
     x->ops = dp->d_ops;
@@ -286,10 +286,12 @@ void fill_ctx(flexar_comm* c, DevProgram* dp, const void* in, void* out, DevCtx*
   x->epochs = c->epochs;
   x->stg_half_bytes = c->half_bytes;
   x->err = c->err_dev;
-  // launch progress words for the crash report: two system-scope stores per launch, only when the report is on
-  // (FLEXAR_PROGRESS=0 keeps the host breadcrumbs and drops the device stores)
+  // launch progress words for the crash report: two system-scope stores into host memory per launch, which
+  // cost 0.4-0.7 us of a small call (profiles/r6_latency): only for launches of at least FLEXAR_PROGRESS_MIN_BYTES
+  // (1 MiB; the breadcrumbs still record every launch), none with FLEXAR_PROGRESS=0 or FLEXAR_CRASH_REPORT=0
   static const bool progress_on = crumbs_on() && !(getenv("FLEXAR_PROGRESS") && *getenv("FLEXAR_PROGRESS") == '0');
-  x->progress = progress_on ? reinterpret_cast<uint64_t*>(c->err_dev) + 1 : nullptr;
+  static const uint64_t progress_min = env_u64("FLEXAR_PROGRESS_MIN_BYTES", 1ull << 20);
+  x->progress = progress_on && bytes >= progress_min ? reinterpret_cast<uint64_t*>(c->err_dev) + 1 : nullptr;
   x->ichunk = c->xfer_chunk;  // 0 = slices (FLEXAR_EXEC_INTERLEAVE, flexar_comm_set_xfer_chunk)
   x->timeout_ticks = c->timeout_ticks;
   x->vec_ok = vec_ok_for(((uintptr_t)in) | ((uintptr_t)out));
@@ -371,7 +373,7 @@ int run_rs_ag(flexar_comm* c, Coll coll, const void* in, void* out, size_t count
     DevProgram* dp = nullptr;
     if ((rc = get_program(c, s, n, es, fs, &dp, coll, count))) return rc;
     DevCtx x;
-    fill_ctx(c, dp, (const char*)in + off * es, (char*)out + off * es, &x);
+    fill_ctx(c, dp, (const char*)in + off * es, (char*)out + off * es, &x, n * es);
     if (dp->prog.zc) {  // the N-block side spans (N - 1) rank strides + this piece
       const uint64_t wide = ((uint64_t)(c->nranks - 1) * count + n) * es;
       const uint64_t in_b = coll == Coll::ALL_GATHER ? n * es : wide, out_b = coll == Coll::REDUCE_SCATTER ? n * es : wide;
@@ -435,7 +437,7 @@ int run_bcast(flexar_comm* c, const void* in, void* out, size_t count, int dtype
     DevProgram* dp = nullptr;
     if ((rc = get_program(c, s, n, es, 1.0f, &dp, Coll::BROADCAST, (uint64_t)root))) return rc;
     DevCtx x;
-    fill_ctx(c, dp, (const char*)in + off * es, (char*)out + off * es, &x);
+    fill_ctx(c, dp, (const char*)in + off * es, (char*)out + off * es, &x, n * es);
     if (dp->prog.zc &&
         (rc = zc_bind(c, dp->prog, (const char*)in + off * es, n * es, (char*)out + off * es, n * es, &x)))
       return rc;
@@ -608,7 +610,7 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
   if (s.kind == AlgoKind::LL) {
     LaunchArgs la;
     la.kind = LAUNCH_LL;
-    fill_ctx(c, nullptr, in, out, &la.ctx);
+    fill_ctx(c, nullptr, in, out, &la.ctx, (uint64_t)count * es);
     la.ctx.count = count;
     la.ctx.scale = fs;
     la.grid = hit ? m.grid : ll_grid(c, count, es);
@@ -644,7 +646,7 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     if (!dp && (rc = get_program(c, s, count, es, fs, &dp))) return rc;
     LaunchArgs la;
     la.kind = LAUNCH_EXEC;
-    fill_ctx(c, dp, in, out, &la.ctx);
+    fill_ctx(c, dp, in, out, &la.ctx, (uint64_t)count * es);
     if (dp->prog.zc && (rc = zc_bind(c, dp->prog, in, (uint64_t)count * es, out, (uint64_t)count * es, &la.ctx)))
       return rc;
     la.grid = hit ? m.grid : choose_grid(c, count * es, dp->prog.nchan);
@@ -681,7 +683,7 @@ int flexar_allreduce_ex(flexar_comm_t c, const void* in, void* out, size_t count
     DevProgram* dp = nullptr;
     if ((rc = get_program(c, s, n, es, fs, &dp))) return rc;
     DevCtx x;
-    fill_ctx(c, dp, (const char*)in + off * es, (char*)out + off * es, &x);
+    fill_ctx(c, dp, (const char*)in + off * es, (char*)out + off * es, &x, n * es);
     if (dp->prog.zc &&
         (rc = zc_bind(c, dp->prog, (const char*)in + off * es, n * es, (char*)out + off * es, n * es, &x)))
       break;
@@ -796,7 +798,7 @@ int flexar_allreduce_fp8(flexar_comm_t c, const void* in, void* out, size_t coun
     if ((rc = get_program(c, s, n, es, fs, &dp))) return rc;
     LaunchArgs la;
     la.kind = LAUNCH_EXEC;
-    fill_ctx(c, dp, (const char*)in + off * es, (char*)out + off * es, &la.ctx);
+    fill_ctx(c, dp, (const char*)in + off * es, (char*)out + off * es, &la.ctx, n * es);
     la.ctx.amax_parts = amax_parts;
     la.grid = choose_grid(c, n * es, dp->prog.nchan);
     la.stream = st;

@@ -326,7 +326,7 @@ const flexar_comm::Reg* reg_lookup(flexar_comm* c, const void* p, uint64_t bytes
 int zc_bind(flexar_comm* c, const Program& P, const void* in, uint64_t in_bytes, const void* out, uint64_t out_bytes,
             DevCtx* x);
 int choose_grid(flexar_comm* c, uint64_t bytes, uint32_t nchan);
-void fill_ctx(flexar_comm* c, DevProgram* dp, const void* in, void* out, DevCtx* x);
+void fill_ctx(flexar_comm* c, DevProgram* dp, const void* in, void* out, DevCtx* x, uint64_t bytes = ~0ull);
 bool zc_registered(flexar_comm* c, const void* in, const void* out, uint64_t bytes);
 int plan_pieces(flexar_comm* c, const AlgoSpec& s, uint64_t count, uint32_t esize, float fs, uint64_t* piece,
                 Coll coll = Coll::ALLREDUCE, uint64_t stride = 0);

@@ -275,7 +275,7 @@ void crash_report_write(const char* why) {
     if (!p || p == kClaimed) continue;
     o.s("[flexar crash report]   communicator rank ").i(g_live[i].rank).s("/").i(g_live[i].nranks).s(" device ")
         .i(g_live[i].device).s(": executor workgroup 0 started epoch ").u(p[0]).s(", finished epoch ").u(p[1])
-        .s("\n");
+        .s(" (launches of >= FLEXAR_PROGRESS_MIN_BYTES, default 1 MiB)\n");
   }
   // newest records: find the highest sequence, walk back
   uint64_t hi = g_next.load(std::memory_order_acquire);
