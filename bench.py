@@ -992,6 +992,11 @@ def run_group_executor(dev, ranks=8, mib=64, iters=5,
     t0 = time.perf_counter()
     count = (mib << 20) // 4
     grp = LocalGroup(ranks, workspace_bytes=4 * (mib << 20))
+    # the same workgroups per rank for every schedule: 28, a multiple of the 7 channels of rhd:7 / tree:4,2:7 /
+    # ring:7 (a grid is rounded down to whole channels, which on its own would cost the channelled forms 1/8 of
+    # their workgroups here: profiles/r6_channels/)
+    grid = 28
+    grp.set_grid(grid)
     rows = []
     try:
         pat = torch.remainder(torch.arange(count, device=dev, dtype=torch.int32), 251)
@@ -1024,8 +1029,9 @@ def run_group_executor(dev, ranks=8, mib=64, iters=5,
     finally:
         grp.close()
         torch.cuda.empty_cache()
-    return {"what": f"{ranks} ranks x {mib} MiB fp32 in one launch on one GPU (LocalGroup): the multi-rank protocol "
-                    "and schedules of the 8-GPU node, shared HBM instead of xGMI", "rows": rows,
+    return {"what": f"{ranks} ranks x {mib} MiB fp32 in one launch on one GPU (LocalGroup, {grid} workgroups per "
+                    "rank): the multi-rank protocol and schedules of the 8-GPU node, shared HBM instead of xGMI",
+            "rows": rows,
             "wall_s": round(time.perf_counter() - t0, 2)}
 
 
