@@ -2,6 +2,7 @@
 objects ship inside a platform wheel; built with no index access (--no-build-isolation)."""
 import glob
 import os
+import shutil
 import subprocess
 import sys
 import zipfile
@@ -21,3 +22,6 @@ def test_wheel_carries_the_native_runtime(tmp_path, nv):
     assert "allreduce_over_mpi_amd/_lib/libflexar.so" in names
     assert any(n.startswith("allreduce_over_mpi_amd/_lib/_fastcall") for n in names)
     assert "allreduce_over_mpi_amd/parallel/backend.py" in names
+    # setuptools builds in the source tree: leave it as it was
+    for d in ("build/lib", "build/bdist.linux-x86_64", "allreduce_over_mpi_amd.egg-info"):
+        shutil.rmtree(os.path.join(REPO, d), ignore_errors=True)
