@@ -1503,6 +1503,8 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
   __shared__ float s_pre;
   const uint32_t tid = threadIdx.x;
   const uint32_t nchan = c.nchan;
+  // channel c = workgroups b == c (mod nchan); contiguous workgroups per channel measured the same bytes and
+  // time (profiles/r6_channels/)
   const uint32_t ch = b % nchan, lb = b / nchan;
   const uint32_t nb = (grid - ch + nchan - 1) / nchan;
   constexpr bool TYPED = !std::is_void<W>::value;
