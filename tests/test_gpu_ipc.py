@@ -454,8 +454,10 @@ def _stress_worker(rank, world, port, calls, q, fault=""):
 
         comm = Communicator(workspace_bytes=32 << 20)
         specs = ["flat", "flat+push", "flat+wt", "flat+push+nts", "ring", "ring+wt", "oneshot", "ll", "dma",
-                 "rhd", "tree:2,2+push", "flat+bidir"] if world == 4 else ["flat", "flat+push+wt", "ring", "oneshot", "ll", "dma",
-                                                              "flat+bidir+wt"]
+                 "rhd", "tree:2,2+push", "flat+bidir", "rhd:3+pull", "tree:2,2:3+push"] if world == 4 else \
+            ["flat", "flat+push+wt", "ring", "oneshot", "ll", "dma", "flat+bidir+wt"]
+        if world == 8:  # link-balanced channelled trees (rhd:7 drives all 7 links in every stage)
+            specs += ["rhd:7+pull", "tree:4,2:7+push"]
         specs += ["flat+zc", "flat+zc+push", "flat+zc+put"]
         # zero-copy calls run on registered arenas (the same offsets on every rank: the same call sequence)
         arena_in = torch.empty(world * 2_000_003 + 64, device="cuda")
