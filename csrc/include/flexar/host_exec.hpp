@@ -196,8 +196,9 @@ struct HostExec {
     const uint32_t ch = gblock % nchan, lb = gblock / nchan;
     const uint32_t nb = (grid - ch + nchan - 1) / nchan;
     const uint32_t unit = P.stg_unit();
-    // slice boundaries keep every operand 16-B aligned: 16 bytes of the narrowest operand type
-    const uint32_t quantum = P.wire >= 4 ? kMxBlock : unit >= 16 ? 1 : (uint32_t)(16 / (P.wire ? unit : sizeof(T)));
+    // slice boundaries as on the device (slice_quantum): whole 256-B runs of the narrowest operand type
+    const uint32_t ub = P.wire ? unit : (uint32_t)sizeof(T);
+    const uint32_t quantum = P.wire >= 4 ? slice_quantum(1, kMxBlock) : slice_quantum(ub, ub >= 16 ? 1 : 16 / ub);
     const uint64_t par = (epoch & 1) ? c.stg_half_bytes : 0;
     auto addr = [&](const Loc& l) -> char* {
       if (l.buf == BUF_STG) return c.peer_stg[l.rank] + par + l.off * unit;

@@ -67,7 +67,7 @@ struct Op {
 };
 
 // Deterministic split of a span across the grid blocks of one channel.
-// Boundaries are multiples of `quantum` elements (16 B worth), so the vector
+// Boundaries are multiples of `quantum` elements (slice_quantum), so the vector
 // path stays aligned on every block. Identical on every rank => sender block b
 // writes exactly the slice receiver block b reads.
 FX_HD FX_INLINE void slice_range(uint64_t len, uint32_t lb, uint32_t nb, uint32_t quantum, uint64_t* lo,
@@ -80,6 +80,18 @@ FX_HD FX_INLINE void slice_range(uint64_t len, uint32_t lb, uint32_t nb, uint32_
   if (h > len) h = len;
   *lo = l;
   *hi = h;
+}
+
+// Slice boundaries in whole FLEXAR_SLICE_ALIGN-byte runs of the narrowest operand (`unit` bytes per element),
+// and never finer than `min_quantum` elements (16 B of vector access, an MX block). Op offsets are already
+// kStageAlignBytes-aligned (the planner's round_up), so every workgroup's slice then starts on a cache-line
+// boundary: with 16-B boundaries three slices in four started mid-line, and each 1 KiB wave access touched 17
+// 64-B lines instead of 16 (profiles/r6_channels/req_split: +8 % TCP->TCC read requests on the 3-channel split).
+#ifndef FLEXAR_SLICE_ALIGN
+#define FLEXAR_SLICE_ALIGN 256
+#endif
+FX_HD FX_INLINE constexpr uint32_t slice_quantum(uint32_t unit, uint32_t min_quantum) {
+  return (uint32_t)FLEXAR_SLICE_ALIGN / unit > min_quantum ? (uint32_t)FLEXAR_SLICE_ALIGN / unit : min_quantum;
 }
 
 constexpr uint32_t kProgSlots = kMaxSlots - 2;

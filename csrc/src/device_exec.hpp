@@ -1510,7 +1510,9 @@ __device__ FX_INLINE void exec_body(const DevCtx& c, const uint32_t b, const uin
   constexpr bool TYPED = !std::is_void<W>::value;
   using WT_ = typename std::conditional<TYPED, W, T>::type;
   constexpr uint32_t U = sizeof(T) < sizeof(WT_) ? sizeof(T) : sizeof(WT_);
-  const uint32_t quantum = IsMx<WT_>::value ? kMxBlock : TYPED ? 16 / U : (sizeof(T) >= 16 ? 1u : (uint32_t)(16 / sizeof(T)));
+  const uint32_t quantum = IsMx<WT_>::value ? slice_quantum(1, kMxBlock)
+                           : TYPED         ? slice_quantum(U, 16 / U)
+                                           : slice_quantum(sizeof(T), sizeof(T) >= 16 ? 1u : (uint32_t)(16 / sizeof(T)));
   const uint64_t epoch = c.epochs[b] + 1;
   const uint64_t par = (epoch & 1) ? c.stg_half_bytes : 0;
   if (tid == 0) s_abort = 0;
@@ -1865,7 +1867,7 @@ __attribute__((amdgpu_waves_per_eu(FLEXAR_REDUCE_OCC4 && PM != PM_WT && IsFp8<T>
     }
   }
   vec &= 1;
-  const uint32_t quantum = sizeof(T) >= 16 ? 1u : (uint32_t)(16 / sizeof(T));
+  const uint32_t quantum = slice_quantum(sizeof(T), sizeof(T) >= 16 ? 1u : (uint32_t)(16 / sizeof(T)));
   uint64_t lo, hi;
   slice_range(n, blockIdx.x, gridDim.x, quantum, &lo, &hi);
   const uint64_t step = PM == PM_WT ? kWtChunkBytes / sizeof(T) : ~0ull;  // 32-bit buffer offsets
