@@ -107,7 +107,7 @@ def main():
 
     base = next((r["us_per_call"] for r in res[0] if r["case"] == "flat:float32"), None)
     for r in res[0]:
-        r.update(ranks=world, mib_per_rank=mib, grid_per_rank=grid, lib=os.path.basename(os.path.dirname(nv.lib_path())),
+        r.update(ranks=world, mib_per_rank=mib, grid_per_rank=grid, lib=os.path.basename(os.path.dirname(os.environ.get("FLEXAR_LIB_PATH") or nv.lib_path())),
                  vs_flat_fp32=round(r["us_per_call"] / base, 3) if base else None)
         print(json.dumps(r), flush=True)
 

@@ -1178,7 +1178,7 @@ __device__ FX_INLINE void mx_elem(const char* const (&s)[kMaxSrc], const uint8_t
 // layout of xfer_mx (every memory instruction contiguous across the workgroup; the scale bytes through
 // buffer descriptors built once, at one per-lane offset shared by every operand), then whole blocks in the
 // contiguous layout (16 elements per lane, a block per lane pair), then the last partial block element-wise.
-template <typename T, typename W, int K, int SP, int PM>
+template <typename T, typename W, int K, int SP, int PM, int ND = kMaxDst>
 __device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_t* const (&ss)[kMaxSrc],
                                    char* const (&d)[kMaxDst], uint8_t* const (&sd)[kMaxDst], int nd, uint32_t dm,
                                    uint64_t n, float scale, bool vec) {
@@ -1203,11 +1203,11 @@ __device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_
     // the scale shadows cover the whole blocks only: the last partial block is the scalar tail's (mx_elem),
     // so a lane of the partial super-group never writes its scale
     const uint64_t nfull = n / kMxBlock;
-    __amdgpu_buffer_rsrc_t rss[K], rsd[kMaxDst];
+    __amdgpu_buffer_rsrc_t rss[K], rsd[ND];
 #pragma unroll
     for (int k = 0; k < K; ++k) rss[k] = rsrc_of(isw(k) ? (const char*)ss[k] : nullptr, isw(k) ? nfull : 0);
 #pragma unroll
-    for (int dd = 0; dd < kMaxDst; ++dd) rsd[dd] = rsrc_of((const char*)sd[dd], sd[dd] ? nfull : 0);
+    for (int dd = 0; dd < ND; ++dd) rsd[dd] = rsrc_of((const char*)sd[dd], sd[dd] ? nfull : 0);
     uint64_t sg = 0;
     // one iteration over UI super-groups; full super-groups beyond the last multiple of UU take the same
     // lane-interleaved layout one at a time (a slice of a few super-groups - DDP buckets, small pieces -
@@ -1215,14 +1215,14 @@ __device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_
     // `lim` elements from super-group sg (fewer for the last, partial one: see xfer_mx)
     auto iter = [&](auto ucnt, uint64_t lim) {
       constexpr int UI = decltype(ucnt)::value;
-      __amdgpu_buffer_rsrc_t bs[K], bd[kMaxDst];
+      __amdgpu_buffer_rsrc_t bs[K], bd[ND];
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const uint64_t es = isw(k) ? 1 : sizeof(T);
         bs[k] = rsrc_of(s[k] + sg * span * es, lim * es);
       }
 #pragma unroll
-      for (int dd = 0; dd < kMaxDst; ++dd) {
+      for (int dd = 0; dd < ND; ++dd) {
         if (dd >= nd) continue;
         const uint64_t es = (dm >> dd) & 1 ? 1 : sizeof(T);
         bd[dd] = rsrc_of(d[dd] + sg * span * es, lim * es);
@@ -1252,7 +1252,7 @@ __device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_
         uint32_t xb[VM];
         mx_group<T, W, K, SP, RL>(raw[u], sb[u], scale, nd, dm, yq, xb, yt);
 #pragma unroll
-        for (int dd = 0; dd < kMaxDst; ++dd) {
+        for (int dd = 0; dd < ND; ++dd) {
           if (dd >= nd) continue;
           const bool wide = (dm >> dd) & 1;
 #pragma unroll
@@ -1306,7 +1306,7 @@ __device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_
     uint32_t xb[1];
     mx_group<T, W, K, SP, G>(raw, sb, scale, nd, dm, yq, xb, yt);
 #pragma unroll
-    for (int dd = 0; dd < kMaxDst; ++dd) {
+    for (int dd = 0; dd < ND; ++dd) {
       if (dd >= nd) continue;
       if ((dm >> dd) & 1) {
         st(dd, v * G, yq);
@@ -1345,16 +1345,42 @@ __device__ FX_INLINE bool xfer_mx_k(int sp, const char* const (&s)[kMaxSrc], cha
 
 // MX wire patterns (validate: typed_pattern_ok): quantising push (K 1, SP_T), reduction (K >= 2, SP_TW),
 // dequantising all-gather (K 1, SP_W, dtype destinations only).
+#ifndef FLEXAR_MX_ND2
+#define FLEXAR_MX_ND2 1
+#endif
 template <typename T, typename W, int K, int PM>
 __device__ FX_INLINE bool xfer_mxb_k(int sp, const char* const (&s)[kMaxSrc], const uint8_t* const (&ss)[kMaxSrc],
                                      char* const (&d)[kMaxDst], uint8_t* const (&sd)[kMaxDst], int nd, uint32_t dm,
                                      uint64_t n, float scale, bool vec) {
+  // An instantiation for at most 2 destinations (own output + the published wire block) keeps 6 fewer destination
+  // pointers / buffer descriptors live: those spilled SGPRs into VGPR lanes and, at fan-in 8, VGPRs to scratch
+  // (profiles/r6_mx_nd/). K = 1 copies with more destinations take the general one. FLEXAR_MX_ND2=0: the A/B
+  // build without it
+  const bool nd2 = FLEXAR_MX_ND2 && nd <= 2;
   if constexpr (K == 1) {
-    if (sp == SP_T) { xfer_mxb<T, W, 1, SP_T, PM>(s, ss, d, sd, nd, dm, n, scale, vec); return true; }
-    if (sp == SP_W && dm == 0) { xfer_mxb<T, W, 1, SP_W, PM>(s, ss, d, sd, nd, dm, n, scale, vec); return true; }
+    if (sp == SP_T) {
+      if (nd2) xfer_mxb<T, W, 1, SP_T, PM, 2>(s, ss, d, sd, nd, dm, n, scale, vec);
+      else xfer_mxb<T, W, 1, SP_T, PM>(s, ss, d, sd, nd, dm, n, scale, vec);
+      return true;
+    }
+    if (sp == SP_W && dm == 0) {
+      if (nd2) xfer_mxb<T, W, 1, SP_W, PM, 2>(s, ss, d, sd, nd, dm, n, scale, vec);
+      else xfer_mxb<T, W, 1, SP_W, PM>(s, ss, d, sd, nd, dm, n, scale, vec);
+      return true;
+    }
     return false;
   } else {
-    if (sp == SP_TW) { xfer_mxb<T, W, K, SP_TW, PM>(s, ss, d, sd, nd, dm, n, scale, vec); return true; }
+    if (sp == SP_TW) {
+      // at most 2 destinations (planner.hpp typed_pattern_ok: fp8 wires always pull): one instantiation. The
+      // general one (up to kMaxDst) at fan-in 8 set the whole kernel's allocation to 256 VGPRs plus scratch
+      if constexpr (FLEXAR_MX_ND2) {
+        if (nd > 2) return false;
+        xfer_mxb<T, W, K, SP_TW, PM, 2>(s, ss, d, sd, nd, dm, n, scale, vec);
+      } else {
+        xfer_mxb<T, W, K, SP_TW, PM>(s, ss, d, sd, nd, dm, n, scale, vec);
+      }
+      return true;
+    }
     return false;
   }
 }
@@ -1722,9 +1748,18 @@ __device__ FX_INLINE void ll_body(const DevCtx& c, const uint32_t b, const uint3
   if (b == 0 && tid == 0 && c.progress) __hip_atomic_store(c.progress + 1, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Production launches take the context by value (no device copy per launch), but exec_body indexes it with
+// run-time values (peer_stg[l.rank], local[l.buf], chan_start[ch]): on a by-value parameter the compiler then
+// copies the whole DevCtx to scratch (36 B / lane of private memory in the untyped executor). Read it in
+// place through the kernarg segment instead (the only explicit argument, at offset 0): scratch 0.
+__device__ FX_INLINE const DevCtx& kernarg_ctx() {
+  return *(const DevCtx*)__builtin_amdgcn_kernarg_segment_ptr();  // C cast: constant -> generic address space
+}
+
 template <typename T, typename OP>
 __global__ void __launch_bounds__(kExecThreads) ll_kernel(DevCtx c) {
-  if constexpr (sizeof(T) <= 4) ll_body<T, OP>(c, blockIdx.x, gridDim.x);
+  (void)c;
+  if constexpr (sizeof(T) <= 4) ll_body<T, OP>(kernarg_ctx(), blockIdx.x, gridDim.x);
 }
 template <typename T, typename OP>
 __global__ void __launch_bounds__(kExecThreads) ll_group_kernel(const DevCtx* ctxs, uint32_t grid_per_rank) {
@@ -1734,7 +1769,8 @@ __global__ void __launch_bounds__(kExecThreads) ll_group_kernel(const DevCtx* ct
 // Production launch: one rank per process, context by value.
 template <typename T, typename OP, int PM>
 __global__ void __launch_bounds__(kExecThreads) exec_kernel(DevCtx c) {
-  exec_body<T, OP, PM>(c, blockIdx.x, gridDim.x);
+  (void)c;
+  exec_body<T, OP, PM>(kernarg_ctx(), blockIdx.x, gridDim.x);
 }
 
 // Typed programs (Program::wire: fp32 partials or an fp8 wire), SUM/AVG only.
@@ -1767,7 +1803,8 @@ constexpr int typed_min_waves() {
 template <typename T, typename W, int PM, int KMAX = kMaxSrc>
 __global__ void __launch_bounds__(kTypedThreads) __attribute__((amdgpu_waves_per_eu(typed_min_waves<W, KMAX>())))
 exec_mx_kernel(DevCtx c) {
-  exec_body<T, OpSum, PM, W, KMAX>(c, blockIdx.x, gridDim.x);
+  (void)c;
+  exec_body<T, OpSum, PM, W, KMAX>(kernarg_ctx(), blockIdx.x, gridDim.x);
 }
 template <typename T, typename W, int PM, int KMAX = kMaxSrc>
 __global__ void __launch_bounds__(kTypedThreads) __attribute__((amdgpu_waves_per_eu(typed_min_waves<W, KMAX>())))
