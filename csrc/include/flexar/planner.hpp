@@ -1121,9 +1121,9 @@ inline bool typed_pattern_ok(const Program& P, const Op& o) {
   const int K = o.nsrc;
   // MX wire: a wire-to-wire copy would have to carry the block scales too (the flat schedule has none)
   if (P.wire >= 4 && sm == all_s && dm) return false;
-  // MX reductions write at most 2 destinations (own output + the published wire block: fp8 wires always pull);
-  // the executor instantiates that form only (device_exec.hpp xfer_mxb_k)
-  if (P.wire >= 4 && K >= 2 && o.ndst > 2) return false;
+  // MX ops write at most 2 destinations (a reduction: own output + the published wire block; fp8 wires always
+  // pull): the executor instantiates that form only (device_exec.hpp xfer_mxb_k)
+  if (P.wire >= 2 && o.ndst > 2) return false;  // the same for the global-scale fp8 wire (device_exec.hpp xfer_mx_k)
   // wire type throughout: fp32 partials of any fan-in; an fp8 wire only copies (its kernels carry no fp8 sum)
   if (sm == all_s && dm == all_d) return fp8 ? K == 1 : true;
   if (!fp8 && sm == 0 && dm == 0) return true;  // dtype throughout

@@ -690,7 +690,7 @@ constexpr int typed_uu(int v) { return v <= FLEXAR_TYPED_UU4_MAXV ? 4 : (v <= FL
 #endif
 constexpr bool typed_pipe(int v) { return v <= FLEXAR_TYPED_PIPE_MAXV; }
 
-template <typename T, typename W, int K, int SP, int PM>
+template <typename T, typename W, int K, int SP, int PM, int ND = kMaxDst>
 __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (&d)[kMaxDst], int nd, uint32_t dm,
                                   uint64_t n, float scale, float pre, float post_inv, bool vec) {
   constexpr int U = sizeof(T) < sizeof(W) ? (int)sizeof(T) : (int)sizeof(W);
@@ -705,12 +705,12 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
   auto isw = [](int k) constexpr -> bool { return SP == SP_W || (SP == SP_TW && k > 0); };
   const uint64_t nt = blockDim.x;
   const uint64_t ng = vec ? n / G : 0;
-  __amdgpu_buffer_rsrc_t rs[K], rd[kMaxDst];
+  __amdgpu_buffer_rsrc_t rs[K], rd[ND];
   if constexpr (WT) {
 #pragma unroll
     for (int k = 0; k < K; ++k) rs[k] = rsrc_of(s[k], n * (isw(k) ? sizeof(W) : sizeof(T)));
 #pragma unroll
-    for (int dd = 0; dd < kMaxDst; ++dd)
+    for (int dd = 0; dd < ND; ++dd)
       if (dd < nd) rd[dd] = rsrc_of(d[dd], n * ((dm >> dd) & 1 ? sizeof(W) : sizeof(T)));
   }
   auto ld = [&](int k, uint64_t byte) -> uint4 {
@@ -787,7 +787,7 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
     float acc[G];
     compute_group(raw, acc);
 #pragma unroll
-    for (int dd = 0; dd < kMaxDst; ++dd) {
+    for (int dd = 0; dd < ND; ++dd) {
       if (dd >= nd) continue;
       uint4 y[VM];
       encode_dst(dd, raw, acc, y);
@@ -845,9 +845,9 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
     };
     auto finish_it = [&](auto ucnt, uint64_t sg0, uint64_t lim, const uint4 (&raw)[decltype(ucnt)::value][K][VM]) {
       constexpr int UI = decltype(ucnt)::value;
-      __amdgpu_buffer_rsrc_t bd[kMaxDst];
+      __amdgpu_buffer_rsrc_t bd[ND];
 #pragma unroll
-      for (int dd = 0; dd < kMaxDst; ++dd) {
+      for (int dd = 0; dd < ND; ++dd) {
         if (dd >= nd) continue;
         const uint64_t es = (dm >> dd) & 1 ? sizeof(W) : sizeof(T);
         bd[dd] = rsrc_of(d[dd] + sg0 * span * es, lim * es);
@@ -857,7 +857,7 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
         float acc[G];
         compute_group(raw[u], acc);
 #pragma unroll
-        for (int dd = 0; dd < kMaxDst; ++dd) {
+        for (int dd = 0; dd < ND; ++dd) {
           if (dd >= nd) continue;
           uint4 y[VM];
           encode_dst(dd, raw[u], acc, y);
@@ -940,7 +940,7 @@ __device__ FX_INLINE void xfer_mx(const char* const (&s)[kMaxSrc], char* const (
     acc *= scale;
     if (FP8 && dm) acc = wround<W>(acc);
 #pragma unroll
-    for (int dd = 0; dd < kMaxDst; ++dd) {
+    for (int dd = 0; dd < ND; ++dd) {
       if (dd >= nd) continue;
       if ((dm >> dd) & 1) st_elem<PM, W>(d[dd], i, Elem<W>::store((typename Elem<W>::acc)acc));
       else st_elem<PM, T>(d[dd], i, Elem<T>::store((typename Elem<T>::acc)(FP8 ? acc * post_inv : acc)));
@@ -1320,6 +1320,11 @@ __device__ FX_INLINE void xfer_mxb(const char* const (&s)[kMaxSrc], const uint8_
   for (uint64_t i = ng * G + threadIdx.x; i < n; i += nt) mx_elem<T, W, K, SP, PM>(s, ss, d, sd, nd, dm, n, scale, i);
 }
 
+// fp8 / MX wire transfers instantiate for at most 2 destinations (xfer_mx_k, xfer_mxb_k); 0 = the A/B build with the
+// general (kMaxDst) form
+#ifndef FLEXAR_MX_ND2
+#define FLEXAR_MX_ND2 1
+#endif
 // The (K, pattern) combinations the planner emits (validate_typed_patterns): fp8 wire = quantising push
 // (K 1, SP_T), reduction (K >= 2, SP_TW), dequantising all-gather (K 1, SP_W); fp32 partials = tree
 // stage 0 (SP_T), ring step (K 2, SP_TW), final stage / temp chains (SP_W). Anything else is reported
@@ -1328,16 +1333,20 @@ template <typename T, typename W, int K, int PM>
 __device__ FX_INLINE bool xfer_mx_k(int sp, const char* const (&s)[kMaxSrc], char* const (&d)[kMaxDst], int nd,
                                     uint32_t dm, uint64_t n, float scale, float pre, float post_inv, bool vec) {
   constexpr bool FP8 = sizeof(W) == 1;
+  // fp8 wires write at most 2 destinations (they always pull: planner.hpp typed_pattern_ok), the same register
+  // saving as the MX wire's (xfer_mxb_k); fp32 partials keep the general form (push all-gathers multicast)
+  constexpr int ND = FP8 && FLEXAR_MX_ND2 ? 2 : kMaxDst;
+  if (nd > ND) return false;
   if (sp == SP_T && (FP8 ? K == 1 : K >= 2)) {
-    if constexpr (FP8 ? K == 1 : K >= 2) xfer_mx<T, W, K, SP_T, PM>(s, d, nd, dm, n, scale, pre, post_inv, vec);
+    if constexpr (FP8 ? K == 1 : K >= 2) xfer_mx<T, W, K, SP_T, PM, ND>(s, d, nd, dm, n, scale, pre, post_inv, vec);
     return true;
   }
   if (sp == SP_TW && K >= 2 && (FP8 || K == 2)) {
-    if constexpr (K >= 2 && (FP8 || K == 2)) xfer_mx<T, W, K, SP_TW, PM>(s, d, nd, dm, n, scale, pre, post_inv, vec);
+    if constexpr (K >= 2 && (FP8 || K == 2)) xfer_mx<T, W, K, SP_TW, PM, ND>(s, d, nd, dm, n, scale, pre, post_inv, vec);
     return true;
   }
   if (sp == SP_W && (FP8 ? K == 1 : K >= 2)) {
-    if constexpr (FP8 ? K == 1 : K >= 2) xfer_mx<T, W, K, SP_W, PM>(s, d, nd, dm, n, scale, pre, post_inv, vec);
+    if constexpr (FP8 ? K == 1 : K >= 2) xfer_mx<T, W, K, SP_W, PM, ND>(s, d, nd, dm, n, scale, pre, post_inv, vec);
     return true;
   }
   return false;
@@ -1345,42 +1354,22 @@ __device__ FX_INLINE bool xfer_mx_k(int sp, const char* const (&s)[kMaxSrc], cha
 
 // MX wire patterns (validate: typed_pattern_ok): quantising push (K 1, SP_T), reduction (K >= 2, SP_TW),
 // dequantising all-gather (K 1, SP_W, dtype destinations only).
-#ifndef FLEXAR_MX_ND2
-#define FLEXAR_MX_ND2 1
-#endif
 template <typename T, typename W, int K, int PM>
 __device__ FX_INLINE bool xfer_mxb_k(int sp, const char* const (&s)[kMaxSrc], const uint8_t* const (&ss)[kMaxSrc],
                                      char* const (&d)[kMaxDst], uint8_t* const (&sd)[kMaxDst], int nd, uint32_t dm,
                                      uint64_t n, float scale, bool vec) {
-  // An instantiation for at most 2 destinations (own output + the published wire block) keeps 6 fewer destination
-  // pointers / buffer descriptors live: those spilled SGPRs into VGPR lanes and, at fan-in 8, VGPRs to scratch
-  // (profiles/r6_mx_nd/). K = 1 copies with more destinations take the general one. FLEXAR_MX_ND2=0: the A/B
-  // build without it
-  const bool nd2 = FLEXAR_MX_ND2 && nd <= 2;
+  // MX ops write at most 2 destinations (planner.hpp typed_pattern_ok; fp8 wires always pull): an instantiation for
+  // 2 keeps 6 destination pointers, 6 scale pointers and their buffer descriptors out of the registers. The general
+  // one (up to kMaxDst) set the fan-in-8 kernel's allocation to 256 VGPRs plus scratch spills (profiles/r6_mx_nd/).
+  // FLEXAR_MX_ND2=0: the A/B build with the general instantiation.
+  constexpr int ND = FLEXAR_MX_ND2 ? 2 : kMaxDst;
+  if (nd > ND) return false;
   if constexpr (K == 1) {
-    if (sp == SP_T) {
-      if (nd2) xfer_mxb<T, W, 1, SP_T, PM, 2>(s, ss, d, sd, nd, dm, n, scale, vec);
-      else xfer_mxb<T, W, 1, SP_T, PM>(s, ss, d, sd, nd, dm, n, scale, vec);
-      return true;
-    }
-    if (sp == SP_W && dm == 0) {
-      if (nd2) xfer_mxb<T, W, 1, SP_W, PM, 2>(s, ss, d, sd, nd, dm, n, scale, vec);
-      else xfer_mxb<T, W, 1, SP_W, PM>(s, ss, d, sd, nd, dm, n, scale, vec);
-      return true;
-    }
+    if (sp == SP_T) { xfer_mxb<T, W, 1, SP_T, PM, ND>(s, ss, d, sd, nd, dm, n, scale, vec); return true; }
+    if (sp == SP_W && dm == 0) { xfer_mxb<T, W, 1, SP_W, PM, ND>(s, ss, d, sd, nd, dm, n, scale, vec); return true; }
     return false;
   } else {
-    if (sp == SP_TW) {
-      // at most 2 destinations (planner.hpp typed_pattern_ok: fp8 wires always pull): one instantiation. The
-      // general one (up to kMaxDst) at fan-in 8 set the whole kernel's allocation to 256 VGPRs plus scratch
-      if constexpr (FLEXAR_MX_ND2) {
-        if (nd > 2) return false;
-        xfer_mxb<T, W, K, SP_TW, PM, 2>(s, ss, d, sd, nd, dm, n, scale, vec);
-      } else {
-        xfer_mxb<T, W, K, SP_TW, PM>(s, ss, d, sd, nd, dm, n, scale, vec);
-      }
-      return true;
-    }
+    if (sp == SP_TW) { xfer_mxb<T, W, K, SP_TW, PM, ND>(s, ss, d, sd, nd, dm, n, scale, vec); return true; }
     return false;
   }
 }
@@ -1800,15 +1789,24 @@ constexpr int typed_min_waves() {
   if (kTypedThreads == 256) return KMAX <= 4 ? 3 : 2;
   return FLEXAR_TYPED_OCC3 && KMAX <= 4 && sizeof(W) == 1 && !IsMx<W>::value ? 3 : 1;
 }
+// 512-thread typed executors stay one workgroup per CU, as every executor was sized and measured: a kernel that
+// comes in at <= 128 VGPRs (bf16 over the MX wire, fan-in <= 4, after the 2-destination change) would otherwise
+// fit two per CU, and the grid then packs onto half the CUs - measured 33 % slower with 4 processes sharing the
+// GPU (profiles/r6_mx_nd/). Claiming v128 keeps the allocation above 128.
+__device__ FX_INLINE void one_workgroup_per_cu() {
+  if constexpr (kTypedThreads == 512) asm volatile("" ::: "v128");
+}
 template <typename T, typename W, int PM, int KMAX = kMaxSrc>
 __global__ void __launch_bounds__(kTypedThreads) __attribute__((amdgpu_waves_per_eu(typed_min_waves<W, KMAX>())))
 exec_mx_kernel(DevCtx c) {
   (void)c;
+  one_workgroup_per_cu();
   exec_body<T, OpSum, PM, W, KMAX>(kernarg_ctx(), blockIdx.x, gridDim.x);
 }
 template <typename T, typename W, int PM, int KMAX = kMaxSrc>
 __global__ void __launch_bounds__(kTypedThreads) __attribute__((amdgpu_waves_per_eu(typed_min_waves<W, KMAX>())))
 exec_mx_group_kernel(const DevCtx* ctxs, uint32_t grid_per_rank) {
+  one_workgroup_per_cu();
   const uint32_t r = blockIdx.x / grid_per_rank;
   exec_body<T, OpSum, PM, W, KMAX>(ctxs[r], blockIdx.x % grid_per_rank, grid_per_rank);
 }
