@@ -132,6 +132,29 @@ int main() {
     P.ops[x].kind = 9;
     EXPECT(!ok(P, N, r, count, count), "op kind");
   }
+  {
+    // fp8 / MX wires: every planner program validates, and an op with a third destination is rejected (the
+    // executor instantiates those transfers for 2 destinations only: device_exec.hpp xfer_mx_k / xfer_mxb_k)
+    for (const char* sp : {"flat+mxe4m3", "flat+e4m3", "flat+mxe5m2"})
+      for (uint32_t n : {2u, 4u, 8u})
+        for (uint32_t rr = 0; rr < n; ++rr) {
+          Program P = plan(sp, n, rr, 1u << 16);
+          EXPECT(ok(P, n, rr, 1u << 16, 1u << 16), (std::string("valid ") + sp).c_str());
+          ++checked;
+        }
+    Program P = plan("flat+mxe4m3", N, r, count);
+    int red = -1;
+    for (size_t i = 0; i < P.ops.size(); ++i)
+      if (P.ops[i].kind == OP_XFER && P.ops[i].nsrc >= 2 && P.ops[i].ndst == 2) red = (int)i;
+    EXPECT(red >= 0, "MX reduction with 2 destinations");
+    if (red >= 0) {
+      Op& o = P.ops[red];
+      o.dst[2] = o.dst[1];  // a third (wire) destination, masks kept consistent
+      o.ndst = 3;
+      o.pad16[1] |= (uint16_t)(((o.pad16[1] >> 1) & 1u) << 2);
+      EXPECT(!ok(P, N, r, count, count), "MX op with 3 destinations");
+    }
+  }
   std::printf("%d programs validated, %d failures\n", checked, failures);
   return failures ? 1 : 0;
 }
