@@ -133,6 +133,7 @@ def _sig(lib):
         "flexar_select_plan_ex": (i, [i, d, i, i, i, cp, sz]),
         "flexar_apply_partials": (i, [cp, i, d, i, i, cp, sz]),
         "flexar_kernel_info": (i, [i, i, i, i, c.POINTER(i), c.POINTER(i)]),
+        "flexar_kernel_info_ex": (i, [i, i, i, i, c.POINTER(i), c.POINTER(i), c.POINTER(i)]),
         "flexar_downgrade_spec": (i, [cp, i, u32, i, cp, sz]),
         "flexar_direct_links": (i, [c.POINTER(c.c_int32), c.POINTER(c.c_int32), i, i]),
         "flexar_probe_blob_size": (sz, []),
@@ -468,11 +469,12 @@ def direct_links(classes, hops, self_rank: int) -> int:
 def kernel_info(dtype="float32", op="sum", kind: int = 0, proto: int = 0) -> dict:
     """Occupancy (512-thread workgroups per CU) and VGPRs of one kernel instantiation (needs a GPU).
     kind: 0 executor (proto 0 fence / 1 nts / 2 wt), 1 LL, 2 reduce, 3/4/5 typed executor (fp32 partials /
-    e4m3 wire / e5m2 wire), 6/7 typed executor with the OCP MX e4m3 / e5m2 wire (the fan-in-8 class)."""
-    occ, regs = ctypes.c_int(0), ctypes.c_int(0)
-    check(lib().flexar_kernel_info(dtype_code(dtype), op_code(op), kind, proto, ctypes.byref(occ), ctypes.byref(regs)),
-          "kernel_info")
-    return {"blocks_per_cu": occ.value, "vgprs": regs.value}
+    e4m3 wire / e5m2 wire), 6/7 typed executor with the OCP MX e4m3 / e5m2 wire (the fan-in-8 class).
+    ``scratch_bytes``: the private segment per lane (spills, stack objects)."""
+    occ, regs, scr = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+    check(lib().flexar_kernel_info_ex(dtype_code(dtype), op_code(op), kind, proto, ctypes.byref(occ), ctypes.byref(regs),
+                                      ctypes.byref(scr)), "kernel_info")
+    return {"blocks_per_cu": occ.value, "vgprs": regs.value, "scratch_bytes": scr.value}
 
 
 def _ptr_array(ptrs):

@@ -309,8 +309,10 @@ void flexar_device_free(void* p);
 /* Kernel facts for a (dtype, op) instantiation: kind 0 = executor (proto 0 fence, 1 +nts, 2 +wt),
  * 1 = LL, 2 = standalone reduce, 3/4/5 = typed executor with fp32 partials / e4m3 wire / e5m2 wire,
  * 6/7 = typed executor with an OCP MX block-scaled e4m3 / e5m2 wire.
- * Writes workgroups resident per CU (512 threads) and VGPRs. */
+ * Writes workgroups resident per CU (512 threads) and VGPRs; the _ex form also the scratch (private segment)
+ * bytes per lane. */
 int flexar_kernel_info(int dtype, int op, int kind, int proto, int* blocks_per_cu, int* vgprs);
+int flexar_kernel_info_ex(int dtype, int op, int kind, int proto, int* blocks_per_cu, int* vgprs, int* scratch_bytes);
 
 /* ---- fault attribution (crumbs.hpp) ------------------------------------------ */
 /* Every launch, copy, RCCL group and phase is appended to a per-process ring of breadcrumbs; on a fatal

@@ -890,6 +890,10 @@ void* flexar_device_alloc(size_t bytes) {
 void flexar_device_free(void* p) { (void)hipFree(p); }
 
 int flexar_kernel_info(int dtype, int op, int kind, int proto, int* blocks_per_cu, int* vgprs) {
+  return flexar_kernel_info_ex(dtype, op, kind, proto, blocks_per_cu, vgprs, nullptr);
+}
+
+int flexar_kernel_info_ex(int dtype, int op, int kind, int proto, int* blocks_per_cu, int* vgprs, int* scratch_bytes) {
   if (kind < 0 || kind > 7 || proto < 0 || proto > 2) { set_error("bad kernel_info arguments"); return FLEXAR_ERR_INVALID; }
   LaunchArgs la;
   la.kind = LAUNCH_QUERY;
@@ -899,6 +903,7 @@ int flexar_kernel_info(int dtype, int op, int kind, int proto, int* blocks_per_c
   la.proto = proto;
   la.occ_out = blocks_per_cu;
   la.regs_out = vgprs;
+  la.scratch_out = scratch_bytes;
   return launch_dtype(dtype, op, la);
 }
 

@@ -21,9 +21,11 @@ inline int query_kernel(K kern, const LaunchArgs& a, int threads = kExecThreads)
   if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kern)) != hipSuccess) {
     (void)hipGetLastError();
     fa.numRegs = 0;
+    fa.localSizeBytes = 0;
   }
   if (a.occ_out) *a.occ_out = occ;
   if (a.regs_out) *a.regs_out = fa.numRegs;
+  if (a.scratch_out) *a.scratch_out = (int)fa.localSizeBytes;
   return 0;
 }
 

@@ -32,6 +32,7 @@ struct LaunchArgs {
   int query = 0;         // QUERY: which kernel
   int* occ_out = nullptr;
   int* regs_out = nullptr;
+  int* scratch_out = nullptr;  // private segment bytes per lane
   int max_fanin = 0;     // typed programs: the widest XFER fan-in (Program::max_nsrc; 0 = unknown, widest kernel)
   int wire = 0;          // EXEC / GROUP / QUERY of a typed program (Program::wire): 1 fp32, 2 e4m3, 3 e5m2,
                          // 4 / 5 MX e4m3 / e5m2

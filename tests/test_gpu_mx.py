@@ -105,6 +105,24 @@ def test_kernel_info_reports_every_executor_class(cuda):
             assert k["blocks_per_cu"] >= 1 and 0 < k["vgprs"] <= 256, (dt, kind, proto, k)
 
 
+def test_production_executors_scratch_free_one_workgroup_per_cu(cuda):
+    """Round 6 (profiles/r6_mx_nd/): every production executor runs without scratch, and at one 512-thread workgroup
+    per CU. Covered: the untyped executor in every protocol, LL, fp32 partials, the global-scale fp8 wire and the
+    fan-in-8 MX wire. Scratch had come from two sources: the fan-in-8 MX spills, and copying the by-value context.
+    A kernel at <= 128 VGPRs would pack two workgroups per CU."""
+    from allreduce_over_mpi_amd import _native as nv
+
+    cases = [(dt, 0, p) for dt in ("float32", "bfloat16") for p in (0, 1, 2)]
+    cases += [(dt, 1, 0) for dt in ("float32", "bfloat16")]
+    cases += [("bfloat16", 3, p) for p in (0, 2)]
+    cases += [(dt, k, p) for dt in ("float32", "bfloat16") for k in (4, 5, 6, 7) for p in (0, 2)]
+    for dt, kind, proto in cases:
+        k = nv.kernel_info(dt, "sum", kind, proto)
+        assert k["scratch_bytes"] == 0, (dt, kind, proto, k)
+        if kind != 1:
+            assert k["blocks_per_cu"] == 1, (dt, kind, proto, k)
+
+
 def test_default_spec_wire_applies_only_where_it_can(cuda, monkeypatch):
     """FLEXAR_ALGO=flat+mxe4m3 as the communicator default: float SUM / AVG allreduces and reduce-scatters take
     the MX wire; integer / MAX allreduces and the all-gather run untyped instead of failing."""
