@@ -309,7 +309,14 @@ __device__ FX_INLINE void xfer_k(const char* const (&s)[kMaxSrc], char* const (&
 #ifndef FLEXAR_UNROLL_WIDE
 #define FLEXAR_UNROLL_WIDE 2
 #endif
-  constexpr int U = (K <= 2) ? 4 : ((K <= 4) ? 2 : FLEXAR_UNROLL_WIDE);  // 16-B loads in flight per lane
+  // 8-bit PROD / MAX / MIN (16 lanes of byte arithmetic per vector) spill at the unroll above in the write-through
+  // and group kernels; FLEXAR_BYTE_OP_U1=1 is the A/B build with one group per lane for them (docs/ROUND6.md)
+#ifndef FLEXAR_BYTE_OP_U1
+#define FLEXAR_BYTE_OP_U1 0
+#endif
+  constexpr bool BYTE_OP = FLEXAR_BYTE_OP_U1 && sizeof(T) == 1 &&
+                           (std::is_same<OP, OpProd>::value || std::is_same<OP, OpMax>::value || std::is_same<OP, OpMin>::value);
+  constexpr int U = BYTE_OP ? 1 : (K <= 2) ? 4 : ((K <= 4) ? 2 : FLEXAR_UNROLL_WIDE);  // 16-B loads in flight per lane
   constexpr bool WT = PM == PM_WT;
   constexpr bool NTS = PM == PM_FENCE_NTS;
   const bool sc = Elem<T>::is_float && scale != 1.0f;
